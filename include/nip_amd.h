@@ -1,0 +1,162 @@
+/*
+ * nip_amd.h -- C-ABI of the MI355X-native NIP forward-backward engine.
+ *
+ * Plain C types only (pointers and sizes); no torch or HIP types appear in the
+ * signatures.  Device pointers are HIP device allocations; `stream` is a
+ * hipStream_t passed as void* (NULL = default stream).
+ *
+ * Each entry point names the reference interface it replaces (paths relative
+ * to the reference tree, manuelschmidt/nip @ v0).  Error codes follow the
+ * reference's convention: 0 = NIP_NO_ERROR (src/niperrorhandler.h:32), else a
+ * NIP_ERROR_* code.  The reference USES those codes (~200 call sites in nip.c,
+ * nipparsers.c, huginnet.y, util/) but never defines them; the values below
+ * are the only ones the project ever had (nip-2010-10-27.tar.gz,
+ * errorhandler.h:5-13).  NIP_ERROR_BAD_LUCK is distinct and non-zero as
+ * util/niptrain.c:153,189 requires.
+ */
+#ifndef NIP_AMD_H
+#define NIP_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef NIP_NO_ERROR
+#define NIP_NO_ERROR               0
+#endif
+#define NIP_ERROR_NULLPOINTER      1
+#define NIP_ERROR_DIVBYZERO        2
+#define NIP_ERROR_INVALID_ARGUMENT 3
+#define NIP_ERROR_OUTOFMEMORY      4
+#define NIP_ERROR_IO               5
+#define NIP_ERROR_GENERAL          6
+#define NIP_ERROR_FILENOTFOUND     7
+#define NIP_ERROR_BAD_LUCK         8
+/* engine-specific: the compiled slice has no GPU execution plan yet */
+#define NIPAMD_ERROR_UNSUPPORTED   100
+/* engine-specific: no usable gfx950 device / HIP runtime failure */
+#define NIPAMD_ERROR_DEVICE        101
+
+/* Per-sequence status bits written by the batched entry points. */
+#define NIPAMD_STATUS_ZERO_MASS    1u  /* some m2 == 0: ll = -DBL_MAX (src/nip.c:1471-1473) */
+#define NIPAMD_STATUS_BAD_LUCK     2u  /* e_step's m1<=0 || m2<=0 || ll>0 (src/nip.c:1827-1854) */
+
+typedef struct nipamd_model nipamd_model;
+
+/* ------------------------------------------------------------------ */
+/* Model construction (host)                                            */
+/* ------------------------------------------------------------------ */
+
+/*
+ * Build a model from a Bayes-net spec given in Hugin-file order.
+ * Replaces parse_model() (src/nip.c:122-294) together with the grammar
+ * actions it drives (src/huginnet.y:202-236, 321-387, 582-780, 1058-1254) and
+ * the join-tree compiler nip_graph_to_cliques() (src/nipgraph.c:518-544).
+ * Variable IDs, clique order, clique dimension order, sepsets, family
+ * cliques/mappings and the parsed-CPT normalisation (huginnet.y:635-636) are
+ * reproduced bit-exactly.
+ *
+ *   n_nodes            nodes in declaration order
+ *   symbols[n]         node symbols (may be NULL)
+ *   card[n]            number of states
+ *   next[n]            index of the NIP_next node, or -1
+ *   n_pots             potential declarations in file order
+ *   pot_child[p]       child node index
+ *   pot_nparents[p]    number of parents
+ *   pot_parents        concatenated parent indices, FILE order
+ *   pot_ndata[p]       number of data values (0 = "data" omitted)
+ *   pot_data           concatenated data in textual order
+ */
+int nipamd_model_from_spec(int n_nodes, const char* const* symbols,
+                           const int* card, const int* next, int n_pots,
+                           const int* pot_child, const int* pot_nparents,
+                           const int* pot_parents, const int* pot_ndata,
+                           const double* pot_data, nipamd_model** out);
+
+/* Same, reading a Hugin .net file (replaces parse_model(char*), src/nip.c:122). */
+int nipamd_model_from_net(const char* path, nipamd_model** out);
+
+/* Replaces free_model() (src/nip.c:485-508). */
+void nipamd_model_free(nipamd_model* m);
+
+/* Number of variables / index of a symbol (replaces model_variable(),
+ * src/nip.c:1584-1597). */
+int nipamd_model_num_vars(const nipamd_model* m);
+int nipamd_model_var_index(const nipamd_model* m, const char* symbol);
+int nipamd_model_var_card(const nipamd_model* m, int v);
+
+/*
+ * Index contract: JSON description of the compiled join
+ * tree -- variables (cards, interface flags, parents, priors, family clique and
+ * mapping), cliques (dimension order, sepset link order, original tables),
+ * sepsets, in/out cliques and interface lists.  Returns the JSON length
+ * (excluding the terminator); writes at most cap bytes.
+ */
+int nipamd_model_desc_json(const nipamd_model* m, char* buf, int cap);
+
+/* Size of the em_learn parameter layout (src/nip.c:2101-2128): for every
+ * variable, a table with the child as dimension 0, then v->parents order. */
+int nipamd_model_param_size(const nipamd_model* m);
+
+/* 1 if the model has a GPU execution plan (SURVEY 8(d) config 2 family). */
+int nipamd_model_gpu_supported(const nipamd_model* m, int n_obs,
+                               const int* obs_vars, int n_query,
+                               const int* query_vars);
+
+/* ------------------------------------------------------------------ */
+/* Hot path (device)                                                    */
+/* ------------------------------------------------------------------ */
+
+/*
+ * Batched forward_backward_inference() (src/nip.c:1320-1581) for B
+ * independent sequences of equal length T, inputs and outputs resident in
+ * HBM, asynchronous on `stream`.
+ *
+ *   d_obs     int32 [B][T][n_obs]; state index, <0 = missing (nip.c:994)
+ *   obs_vars  host int[n_obs]: model variable of each column (ts->observed)
+ *   query     host int[n_query]: variables of interest (vars[] of the API)
+ *   d_post    double [B][T][sum card(query)]  -- uncertain_series->data
+ *   d_ll      double [B] log-likelihood SUM over t as the reference returns
+ *             it (nip.c:1466; the header's "average", nip.h:393, is wrong),
+ *             or NULL
+ *   d_status  uint32 [B] NIPAMD_STATUS_* bits, or NULL
+ */
+int nipamd_fb(nipamd_model* m, const int32_t* d_obs, int n_obs,
+              const int* obs_vars, int B, int T, int n_query,
+              const int* query, double* d_post, double* d_ll,
+              uint32_t* d_status, void* stream);
+
+/* Host-buffer convenience wrapper around nipamd_fb (copies in and out and
+ * synchronises); the PCIe-inclusive path. */
+int nipamd_fb_host(nipamd_model* m, const int32_t* obs, int n_obs,
+                   const int* obs_vars, int B, int T, int n_query,
+                   const int* query, double* post, double* ll,
+                   uint32_t* status);
+
+/*
+ * Batched e_step() (src/nip.c:1708-2007): expected counts of B sequences
+ * summed into d_counts (double [param_size], em_learn layout, caller
+ * initialised -- em_learn starts from 1.0, nip.c:2172).  Summation over the
+ * batch is deterministic (fixed order).  d_ll [B] and d_status [B] optional.
+ */
+int nipamd_estep(nipamd_model* m, const int32_t* d_obs, int n_obs,
+                 const int* obs_vars, int B, int T, double* d_counts,
+                 double* d_ll, uint32_t* d_status, void* stream);
+
+/* m_step() (src/nip.c:2010-2071): normalise params (host, em_learn layout)
+ * and re-initialise the model's tables and priors from them. */
+int nipamd_m_step(nipamd_model* m, const double* params);
+
+/* Current clique original table / prior of an independent variable. */
+int nipamd_model_original(const nipamd_model* m, int clique, double* out, int cap);
+int nipamd_model_prior(const nipamd_model* m, int v, double* out);
+
+/* Last error message (thread-local), for diagnostics. */
+const char* nipamd_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NIP_AMD_H */

@@ -1,0 +1,249 @@
+"""nip_amd -- MI355X-native forward-backward join-tree engine for NIP's DBNs.
+
+Python mirror of the reference's top-level interface for this path
+(src/nip.h): ``parse_model`` / ``model_variable`` / ``forward_backward_inference``
+/ ``em_learn``-pieces, batched over sequences and backed by the gfx950 C-ABI
+library ``_lib/libnip_amd.so`` (include/nip_amd.h).  The library is loaded
+through ctypes with plain pointers; torch is only used by callers for device
+memory and streams.  There is no CPU fallback: if the library or a GPU is
+missing, calls raise ``NipError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+
+import numpy as np
+
+from . import build as _build
+
+__all__ = ["NipError", "Model", "parse_model", "lib", "forward_backward_inference",
+           "forward_backward_inference_host", "LIB_PATH"]
+
+LIB_PATH = _build.LIB
+
+NIP_NO_ERROR = 0
+NIP_ERROR_NULLPOINTER = 1
+NIP_ERROR_DIVBYZERO = 2
+NIP_ERROR_INVALID_ARGUMENT = 3
+NIP_ERROR_OUTOFMEMORY = 4
+NIP_ERROR_IO = 5
+NIP_ERROR_GENERAL = 6
+NIP_ERROR_FILENOTFOUND = 7
+NIP_ERROR_BAD_LUCK = 8
+NIPAMD_ERROR_UNSUPPORTED = 100
+NIPAMD_ERROR_DEVICE = 101
+STATUS_ZERO_MASS = 1
+STATUS_BAD_LUCK = 2
+
+# every entry point declared in include/nip_amd.h
+EXPORTS = [
+    "nipamd_model_from_spec", "nipamd_model_from_net", "nipamd_model_free",
+    "nipamd_model_num_vars", "nipamd_model_var_index", "nipamd_model_var_card",
+    "nipamd_model_desc_json", "nipamd_model_param_size", "nipamd_model_gpu_supported",
+    "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
+    "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
+]
+
+
+class NipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("nip_amd error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load the gfx950 C-ABI library (raises if it was never built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NipError(NIPAMD_ERROR_DEVICE,
+                           "native library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        vp, ip, dp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)
+        L.nipamd_model_from_spec.argtypes = [C.c_int, C.POINTER(C.c_char_p), ip, ip, C.c_int,
+                                             ip, ip, ip, ip, dp, C.POINTER(vp)]
+        L.nipamd_model_from_net.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.nipamd_model_free.argtypes = [vp]
+        L.nipamd_model_free.restype = None
+        L.nipamd_model_num_vars.argtypes = [vp]
+        L.nipamd_model_var_index.argtypes = [vp, C.c_char_p]
+        L.nipamd_model_var_card.argtypes = [vp, C.c_int]
+        L.nipamd_model_desc_json.argtypes = [vp, C.c_char_p, C.c_int]
+        L.nipamd_model_param_size.argtypes = [vp]
+        L.nipamd_model_gpu_supported.argtypes = [vp, C.c_int, ip, C.c_int, ip]
+        L.nipamd_fb.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, ip,
+                                vp, vp, vp, vp]
+        L.nipamd_fb_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, ip,
+                                     vp, vp, vp]
+        L.nipamd_estep.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
+        L.nipamd_m_step.argtypes = [vp, dp]
+        L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
+        L.nipamd_model_prior.argtypes = [vp, C.c_int, dp]
+        L.nipamd_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise NipError(rc, lib().nipamd_last_error().decode())
+
+
+def _ints(xs):
+    a = (C.c_int * max(len(xs), 1))()
+    for i, x in enumerate(xs):
+        a[i] = int(x)
+    return a
+
+
+class Model:
+    """A compiled DBN time slice (the reference's nip_model, src/nip.h:71-104)."""
+
+    def __init__(self, handle):
+        self._h = C.c_void_p(handle)
+        self._desc = None
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().nipamd_model_free(self._h)
+        except Exception:
+            pass
+
+    # -- construction ---------------------------------------------------
+    @classmethod
+    def from_net(cls, path: str) -> "Model":
+        h = C.c_void_p()
+        _check(lib().nipamd_model_from_net(path.encode(), C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_spec(cls, nodes, potentials) -> "Model":
+        """nodes: [(symbol, card, next_symbol_or_None)] in declaration order;
+        potentials: [(child, [parents in file order], data_or_None)]."""
+        syms = [n[0] for n in nodes]
+        idx = {s: i for i, s in enumerate(syms)}
+        card = [int(n[1]) for n in nodes]
+        nxt = [idx[n[2]] if n[2] else -1 for n in nodes]
+        child, npar, par, nd, data = [], [], [], [], []
+        for ch, ps, d in potentials:
+            child.append(idx[ch]); npar.append(len(ps)); par += [idx[p] for p in ps]
+            d = [] if d is None else list(np.asarray(d, np.float64).ravel())
+            nd.append(len(d)); data += d
+        csyms = (C.c_char_p * len(syms))(*[s.encode() for s in syms])
+        dbuf = (C.c_double * max(len(data), 1))(*data)
+        h = C.c_void_p()
+        _check(lib().nipamd_model_from_spec(len(syms), csyms, _ints(card), _ints(nxt), len(child),
+                                            _ints(child), _ints(npar), _ints(par), _ints(nd),
+                                            dbuf, C.byref(h)))
+        return cls(h.value)
+
+    # -- introspection (the index contract) -----------------------------
+    def desc(self) -> dict:
+        if self._desc is None:
+            n = lib().nipamd_model_desc_json(self._h, None, 0)
+            buf = C.create_string_buffer(n + 1)
+            lib().nipamd_model_desc_json(self._h, buf, n + 1)
+            self._desc = json.loads(buf.value.decode())
+        return self._desc
+
+    @property
+    def num_vars(self):
+        return lib().nipamd_model_num_vars(self._h)
+
+    def variable(self, symbol: str) -> int:
+        """model_variable() (src/nip.c:1584): index of a symbol, or -1."""
+        return lib().nipamd_model_var_index(self._h, symbol.encode())
+
+    def card(self, v: int) -> int:
+        return lib().nipamd_model_var_card(self._h, int(v))
+
+    def param_size(self) -> int:
+        return lib().nipamd_model_param_size(self._h)
+
+    def gpu_supported(self, obs_vars, query) -> bool:
+        return bool(lib().nipamd_model_gpu_supported(self._h, len(obs_vars), _ints(obs_vars),
+                                                     len(query), _ints(query)))
+
+    def original(self, c: int) -> np.ndarray:
+        n = lib().nipamd_model_original(self._h, c, None, 0)
+        out = np.zeros(n)
+        lib().nipamd_model_original(self._h, c, out.ctypes.data_as(C.POINTER(C.c_double)), n)
+        return out
+
+    def prior(self, v: int):
+        out = np.zeros(self.card(v))
+        n = lib().nipamd_model_prior(self._h, v, out.ctypes.data_as(C.POINTER(C.c_double)))
+        return out if n > 0 else None
+
+    def m_step(self, params) -> None:
+        """m_step() (src/nip.c:2010): params in the em_learn layout."""
+        p = np.ascontiguousarray(params, np.float64)
+        assert p.size == self.param_size()
+        _check(lib().nipamd_m_step(self._h, p.ctypes.data_as(C.POINTER(C.c_double))))
+        self._desc = None
+
+
+def parse_model(path: str) -> Model:
+    """parse_model() (src/nip.c:122): read a Hugin .net file."""
+    return Model.from_net(path)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+def forward_backward_inference(model: Model, obs, obs_vars, query, post=None, ll=None,
+                               status=None, stream=None):
+    """Batched forward_backward_inference() (src/nip.c:1320) on the GPU.
+
+    obs: torch int32 CUDA tensor [B, T, n_obs] (state index, <0 missing).
+    Returns (post [B, T, sum card(query)] float64, ll [B] float64, status [B] int32),
+    all CUDA tensors, computed asynchronously on ``stream`` (default: torch's
+    current stream).  ll is the SUM over t, as the reference returns it.
+    """
+    import torch
+    if obs.dim() == 2:
+        obs = obs.unsqueeze(-1)
+    assert obs.dtype == torch.int32 and obs.is_cuda and obs.is_contiguous()
+    B, T, nobs = obs.shape
+    assert nobs == len(obs_vars)
+    width = sum(model.card(v) for v in query)
+    dev = obs.device
+    if post is None:
+        post = torch.empty((B, T, width), dtype=torch.float64, device=dev)
+    if ll is None:
+        ll = torch.empty((B,), dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    _check(lib().nipamd_fb(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
+                           len(query), _ints(query), C.c_void_p(post.data_ptr()),
+                           C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()),
+                           _stream_ptr(stream)))
+    return post, ll, status
+
+
+def forward_backward_inference_host(model: Model, obs, obs_vars, query):
+    """Same, from host numpy buffers (PCIe-inclusive, synchronous)."""
+    obs = np.ascontiguousarray(np.asarray(obs, np.int32))
+    if obs.ndim == 2:
+        obs = obs[:, :, None]
+    B, T, nobs = obs.shape
+    width = sum(model.card(v) for v in query)
+    post = np.zeros((B, T, width))
+    ll = np.zeros(B)
+    status = np.zeros(B, np.uint32)
+    _check(lib().nipamd_fb_host(model._h, obs.ctypes.data_as(C.c_void_p), nobs, _ints(obs_vars),
+                                B, T, len(query), _ints(query), post.ctypes.data_as(C.c_void_p),
+                                ll.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
+    return post, ll, status

@@ -1,0 +1,35 @@
+"""Build the nip_amd C-ABI shared library for gfx950 (in-tree)."""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIB_DIR, "libnip_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("NIPAMD_ARCH", "gfx950")
+
+
+def sources():
+    csrc = os.path.join(PKG, "csrc")
+    return sorted(glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.hip")))
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cmd = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-result",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"),
+           *sources(), "-o", LIB]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

@@ -1,0 +1,626 @@
+// compile.cpp -- Bayes-net spec -> DBN time-slice join tree, host side.
+//
+// Re-derives, bit for bit, the structures the reference builds at parse time:
+//   * variable IDs = declaration order        (src/nipvariable.c:56-128)
+//   * parsed CPT reorder + normalisation      (src/nipjointree.c:341-480,
+//                                              src/huginnet.y:582-780)
+//   * interface flags                         (src/huginnet.y:1155-1254)
+//   * moralise / interface edges / triangulate / cliques / sepsets
+//                                             (src/nipgraph.c:300-612, 616-822,
+//                                              src/nipheap.c:42-298)
+//   * family cliques and mappings             (src/nipjointree.c:967-1064)
+//   * clique initialisation with the CPTs     (src/nipjointree.c:713-772)
+//   * model assembly, in/out cliques          (src/nip.c:147-264)
+// The heap, the cluster/sepset cost keys (including the sepset secondary key
+// that is always 0 because of `if(!s)`, nipgraph.c:656) and every tie-break are
+// reproduced, since the clique array order depends on them.
+#include "model.h"
+
+#include "nip_amd.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <sstream>
+
+namespace nipamd {
+namespace {
+
+// ------------------------------------------------------------------
+// Binary min-heap with the reference's (non-standard) update semantics.
+// ------------------------------------------------------------------
+struct HeapItem {
+  std::vector<int> content;   // cluster: [v, neighbours...]; sepset: {index}
+  int primary = 0, secondary = 0;
+};
+
+class RefHeap {
+ public:
+  using KeyFn = std::function<void(HeapItem&)>;
+  explicit RefHeap(KeyFn keys) : keys_(std::move(keys)) {}
+
+  void insert(std::vector<int> content) {
+    auto it = std::make_unique<HeapItem>();
+    it->content = std::move(content);
+    keys_(*it);
+    items_.push_back(std::move(it));
+    heapified_ = false;
+  }
+  // nip_build_min_heap (nipheap.c:167-190): full heapify unless already
+  // heapified, in which case only the updated indices are sifted DOWN.
+  void build() {
+    if (!heapified_) {
+      for (int i = parent(size() - 1); i >= 0; i--) heapify(i);
+    } else {
+      for (int idx : updated_) heapify(idx);
+    }
+    updated_.clear();
+    heapified_ = true;
+  }
+  // nip_heap_extract_min (nipheap.c:193-220)
+  bool extract(std::vector<int>& out) {
+    if (size() < 1) return false;
+    std::unique_ptr<HeapItem> mn = std::move(items_[0]);
+    items_[0] = std::move(items_[size() - 1]);
+    items_.pop_back();
+    if (size() > 0) heapify(0);
+    out = std::move(mn->content);
+    return true;
+  }
+  int search_first(int v) const {  // nip_search_heap_item with nip_family_cluster
+    for (int n = 0; n < size(); n++)
+      if (!items_[n]->content.empty() && items_[n]->content[0] == v) return n;
+    return -1;
+  }
+  const std::vector<int>& get(int i) const { return items_[i]->content; }
+  void set(int i, std::vector<int> c) {  // nip_set_heap_item (nipheap.c:152-164)
+    items_[i]->content = std::move(c);
+    keys_(*items_[i]);
+    updated_.push_back(i);
+  }
+  int size() const { return (int)items_.size(); }
+
+ private:
+  static int parent(int i) { return (i - 1) / 2; }
+  static bool less(const HeapItem* a, const HeapItem* b) {  // nipheap.c:247-258
+    if (a) {
+      if (b) return a->primary < b->primary ||
+                    (a->primary == b->primary && a->secondary < b->secondary);
+      return true;
+    }
+    return false;
+  }
+  void heapify(int i) {  // nip_min_heapify (nipheap.c:261-285)
+    for (;;) {
+      int l = 2 * i + 1, r = 2 * (i + 1), mn = i;
+      if (l < size() && less(items_[l].get(), items_[i].get())) mn = l;
+      if (r < size() && less(items_[r].get(), items_[mn].get())) mn = r;
+      if (mn == i) break;
+      std::swap(items_[mn], items_[i]);
+      i = mn;
+    }
+  }
+  KeyFn keys_;
+  std::vector<std::unique_ptr<HeapItem>> items_;
+  std::vector<int> updated_;
+  bool heapified_ = false;
+};
+
+bool is_parent(const std::vector<std::vector<int>>& parents, int p, int c) {
+  for (int q : parents[c]) if (q == p) return true;
+  return false;
+}
+
+// nip_variable_union(a, b) (nipvariable.c:446-502): a, then b's missing ones.
+std::vector<int> var_union(const std::vector<int>& a, const std::vector<int>& b) {
+  std::vector<int> c = a;
+  for (int x : b) if (std::find(c.begin(), c.end(), x) == c.end()) c.push_back(x);
+  return c;
+}
+
+// nip_variable_isect(a, b) (nipvariable.c:506-557): a's order.
+std::vector<int> var_isect(const std::vector<int>& a, const std::vector<int>& b) {
+  std::vector<int> c;
+  for (int x : a) if (std::find(b.begin(), b.end(), x) != b.end()) c.push_back(x);
+  return c;
+}
+
+struct Graph {
+  int n;
+  std::vector<int> adj;  // adj[i*n+j]
+  int& at(int i, int j) { return adj[(size_t)i * n + j]; }
+};
+
+// Triangulation + clique array (nipgraph.c:443-515, 389-440).  Returns the
+// clique variable lists (ascending index) in clique-array order.
+int triangulate(Graph& gu, const std::vector<int>& card,
+                const std::vector<std::vector<int>>& parents,
+                std::vector<std::vector<int>>& cliques, std::string& err) {
+  const int n = gu.n;
+  RefHeap h([&](HeapItem& it) {
+    const auto& vs = it.content;
+    int sum = 0;                         // nip_cluster_primary_cost (nipgraph.c:616-636)
+    for (size_t i = 0; i < vs.size(); i++)
+      for (size_t j = i + 1; j < vs.size(); j++) sum += !is_parent(parents, vs[i], vs[j]);
+    uint32_t prod = 1;                   // nip_cluster_secondary_cost (:638-644), int wrap
+    for (int v : vs) prod *= (uint32_t)card[v];
+    it.primary = sum;
+    it.secondary = (int)prod;
+  });
+  for (int i = 0; i < n; i++) {          // nip_build_cluster_heap (:670-713)
+    std::vector<int> cl{i};
+    for (int j = 0; j < n; j++) if (gu.at(i, j)) cl.push_back(j);
+    h.insert(std::move(cl));
+  }
+  h.build();
+
+  std::vector<std::vector<char>> sets;   // prepend-ordered list (front = newest)
+  for (int i = 0; i < n; i++) {
+    std::vector<int> cl;
+    if (!h.extract(cl)) { err = "cluster heap exhausted"; return -1; }
+    std::vector<char> vset(n, 0);
+    for (size_t j = 0; j < cl.size(); j++) {
+      vset[cl[j]] = 1;
+      for (size_t k = j + 1; k < cl.size(); k++) { gu.at(cl[j], cl[k]) = 1; gu.at(cl[k], cl[j]) = 1; }
+    }
+    // nip_update_cluster_heap (:725-778)
+    const int removed = cl[0];
+    for (size_t k = 1; k < cl.size(); k++) {
+      int idx = h.search_first(cl[k]);
+      if (idx < 0) { err = "neighbour cluster missing from heap (reference would assert)"; return -1; }
+      std::vector<int> u = var_union(h.get(idx), cl), nc;
+      for (int x : u) if (x != removed) nc.push_back(x);
+      h.set(idx, std::move(nc));
+    }
+    h.build();
+    // nip_int_array_list_contains_subset (niplists.c:598-619)
+    bool subset = false;
+    for (const auto& s : sets) {
+      bool ok = true;
+      for (int v = 0; v < n; v++) if (vset[v] && !s[v]) { ok = false; break; }
+      if (ok) { subset = true; break; }
+    }
+    if (!subset) sets.insert(sets.begin(), std::move(vset));
+  }
+  // nip_cluster_list_to_clique_array: list head fills the LAST slot.
+  const int nc = (int)sets.size();
+  cliques.assign(nc, {});
+  int counter = nc;
+  for (const auto& s : sets) {
+    std::vector<int> cv;
+    for (int v = 0; v < n; v++) if (s[v]) cv.push_back(v);
+    cliques[--counter] = cv;             // ids ascend with index: already sorted
+  }
+  return nc;
+}
+
+// nip_cliques_connected (nipjointree.c:546-577)
+bool connected(const std::vector<Clique>& cq, const std::vector<Sepset>& ss,
+               std::vector<char>& mark, int one, int two) {
+  mark[one] = 1;
+  if (one == two) return true;
+  for (int s : cq[one].links) {
+    if (!mark[ss[s].a]) { if (connected(cq, ss, mark, ss[s].a, two)) return true; }
+    else if (!mark[ss[s].b]) { if (connected(cq, ss, mark, ss[s].b, two)) return true; }
+  }
+  return false;
+}
+
+// nip_create_sepsets (nipgraph.c:547-612) with the sepset heap (:781-822).
+void create_sepsets(std::vector<Clique>& cq, std::vector<Sepset>& ss) {
+  const int nc = (int)cq.size();
+  std::vector<Sepset> cand;
+  for (int i = 0; i < nc - 1; i++)
+    for (int j = i + 1; j < nc; j++) {
+      Sepset s; s.a = i; s.b = j; s.vars = var_isect(cq[i].vars, cq[j].vars);
+      cand.push_back(std::move(s));
+    }
+  RefHeap h([&](HeapItem& it) {
+    it.primary = -(int)cand[it.content[0]].vars.size();  // nip_sepset_primary_cost
+    it.secondary = 0;                                    // :652-667, always 0
+  });
+  for (size_t k = 0; k < cand.size(); k++) h.insert({(int)k});
+  h.build();
+  std::vector<Sepset> confirmed;
+  int inserted = 0;
+  while (inserted < nc - 1) {
+    std::vector<int> item;
+    if (!h.extract(item)) break;
+    const Sepset& s = cand[item[0]];
+    std::vector<char> mark(nc, 0);
+    if (!connected(cq, confirmed, mark, s.a, s.b)) {
+      int id = (int)confirmed.size();
+      confirmed.push_back(s);
+      // nip_confirm_sepset (nipjointree.c:211-234): prepend to both lists
+      cq[s.a].links.insert(cq[s.a].links.begin(), id);
+      cq[s.b].links.insert(cq[s.b].links.begin(), id);
+      inserted++;
+    }
+  }
+  ss = std::move(confirmed);
+}
+
+// nip_find_clique (nipjointree.c:1043-1064)
+int find_clique(const std::vector<Clique>& cq, const std::vector<int>& vs) {
+  for (size_t i = 0; i < cq.size(); i++) {
+    size_t ok = 0;
+    for (int v : vs)
+      if (std::find(cq[i].vars.begin(), cq[i].vars.end(), v) != cq[i].vars.end()) ok++;
+    if (ok == vs.size()) return (int)i;
+  }
+  return -1;
+}
+
+void normalise_array(double* r, int n) {  // nippotential.c:349-359
+  double sum = 0;
+  for (int i = 0; i < n; i++) sum += r[i];
+  if (sum == 0) return;
+  for (int i = 0; i < n; i++) r[i] /= sum;
+}
+
+// Multiply probs (dims = `pvars`, ascending IDs) into a clique table through
+// the positions of pvars in the clique (nip_init_potential, nippotential.c:525-564).
+void init_into(const std::vector<int>& cvars, const std::vector<int>& card,
+               std::vector<double>& tgt, const std::vector<int>& pvars,
+               const std::vector<double>& probs, const std::vector<int>& map) {
+  const int cd = (int)cvars.size();
+  std::vector<int> idx(cd, 0);
+  for (size_t i = 0; i < tgt.size(); i++) {
+    int j = 0, stride = 1;
+    for (size_t k = 0; k < pvars.size(); k++) { j += idx[map[k]] * stride; stride *= card[pvars[k]]; }
+    tgt[i] *= probs[j];
+    for (int k = 0; k < cd; k++) { if (++idx[k] < card[cvars[k]]) break; idx[k] = 0; }
+  }
+}
+
+}  // namespace
+
+int compile_graph_only(int n, const std::vector<int>& card,
+                       const std::vector<std::pair<int, int>>& edges, bool set_parents,
+                       std::vector<std::vector<int>>& cliques_out, std::string& err) {
+  Graph g{n, std::vector<int>((size_t)n * n, 0)};
+  std::vector<std::vector<int>> parents(n);
+  for (auto& e : edges) {
+    g.at(e.first, e.second) = 1;
+    if (set_parents) parents[e.second].push_back(e.first);
+  }
+  Graph gm = g;  // nip_moralise_graph (nipgraph.c:325-351)
+  for (int v = 0; v < n; v++)
+    for (int i = 0; i < n; i++)
+      if (g.at(i, v))
+        for (int j = i + 1; j < n; j++) { gm.at(i, j) |= g.at(j, v); gm.at(j, i) |= g.at(j, v); }
+  Graph gu = gm;
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) gu.at(i, j) = gm.at(i, j) || gm.at(j, i);
+  return triangulate(gu, card, parents, cliques_out, err);
+}
+
+int compile_model(const NetSpec& spec, Model& m, std::string& err) {
+  const int n = (int)spec.card.size();
+  m = Model();
+  m.vars.resize(n);
+  for (int i = 0; i < n; i++) {
+    m.vars[i].symbol = i < (int)spec.symbols.size() ? spec.symbols[i] : ("V" + std::to_string(i));
+    m.vars[i].card = spec.card[i];
+    if (spec.card[i] <= 0) { err = "non-positive cardinality"; return NIP_ERROR_INVALID_ARGUMENT; }
+  }
+  auto& V = m.vars;
+
+  // --- potentialDeclaration actions (huginnet.y:582-780) ---
+  struct Parsed { int child; std::vector<int> parents; std::vector<int> ids; std::vector<double> data; };
+  std::vector<Parsed> parsed;
+  for (const auto& p : spec.pots) {
+    Parsed q;
+    q.child = p.child;
+    q.parents.assign(p.parents.rbegin(), p.parents.rend());  // prepend (:753-766)
+    std::vector<int> fam{p.child};
+    fam.insert(fam.end(), q.parents.begin(), q.parents.end());
+    // nip_create_potential (nipjointree.c:341-480): reorder to ascending ID
+    std::vector<int> sorted = fam;
+    std::sort(sorted.begin(), sorted.end());
+    size_t size = 1;
+    for (int v : fam) size *= (size_t)V[v].card;
+    q.ids = sorted;
+    q.data.assign(size, 1.0);
+    if (p.has_data) {
+      if (p.data.size() < size) { err = "not enough elements in potential"; return NIP_ERROR_INVALID_ARGUMENT; }
+      const int d = (int)fam.size();
+      std::vector<int> rank(d);
+      for (int j = 0; j < d; j++) rank[j] = (int)(std::find(sorted.begin(), sorted.end(), fam[j]) - sorted.begin());
+      std::vector<int> idx(d, 0);  // multi-index over sorted dims
+      for (size_t i = 0; i < size; i++) {
+        size_t src = 0, stride = 1;
+        for (int j = 0; j < d; j++) { src += (size_t)idx[rank[j]] * stride; stride *= (size_t)V[fam[j]].card; }
+        q.data[i] = p.data[src];
+        for (int k = 0; k < d; k++) { if (++idx[k] < V[sorted[k]].card) break; idx[k] = 0; }
+      }
+    }
+    if (!q.parents.empty()) {
+      // nip_normalise_cpd over dimension 0 = lowest ID of the family (:635-636)
+      const int c0 = V[sorted[0]].card;
+      for (size_t i = 0; i < size; i += c0) normalise_array(q.data.data() + i, c0);
+    } else if (p.has_data) {
+      normalise_array(q.data.data(), (int)size);           // :665-666
+    }
+    parsed.push_back(std::move(q));
+  }
+
+  // --- parsed_vars_to_graph (huginnet.y:1058-1103) ---
+  Graph g{n, std::vector<int>((size_t)n * n, 0)};
+  std::vector<std::vector<int>> parents(n);
+  for (const auto& q : parsed) {
+    for (int p : q.parents) g.at(p, q.child) = 1;
+    V[q.child].parents = q.parents;                        // nip_set_parents
+    parents[q.child] = q.parents;
+  }
+
+  // --- interface_to_vars (huginnet.y:1155-1254) ---
+  for (int i = 0; i < n; i++) {
+    int nx = spec.next[i];
+    if (nx >= 0) {
+      if (V[nx].card != V[i].card) { err = "invalid NIP_next: cardinalities differ"; return NIP_ERROR_GENERAL; }
+      V[i].next = nx; V[nx].previous = i;
+    }
+  }
+  for (int k = 0; k < n; k++) {
+    bool mm = false;
+    for (int p : V[k].parents)
+      if (V[p].next >= 0) {
+        V[p].ifs |= IF_OLD_OUTGOING; V[V[p].next].ifs |= IF_OUTGOING; V[k].ifs |= IF_INCOMING; mm = true;
+      }
+    if (mm)
+      for (int p : V[k].parents) if (V[p].next < 0) V[p].ifs |= IF_INCOMING;
+  }
+
+  // --- nip_graph_to_cliques (nipgraph.c:518-544) ---
+  Graph gm = g;
+  for (int v = 0; v < n; v++)
+    for (int i = 0; i < n; i++)
+      if (g.at(i, v))
+        for (int j = i + 1; j < n; j++) { gm.at(i, j) |= g.at(j, v); gm.at(j, i) |= g.at(j, v); }
+  Graph gi = gm;  // nip_add_interface_edges (:354-386)
+  for (int i = 0; i < n; i++)
+    for (int j = i + 1; j < n; j++)
+      if (((V[i].ifs & IF_OLD_OUTGOING) && (V[j].ifs & IF_OLD_OUTGOING)) ||
+          ((V[i].ifs & IF_OUTGOING) && (V[j].ifs & IF_OUTGOING))) { gi.at(i, j) = 1; gi.at(j, i) = 1; }
+  Graph gu = gi;
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) gu.at(i, j) = gi.at(i, j) || gi.at(j, i);
+  std::vector<std::vector<int>> cl;
+  std::vector<int> card(n);
+  for (int i = 0; i < n; i++) card[i] = V[i].card;
+  if (triangulate(gu, card, parents, cl, err) < 0) return NIP_ERROR_GENERAL;
+  m.cliques.resize(cl.size());
+  for (size_t c = 0; c < cl.size(); c++) {
+    m.cliques[c].vars = cl[c];
+    size_t sz = 1;
+    for (int v : cl[c]) sz *= (size_t)V[v].card;
+    m.cliques[c].original.assign(sz, 1.0);
+  }
+  std::vector<Sepset> ss;
+  create_sepsets(m.cliques, ss);
+
+  // sepset numbering: first appearance walking cliques in order, then each
+  // clique's link list in order (the order the index contract is dumped in)
+  {
+    std::vector<int> remap(ss.size(), -1);
+    int next_id = 0;
+    for (auto& c : m.cliques)
+      for (int s : c.links) if (remap[s] < 0) remap[s] = next_id++;
+    m.sepsets.resize(ss.size());
+    for (size_t s = 0; s < ss.size(); s++) m.sepsets[remap[s]] = ss[s];
+    for (auto& c : m.cliques) for (int& s : c.links) s = remap[s];
+  }
+
+  // --- families (nipjointree.c:967-1040) ---
+  for (int v = 0; v < n; v++) {
+    std::vector<int> fam = V[v].parents;
+    fam.push_back(v);
+    V[v].family = find_clique(m.cliques, fam);
+    if (V[v].family < 0) { err = "no family clique for " + V[v].symbol; return NIP_ERROR_GENERAL; }
+    const auto& cv = m.cliques[V[v].family].vars;
+    V[v].family_mapping.assign(V[v].parents.size() + 1, 0);
+    for (size_t i = 0; i < cv.size(); i++) if (cv[i] == v) { V[v].family_mapping[0] = (int)i; break; }
+    size_t found = 0;
+    for (size_t i = 0; i < cv.size() && found < V[v].parents.size(); i++)
+      for (size_t j = 0; j < V[v].parents.size(); j++)
+        if (cv[i] == V[v].parents[j]) { V[v].family_mapping[j + 1] = (int)i; found++; break; }
+    V[v].family_pos = V[v].family_mapping[0];
+  }
+
+  // --- parsed_potentials_to_jtree (huginnet.y:1110-1152) ---
+  for (const auto& q : parsed) {
+    const int fc = V[q.child].family;
+    if (q.ids.size() > 1) {
+      // nip_init_clique (nipjointree.c:713-772): positions of the potential's
+      // (ascending-ID) variables in the clique, in clique order
+      const auto& cv = m.cliques[fc].vars;
+      std::vector<int> map;
+      if (q.ids.size() < cv.size()) {
+        for (size_t i = 0; i < cv.size() && map.size() < q.ids.size(); i++) {
+          int var = cv[i];
+          for (int p : q.parents) if (var == p) map.push_back((int)i);
+          if (var == q.child) map.push_back((int)i);
+        }
+      } else {
+        for (size_t i = 0; i < cv.size(); i++) map.push_back((int)i);
+      }
+      init_into(cv, card, m.cliques[fc].original, q.ids, q.data, map);
+    } else {
+      V[q.child].has_prior = true;                         // nip_set_prior
+      V[q.child].prior = q.data;
+    }
+  }
+
+  // --- model assembly (nip.c:147-264) ---
+  for (int v = 0; v < n; v++)
+    if (V[v].parents.empty() && !V[v].has_prior) { V[v].has_prior = true; V[v].prior.assign(V[v].card, 0.0); }
+  for (int v = 0; v < n; v++) {
+    if (V[v].ifs & IF_OLD_OUTGOING) { m.previous_outgoing.push_back(v); m.outgoing.push_back(V[v].next); }
+    if (!V[v].parents.empty()) m.children.push_back(v); else m.independent.push_back(v);
+  }
+  if (!m.outgoing.empty()) {
+    m.in_clique = find_clique(m.cliques, m.previous_outgoing);
+    m.out_clique = find_clique(m.cliques, m.outgoing);
+  }
+  build_chain_plan(m);
+  return 0;
+}
+
+int param_size(const Model& m) {
+  int tot = 0;
+  for (const auto& v : m.vars) {
+    int s = v.card;
+    for (int p : v.parents) s *= m.vars[p].card;
+    tot += s;
+  }
+  return tot;
+}
+
+// m_step (src/nip.c:2010-2071) on the host tables.
+int m_step(Model& m, const double* params) {
+  std::vector<int> card(m.vars.size());
+  for (size_t i = 0; i < m.vars.size(); i++) card[i] = m.vars[i].card;
+  std::vector<std::vector<double>> P;
+  size_t off = 0;
+  for (const auto& v : m.vars) {
+    size_t s = v.card;
+    for (int p : v.parents) s *= m.vars[p].card;
+    std::vector<double> t(params + off, params + off + s);
+    for (size_t i = 0; i < s; i += v.card) normalise_array(t.data() + i, v.card);  // normalise_cpd
+    P.push_back(std::move(t));
+    off += s;
+  }
+  for (auto& c : m.cliques) std::fill(c.original.begin(), c.original.end(), 1.0);  // total_reset
+  for (size_t i = 0; i < m.vars.size(); i++) {
+    auto& v = m.vars[i];
+    if (!v.parents.empty()) {
+      // nip_init_potential(params, family->original_p, family_mapping): the
+      // parameter dims are (child, parents...) in v->parents order
+      std::vector<int> pvars{(int)i};
+      pvars.insert(pvars.end(), v.parents.begin(), v.parents.end());
+      init_into(m.cliques[v.family].vars, card, m.cliques[v.family].original, pvars, P[i], v.family_mapping);
+    } else {
+      v.prior = P[i];  // nip_total_marginalise(params, prior, 0) of a 1-D table
+    }
+  }
+  build_chain_plan(m);
+  return 0;
+}
+
+// ------------------------------------------------------------------
+// Index-contract dump (same schema as oracle/ref/nipref_harness.c nh_desc)
+// ------------------------------------------------------------------
+namespace {
+void put_ints(std::ostringstream& o, const std::vector<int>& v) {
+  o << "[";
+  for (size_t i = 0; i < v.size(); i++) o << (i ? "," : "") << v[i];
+  o << "]";
+}
+void put_doubles(std::ostringstream& o, const std::vector<double>& v) {
+  char b[40];
+  o << "[";
+  for (size_t i = 0; i < v.size(); i++) { std::snprintf(b, sizeof b, "%.17g", v[i]); o << (i ? "," : "") << b; }
+  o << "]";
+}
+}  // namespace
+
+std::string model_desc_json(const Model& m) {
+  std::ostringstream o;
+  o << "{\"vars\":[";
+  for (size_t i = 0; i < m.vars.size(); i++) {
+    const auto& v = m.vars[i];
+    o << (i ? "," : "") << "{\"symbol\":\"" << v.symbol << "\",\"card\":" << v.card
+      << ",\"if\":" << v.ifs << ",\"next\":" << v.next << ",\"previous\":" << v.previous
+      << ",\"parents\":";
+    put_ints(o, v.parents);
+    o << ",\"prior\":";
+    if (v.parents.empty() && v.has_prior) put_doubles(o, v.prior); else o << "null";
+    o << ",\"family\":" << v.family << ",\"family_mapping\":";
+    put_ints(o, v.family_mapping);
+    o << "}";
+  }
+  o << "],\"cliques\":[";
+  for (size_t c = 0; c < m.cliques.size(); c++) {
+    o << (c ? "," : "") << "{\"vars\":";
+    put_ints(o, m.cliques[c].vars);
+    o << ",\"links\":";
+    put_ints(o, m.cliques[c].links);
+    o << ",\"original\":";
+    put_doubles(o, m.cliques[c].original);
+    o << "}";
+  }
+  o << "],\"sepsets\":[";
+  for (size_t s = 0; s < m.sepsets.size(); s++) {
+    o << (s ? "," : "") << "{\"a\":" << m.sepsets[s].a << ",\"b\":" << m.sepsets[s].b << ",\"vars\":";
+    put_ints(o, m.sepsets[s].vars);
+    o << "}";
+  }
+  o << "],\"in_clique\":" << m.in_clique << ",\"out_clique\":" << m.out_clique << ",\"outgoing\":";
+  put_ints(o, m.outgoing);
+  o << ",\"previous_outgoing\":";
+  put_ints(o, m.previous_outgoing);
+  o << ",\"independent\":";
+  put_ints(o, m.independent);
+  o << ",\"children\":";
+  put_ints(o, m.children);
+  o << "}";
+  return o.str();
+}
+
+// ------------------------------------------------------------------
+// Chain (HMM) execution plan.
+// ------------------------------------------------------------------
+void build_chain_plan(Model& m) {
+  ChainPlan& P = m.chain;
+  P = ChainPlan();
+  if (m.outgoing.size() != 1 || m.cliques.size() != 2 || m.vars.size() != 3) return;
+  const int vp = m.previous_outgoing[0], vc = m.outgoing[0];
+  if (m.in_clique != m.out_clique || m.in_clique < 0) return;
+  const int ct = m.in_clique, ce = 1 - ct;
+  const auto& tv = m.cliques[ct].vars;
+  if (tv.size() != 2 || std::find(tv.begin(), tv.end(), vp) == tv.end() ||
+      std::find(tv.begin(), tv.end(), vc) == tv.end()) return;
+  int vo = -1;
+  for (int v = 0; v < 3; v++) if (v != vp && v != vc) vo = v;
+  const auto& ev = m.cliques[ce].vars;
+  if (ev.size() != 2 || std::find(ev.begin(), ev.end(), vc) == ev.end() ||
+      std::find(ev.begin(), ev.end(), vo) == ev.end()) return;
+  // structural roles: vp independent (prior), vc child of vp, vo child of vc
+  if (!m.vars[vp].parents.empty() || m.vars[vc].parents != std::vector<int>{vp} ||
+      m.vars[vo].parents != std::vector<int>{vc}) return;
+  if (m.vars[vp].family != ct || m.vars[vc].family != ct || m.vars[vo].family != ce) return;
+  const int N = m.vars[vp].card, M = m.vars[vo].card;
+  if (N > 16 || N < 1 || M < 1 || M > 1024) return;
+  P.N = N; P.M = M; P.v_prev = vp; P.v_cur = vc; P.v_obs = vo; P.c_trans = ct; P.c_emit = ce;
+  P.A.assign(256, 0.0);
+  const auto& ot = m.cliques[ct].original;
+  const bool prev_first = tv[0] == vp;       // dimension 0 = lower ID
+  for (int x = 0; x < N; x++)
+    for (int y = 0; y < N; y++) P.A[x * 16 + y] = prev_first ? ot[x + N * y] : ot[y + N * x];
+  const auto& oe = m.cliques[ce].original;
+  const bool cur_first = ev[0] == vc;
+  P.Etab.assign((size_t)(M + 2) * 16, 0.0);
+  std::vector<double> s(16, 0.0);
+  for (int y = 0; y < N; y++) {
+    for (int mm = 0; mm < M; mm++) {
+      double e = cur_first ? oe[y + N * mm] : oe[mm + M * y];
+      P.Etab[(size_t)mm * 16 + y] = e;
+      s[y] += e;   // nip_general_marginalise order over the clique isn't needed: tolerance
+    }
+    P.Etab[(size_t)M * 16 + y] = s[y];
+  }
+  P.pi.assign(16, 0.0);
+  for (int x = 0; x < N; x++) P.pi[x] = m.vars[vp].prior[x];
+  P.ts.assign(16, 0.0);
+  for (int x = 0; x < N; x++) {
+    double acc = 0;
+    for (int y = 0; y < N; y++) acc += P.A[x * 16 + y] * s[y];
+    P.ts[x] = acc;
+  }
+  P.valid = true;
+}
+
+}  // namespace nipamd

@@ -1,0 +1,317 @@
+// engine.cpp -- C-ABI of the nip_amd engine (include/nip_amd.h).
+//
+// Host side of the hot path: owns the compiled model, its device-resident
+// tables and scratch, validates the request against the GPU execution plan
+// and launches the gfx950 kernels on the caller's stream.  There is no CPU
+// fallback: a request the GPU plan does not cover fails with
+// NIPAMD_ERROR_UNSUPPORTED, and a missing/unusable device with
+// NIPAMD_ERROR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "chain_kernels.h"
+#include "model.h"
+#include "nip_amd.h"
+
+struct nipamd_model {
+  nipamd::Model m;
+  unsigned version = 1;          // bumped whenever the tables change
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_OK(expr)                                                         \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess)                                                    \
+      return fail(NIPAMD_ERROR_DEVICE, std::string(#expr) + ": " +          \
+                                           hipGetErrorString(e_));           \
+  } while (0)
+
+struct DevState {
+  int device = -1;
+  unsigned version = 0;
+  double* A = nullptr;
+  double* Etab = nullptr;
+  double* pi = nullptr;
+  double* ts = nullptr;
+  double* S = nullptr;
+  size_t S_bytes = 0;
+};
+
+DevState* dev_of(nipamd_model* mm) {
+  if (!mm->m.dev) mm->m.dev = new DevState();
+  return static_cast<DevState*>(mm->m.dev);
+}
+
+void dev_release(DevState* d) {
+  if (!d) return;
+  (void)hipFree(d->A); (void)hipFree(d->Etab); (void)hipFree(d->pi); (void)hipFree(d->ts); (void)hipFree(d->S);
+  *d = DevState();
+}
+
+// Upload the chain plan's tables to the current device (once per version).
+int ensure_tables(nipamd_model* mm) {
+  int dev = -1;
+  HIP_OK(hipGetDevice(&dev));
+  DevState* d = dev_of(mm);
+  if (d->device != dev) { dev_release(d); d->device = dev; }
+  if (d->version == mm->version && d->A) return 0;
+  const auto& P = mm->m.chain;
+  (void)hipFree(d->A); (void)hipFree(d->Etab); (void)hipFree(d->pi); (void)hipFree(d->ts);
+  d->A = d->Etab = d->pi = d->ts = nullptr;
+  HIP_OK(hipMalloc(&d->A, P.A.size() * sizeof(double)));
+  HIP_OK(hipMalloc(&d->Etab, P.Etab.size() * sizeof(double)));
+  HIP_OK(hipMalloc(&d->pi, P.pi.size() * sizeof(double)));
+  HIP_OK(hipMalloc(&d->ts, P.ts.size() * sizeof(double)));
+  HIP_OK(hipMemcpy(d->A, P.A.data(), P.A.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d->Etab, P.Etab.data(), P.Etab.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d->pi, P.pi.data(), P.pi.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d->ts, P.ts.data(), P.ts.size() * sizeof(double), hipMemcpyHostToDevice));
+  d->version = mm->version;
+  return 0;
+}
+
+int ensure_scratch(nipamd_model* mm, size_t bytes) {
+  DevState* d = dev_of(mm);
+  if (d->S_bytes >= bytes) return 0;
+  (void)hipFree(d->S);
+  d->S = nullptr;
+  d->S_bytes = 0;
+  HIP_OK(hipMalloc(&d->S, bytes));
+  d->S_bytes = bytes;
+  return 0;
+}
+
+// Which GPU plan (if any) covers this request.
+int check_chain_request(const nipamd_model* mm, int n_obs, const int* obs_vars,
+                        int n_query, const int* query, int* obs_col, std::string& why) {
+  const auto& P = mm->m.chain;
+  if (!P.valid) { why = "model slice is not chain-shaped (GPU plan: HMM-shaped DBN)"; return 0; }
+  int col = -1;
+  for (int i = 0; i < n_obs; i++) {
+    if (obs_vars[i] == P.v_obs) { if (col >= 0) { why = "observed variable listed twice"; return 0; } col = i; }
+    else { why = "evidence on a variable other than the emission variable is not in the GPU plan"; return 0; }
+  }
+  if (col < 0 && n_obs > 0) { why = "no usable observation column"; return 0; }
+  for (int i = 0; i < n_query; i++)
+    if (query[i] != P.v_cur) { why = "query variable other than the current-slice interface variable"; return 0; }
+  *obs_col = col;
+  return 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nipamd_last_error(void) { return g_err.c_str(); }
+
+int nipamd_model_from_spec(int n_nodes, const char* const* symbols, const int* card,
+                           const int* next, int n_pots, const int* pot_child,
+                           const int* pot_nparents, const int* pot_parents,
+                           const int* pot_ndata, const double* pot_data,
+                           nipamd_model** out) {
+  if (!out || !card || n_nodes <= 0) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  nipamd::NetSpec spec;
+  for (int i = 0; i < n_nodes; i++) {
+    spec.symbols.push_back(symbols && symbols[i] ? symbols[i] : ("V" + std::to_string(i)));
+    spec.card.push_back(card[i]);
+    spec.next.push_back(next ? next[i] : -1);
+  }
+  size_t po = 0, dof = 0;
+  for (int p = 0; p < n_pots; p++) {
+    nipamd::NetSpec::Pot q;
+    q.child = pot_child[p];
+    for (int k = 0; k < pot_nparents[p]; k++) q.parents.push_back(pot_parents[po++]);
+    q.has_data = pot_ndata[p] > 0;
+    q.data.assign(pot_data + dof, pot_data + dof + pot_ndata[p]);
+    dof += pot_ndata[p];
+    if (q.child < 0 || q.child >= n_nodes) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad child index");
+    for (int v : q.parents) if (v < 0 || v >= n_nodes) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad parent index");
+    spec.pots.push_back(std::move(q));
+  }
+  auto* mm = new nipamd_model();
+  std::string err;
+  int rc = nipamd::compile_model(spec, mm->m, err);
+  if (rc) { delete mm; return fail(rc, err); }
+  *out = mm;
+  return 0;
+}
+
+int nipamd_model_from_net(const char* path, nipamd_model** out) {
+  if (!path || !out) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  std::ifstream f(path);
+  if (!f) return fail(NIP_ERROR_FILENOTFOUND, std::string("cannot open ") + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  nipamd::NetSpec spec;
+  std::string err;
+  int rc = nipamd::parse_net_file(ss.str(), spec, err);
+  if (rc) return fail(rc, err);
+  auto* mm = new nipamd_model();
+  rc = nipamd::compile_model(spec, mm->m, err);
+  if (rc) { delete mm; return fail(rc, err); }
+  *out = mm;
+  return 0;
+}
+
+void nipamd_model_free(nipamd_model* mm) {
+  if (!mm) return;
+  DevState* d = static_cast<DevState*>(mm->m.dev);
+  dev_release(d);
+  delete d;
+  delete mm;
+}
+
+int nipamd_model_num_vars(const nipamd_model* mm) { return mm ? (int)mm->m.vars.size() : -1; }
+
+int nipamd_model_var_index(const nipamd_model* mm, const char* symbol) {
+  if (!mm || !symbol) return -1;
+  for (size_t i = 0; i < mm->m.vars.size(); i++)
+    if (mm->m.vars[i].symbol == symbol) return (int)i;
+  return -1;
+}
+
+int nipamd_model_var_card(const nipamd_model* mm, int v) {
+  if (!mm || v < 0 || v >= (int)mm->m.vars.size()) return -1;
+  return mm->m.vars[v].card;
+}
+
+int nipamd_model_desc_json(const nipamd_model* mm, char* buf, int cap) {
+  if (!mm) return -1;
+  std::string s = nipamd::model_desc_json(mm->m);
+  if (buf && cap > 0) {
+    size_t n = s.size() < (size_t)(cap - 1) ? s.size() : (size_t)(cap - 1);
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int)s.size();
+}
+
+int nipamd_model_param_size(const nipamd_model* mm) { return mm ? nipamd::param_size(mm->m) : -1; }
+
+int nipamd_model_gpu_supported(const nipamd_model* mm, int n_obs, const int* obs_vars,
+                               int n_query, const int* query) {
+  if (!mm) return 0;
+  int col; std::string why;
+  return check_chain_request(mm, n_obs, obs_vars, n_query, query, &col, why);
+}
+
+int nipamd_model_original(const nipamd_model* mm, int c, double* out, int cap) {
+  if (!mm || c < 0 || c >= (int)mm->m.cliques.size()) return -1;
+  const auto& o = mm->m.cliques[c].original;
+  size_t n = o.size() < (size_t)cap ? o.size() : (size_t)cap;
+  if (out) std::memcpy(out, o.data(), n * sizeof(double));
+  return (int)o.size();
+}
+
+int nipamd_model_prior(const nipamd_model* mm, int v, double* out) {
+  if (!mm || v < 0 || v >= (int)mm->m.vars.size()) return -1;
+  const auto& var = mm->m.vars[v];
+  if (!var.has_prior || !var.parents.empty()) return 0;
+  if (out) std::memcpy(out, var.prior.data(), var.prior.size() * sizeof(double));
+  return (int)var.prior.size();
+}
+
+int nipamd_m_step(nipamd_model* mm, const double* params) {
+  if (!mm || !params) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  int rc = nipamd::m_step(mm->m, params);
+  mm->version++;
+  return rc;
+}
+
+int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+              int B, int T, int n_query, const int* query, double* d_post,
+              double* d_ll, uint32_t* d_status, void* stream) {
+  if (!mm || B < 0 || T < 1 || (n_obs > 0 && (!d_obs || !obs_vars)) || (n_query > 0 && (!query || !d_post)))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (B == 0) return 0;
+  int col = -1;
+  std::string why;
+  if (!check_chain_request(mm, n_obs, obs_vars, n_query, query, &col, why))
+    return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+  const auto& P = mm->m.chain;
+  if (P.M + 2 > 255) return fail(NIPAMD_ERROR_UNSUPPORTED, "observation cardinality above 253");
+  if (nipamd::chain_fb_lds_bytes(P.M, T) > 96 * 1024)
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
+  if (int rc = ensure_tables(mm)) return rc;
+  if (int rc = ensure_scratch(mm, (size_t)B * T * 16 * sizeof(double))) return rc;
+  DevState* d = dev_of(mm);
+  nipamd::ChainArgs a{};
+  a.obs = d_obs;
+  a.obs_bstride = (long)T * (n_obs > 0 ? n_obs : 1);
+  a.obs_tstride = n_obs > 0 ? n_obs : 1;
+  a.obs_col = col;
+  static const int32_t kNone = -1;
+  if (col < 0) { a.obs = nullptr; }
+  a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = P.M;
+  a.A = d->A; a.Etab = d->Etab; a.pi = d->pi; a.ts = d->ts; a.S = d->S;
+  int stride = 0;
+  for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
+  a.post = d_post;
+  a.post_bstride = (long)T * stride;
+  a.post_tstride = stride;
+  a.post_off = 0;
+  a.ll = d_ll;
+  a.status = d_status;
+  (void)kNone;
+  if (n_query == 0) { a.post = nullptr; }
+  // query variables all equal the chain variable: one launch per copy keeps
+  // the kernel simple (the common case is exactly one)
+  const int nq = n_query > 0 ? n_query : 1;
+  for (int q = 0; q < nq; q++) {
+    a.post_off = q * P.N;
+    if (q > 0) { a.ll = nullptr; a.status = nullptr; }
+    if (nipamd::chain_fb_launch(a, (hipStream_t)stream))
+      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  }
+  return 0;
+}
+
+int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
+                   int B, int T, int n_query, const int* query, double* post,
+                   double* ll, uint32_t* status) {
+  if (!mm || B < 0 || T < 1) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (B == 0) return 0;
+  int stride = 0;
+  for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
+  int32_t* d_obs = nullptr; double* d_post = nullptr; double* d_ll = nullptr; uint32_t* d_st = nullptr;
+  const size_t nob = (size_t)B * T * (n_obs > 0 ? n_obs : 1);
+  const size_t npo = (size_t)B * T * (stride > 0 ? stride : 1);
+  HIP_OK(hipMalloc(&d_obs, nob * sizeof(int32_t)));
+  HIP_OK(hipMalloc(&d_post, npo * sizeof(double)));
+  HIP_OK(hipMalloc(&d_ll, (size_t)B * sizeof(double)));
+  HIP_OK(hipMalloc(&d_st, (size_t)B * sizeof(uint32_t)));
+  if (n_obs > 0) HIP_OK(hipMemcpy(d_obs, obs, nob * sizeof(int32_t), hipMemcpyHostToDevice));
+  int rc = nipamd_fb(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_st, nullptr);
+  if (rc == 0) {
+    HIP_OK(hipDeviceSynchronize());
+    if (post && stride > 0) HIP_OK(hipMemcpy(post, d_post, npo * sizeof(double), hipMemcpyDeviceToHost));
+    if (ll) HIP_OK(hipMemcpy(ll, d_ll, (size_t)B * sizeof(double), hipMemcpyDeviceToHost));
+    if (status) HIP_OK(hipMemcpy(status, d_st, (size_t)B * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(d_obs); (void)hipFree(d_post); (void)hipFree(d_ll); (void)hipFree(d_st);
+  return rc;
+}
+
+int nipamd_estep(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                 int B, int T, double* d_counts, double* d_ll, uint32_t* d_status, void* stream) {
+  (void)d_obs; (void)n_obs; (void)obs_vars; (void)B; (void)T; (void)d_counts; (void)d_ll; (void)d_status; (void)stream;
+  if (!mm) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step not built yet");
+}
+
+}  // extern "C"

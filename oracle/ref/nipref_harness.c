@@ -40,7 +40,7 @@
 #include "nipjointree.h"
 #include "nipgraph.h"
 
-#define NH_MAX_MODELS 64
+#define NH_MAX_MODELS 65536
 
 /* Layout-compatible subset of nip_model_struct (src/nip.h:71-104); only the
  * harness reads it, so it is declared locally instead of pulling in nip.h
