@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Benchmark: sequence-timesteps/s of batched fwd-bwd smoothing (BASELINE.json).
+
+One "step" = one pass of the hot path (nipamd_fb: forward_backward_inference,
+src/nip.c:1320, batched) over one batch of B synthetic sequences x T time
+slices resident in HBM -- SURVEY 8(d) config 2: HMM-shaped DBN with 16 hidden
+and 16 observed states, B = 4096 sequences per GPU, T = 1024.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 is launched by torch.distributed.run (one process per GPU, RCCL for the
+barrier / max-over-ranks only: sequences shard with no data-path collective,
+"scaling": "weak").  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "sequence-timesteps/s fwd-bwd smoothing, 16-state DBN; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0            # MI355X spec (MI355X_MICROARCH.md chip table)
+
+
+def algorithmic_bytes_per_seq_step(N: int) -> int:
+    """What the path must move per sequence-timestep (Roofline):
+    observation int32 read once (4 B), one 16-wide fp64 interface message
+    written and read back (alpha for t < T/2, beta for t >= T/2: 2 x 128 B),
+    the N-wide fp64 posterior written (8N B)."""
+    return 4 + 2 * 16 * 8 + 8 * N
+
+
+def cpu_baseline(nodes, pots, obs, budget_s: float = 12.0):
+    """Reference CPU path on this host, single core, bounded sample."""
+    from oracle import bind
+    from nip_amd import synth
+    kind = "reference"
+    try:
+        if not bind.ref_available():
+            raise RuntimeError("oracle/_ref not built")
+        orc = bind.RefHarness(synth.spec_to_replay(nodes, pots))
+    except Exception:
+        kind = "port"
+        import nip_amd
+        orc = bind.PortOracle(nip_amd.Model.from_spec(nodes, pots).desc())
+    T = obs.shape[1]
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        orc.fb(obs[n], [2], [1])
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= obs.shape[0]:
+            break
+    return {"value": n * T / el, "unit": "sequence-timesteps/s", "cores": 1, "kind": kind,
+            "sample": "%d sequences x T=%d of the bench workload, forward_backward_inference with "
+                      "ll, %s, gcc -O2, %.1f s" % (
+                          n, T, "reference nippotential/nipjointree/nipgraph compiled from "
+                          "/root/reference sources + restated nip.c loop" if kind == "reference"
+                          else "standalone C restatement (oracle/nip_oracle.c)", el)}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="sequences per GPU")
+    ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import nip_amd
+    from nip_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    B, T, N, M = args.batch, args.T, args.N, args.M
+    nodes, pots = synth.hmm_spec(N, M)
+    model = nip_amd.Model.from_spec(nodes, pots)
+    ov, q = [model.variable("M1")], [model.variable("P1")]
+    obs_np = synth.observations(B, T, M, seed=1 + 7919 * rank)
+    obs = torch.from_numpy(obs_np).to(dev)
+    post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
+    ll = torch.empty((B,), dtype=torch.float64, device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def step():
+        nip_amd.forward_backward_inference(model, obs, ov, q, post, ll, st)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[dev.index])
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record()
+        step()
+        evs[i][1].record()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if not args.no_check and (not bool(torch.isfinite(ll).all()) or int(st.abs().sum()) != 0):
+        raise SystemExit("bench: non-finite log-likelihood / zero-mass status on synthetic data")
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    units = B * T * args.steps * world
+    value = units / elapsed
+    bpu = algorithmic_bytes_per_seq_step(N)
+    achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
+    workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (N, M, B, T)
+    traffic = load_traffic(workload)
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": value, "unit": "sequence-timesteps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": workload, "B_per_gpu": B, "T": T, "hidden_states": N,
+                       "observed_states": M, "parallelism": "dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel": "chain_fb_kernel",
+                         "kernel_ms": kern_ms, "bytes_per_unit": bpu},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(nodes, pots, obs_np)
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

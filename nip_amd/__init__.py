@@ -21,7 +21,7 @@ from . import build as _build
 __all__ = ["NipError", "Model", "parse_model", "lib", "forward_backward_inference",
            "forward_backward_inference_host", "LIB_PATH"]
 
-LIB_PATH = _build.LIB
+LIB_PATH = os.environ.get("NIPAMD_LIB", _build.LIB)
 
 NIP_NO_ERROR = 0
 NIP_ERROR_NULLPOINTER = 1

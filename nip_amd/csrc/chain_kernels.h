@@ -17,7 +17,7 @@ struct ChainArgs {
   const double* Etab;    // [(M+2)][16]
   const double* pi;      // [16]
   const double* ts;      // [16]
-  double* S;             // scratch [B][T][16]: alpha_t (t < H), beta_t (t >= H)
+  double* S;             // scratch, chain_scratch_bytes(B, T)
   double* post;          // posterior output
   long post_bstride;     // elements between sequences
   int post_tstride;      // elements between time steps
@@ -26,6 +26,14 @@ struct ChainArgs {
   unsigned* status;      // [B] or nullptr
   double* counts;        // E-step only: per-block partial counts
 };
+
+// Scratch layout: per sequence kGuard + T + kGuard steps of 16 doubles
+// (alpha_t for t < H, beta_t for t >= H), plus one sink row after the last
+// sequence for lanes that must not write.  Guards let prefetch over-run.
+constexpr int kScratchGuard = 16;   // >= 2 chunks: the deepest prefetch over-run
+__host__ __device__ inline long chain_scratch_row(int T) { return (long)(T + 2 * kScratchGuard) * 16; }
+__host__ __device__ inline int chain_codes_row(int T) { return ((T + 7) & ~7) + 2 * kScratchGuard; }
+inline size_t chain_scratch_bytes(long B, int T) { return (size_t)(B + 2) * chain_scratch_row(T) * sizeof(double); }
 
 size_t chain_fb_lds_bytes(int M, int T);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);

@@ -42,42 +42,57 @@ namespace nipamd {
 
 namespace {
 
+// DPP row_ror:K -- every lane of a 16-lane row has a source, so no "old"
+// operand is needed (mov_dpp with bound_ctrl)
 template <int K>
 __device__ __forceinline__ double row_ror(double v) {
   static_assert(K > 0 && K < 16, "row_ror");
   const int lo = __double2loint(v), hi = __double2hiint(v);
-  const int rl = __builtin_amdgcn_update_dpp(0, lo, 0x120 + K, 0xF, 0xF, false);
-  const int rh = __builtin_amdgcn_update_dpp(0, hi, 0x120 + K, 0xF, 0xF, false);
+  const int rl = __builtin_amdgcn_mov_dpp(lo, 0x120 + K, 0xF, 0xF, true);
+  const int rh = __builtin_amdgcn_mov_dpp(hi, 0x120 + K, 0xF, 0xF, true);
   return __hiloint2double(rh, rl);
 }
 
-template <int K>
-__device__ __forceinline__ int row_ror_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x120 + K, 0xF, 0xF, false);
+
+
+// acc += (value of lane K of this row) * c   -- one v_fmac_f64 with a 64-bit
+// DPP row_newbcast source (gfx950 DP-ALU DPP); the broadcast costs nothing
+// extra.  hipcc neither pads nor schedules inside asm, so the VALU->DPP read
+// hazard (2 wait states) is covered by the s_nop in the first term (NOP_FIRST).
+template <int K, bool NOP_FIRST>
+__device__ __forceinline__ void fmac_bcast(double& acc, double v, double c) {
+  if (NOP_FIRST)
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(v), "v"(c), "n"(K));
+  else
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(v), "v"(c), "n"(K));
 }
 
-// out[k] = value held by the lane that row_ror:k reads from (out[0] = own)
-__device__ __forceinline__ void row_gather(double v, double (&out)[16]) {
-  out[0] = v;
-  out[1] = row_ror<1>(v);   out[2] = row_ror<2>(v);   out[3] = row_ror<3>(v);
-  out[4] = row_ror<4>(v);   out[5] = row_ror<5>(v);   out[6] = row_ror<6>(v);
-  out[7] = row_ror<7>(v);   out[8] = row_ror<8>(v);   out[9] = row_ror<9>(v);
-  out[10] = row_ror<10>(v); out[11] = row_ror<11>(v); out[12] = row_ror<12>(v);
-  out[13] = row_ror<13>(v); out[14] = row_ror<14>(v); out[15] = row_ror<15>(v);
-}
-
-__device__ __forceinline__ void row_sources(int y, int (&src)[16]) {
-  src[0] = y;
-  src[1] = row_ror_i<1>(y);   src[2] = row_ror_i<2>(y);   src[3] = row_ror_i<3>(y);
-  src[4] = row_ror_i<4>(y);   src[5] = row_ror_i<5>(y);   src[6] = row_ror_i<6>(y);
-  src[7] = row_ror_i<7>(y);   src[8] = row_ror_i<8>(y);   src[9] = row_ror_i<9>(y);
-  src[10] = row_ror_i<10>(y); src[11] = row_ror_i<11>(y); src[12] = row_ror_i<12>(y);
-  src[13] = row_ror_i<13>(y); src[14] = row_ror_i<14>(y); src[15] = row_ror_i<15>(y);
+// sum_k x[lane k] * c[k] over the 16 lanes of the row, x read by broadcast;
+// the result is identical in every lane (fixed k order).
+__device__ __forceinline__ double dot_bcast(double x, const double (&c)[16]) {
+#ifdef NIPAMD_ABLATE_NO_DOT      // timing-only ablation build (wrong results)
+  return x * c[0];
+#endif
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  fmac_bcast<0, true>(a0, x, c[0]);   fmac_bcast<1, false>(a1, x, c[1]);
+  fmac_bcast<2, false>(a2, x, c[2]);  fmac_bcast<3, false>(a3, x, c[3]);
+  fmac_bcast<4, false>(a0, x, c[4]);  fmac_bcast<5, false>(a1, x, c[5]);
+  fmac_bcast<6, false>(a2, x, c[6]);  fmac_bcast<7, false>(a3, x, c[7]);
+  fmac_bcast<8, false>(a0, x, c[8]);  fmac_bcast<9, false>(a1, x, c[9]);
+  fmac_bcast<10, false>(a2, x, c[10]); fmac_bcast<11, false>(a3, x, c[11]);
+  fmac_bcast<12, false>(a0, x, c[12]); fmac_bcast<13, false>(a1, x, c[13]);
+  fmac_bcast<14, false>(a2, x, c[14]); fmac_bcast<15, false>(a3, x, c[15]);
+  return (a0 + a1) + (a2 + a3);
 }
 
 // Sum over the 16 lanes of the row; identical bits in every lane (each level
 // pairs lanes whose partial sums are equal, and IEEE addition commutes).
 __device__ __forceinline__ double row_sum(double x) {
+#ifdef NIPAMD_ABLATE_NO_REDUCE   // timing-only ablation build (wrong results)
+  return x;
+#endif
   x += row_ror<8>(x);
   x += row_ror<4>(x);
   x += row_ror<2>(x);
@@ -85,165 +100,255 @@ __device__ __forceinline__ double row_sum(double x) {
   return x;
 }
 
-__device__ __forceinline__ double dot16(const double (&a)[16], const double (&c)[16]) {
-  double s0 = a[0] * c[0], s1 = a[1] * c[1], s2 = a[2] * c[2], s3 = a[3] * c[3];
-#pragma unroll
-  for (int k = 4; k < 16; k += 4) {
-    s0 = __builtin_fma(a[k], c[k], s0);
-    s1 = __builtin_fma(a[k + 1], c[k + 1], s1);
-    s2 = __builtin_fma(a[k + 2], c[k + 2], s2);
-    s3 = __builtin_fma(a[k + 3], c[k + 3], s3);
-  }
-  return (s0 + s1) + (s2 + s3);
-}
 
 // exponent e such that x = m * 2^e, m in [0.5, 1); 0 for x == 0
 __device__ __forceinline__ int exp2_of(double x) {
   return x != 0.0 ? __builtin_amdgcn_frexp_exp(x) : 0;
 }
 
+// x / c for the row-uniform normaliser c (x itself when c == 0, as
+// nip_normalise_array leaves an all-zero array alone, nippotential.c:354):
+// v_rcp_f64 refined by two Newton steps, then one multiply.
+__device__ __forceinline__ double div_by(double x, double c) {
+  if (c == 0.0) return x;
+  double r = __builtin_amdgcn_rcp(c);
+  r = __builtin_fma(r, __builtin_fma(-c, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-c, r, 1.0), r);
+  return x * r;
+}
+
+constexpr int kChunk = 8;   // steps per unrolled chunk; prefetch distance = 1 chunk
+
+// Per-chunk prefetch registers: evidence values from LDS and (phase B) the
+// other direction's interface vector from HBM, issued one chunk ahead so no
+// step waits on a fresh load.
+struct Prefetch {
+  double e[kChunk];
+  double s[kChunk];
+};
+
 }  // namespace
 
 constexpr int kChainsPerBlock = 8;   // 8 sequences; waves 0-1 forward, 2-3 backward
 constexpr int kThreads = 256;
 
-__global__ __launch_bounds__(kThreads)
+namespace {
+
+constexpr int kGuard = kScratchGuard;   // guard steps on both sides of every codes / S row
+
+// Per-row view of a chain: rows 0,1 of every wave run the forward filter of
+// sequences 2w, 2w+1; rows 2,3 run the backward filter of the same two
+// sequences, so every wave issues the same instruction stream (the two
+// directions differ only in data: A column vs row, time direction, and which
+// of u / u*e is the interface vector).
+struct ChainCtx {
+  const double* Et;        // LDS evidence table, this lane's column (Et + y)
+  const uint8_t* codes;    // LDS codes of this sequence; codes[-kGuard .. T+kGuard)
+  const double* Sload;     // S row of this sequence (+y); guard steps both sides
+  double* Sstore;          // same, or a sink for lanes that must not write
+  long Sstride;            // 16, or 0 for the sink
+  double* Pstore;          // posterior of this sequence (+off+y), or a sink
+  long Pstride;            // post_tstride, or 0 for the sink
+};
+
+// Prefetch kChunk steps of this row starting at t0 in direction dir.  The
+// guard steps make every index in [-kGuard, T + kGuard) readable, so the tail
+// of a phase needs no clamping (its values are never used).
+__device__ __forceinline__ void load_chunk(const ChainCtx& c, Prefetch& p, int t0, int dir,
+                                           bool with_s) {
+  int code[kChunk];
+#pragma unroll
+  for (int j = 0; j < kChunk; j++) {
+    const int t = t0 + dir * j;
+    code[j] = c.codes[t];
+    if (with_s) p.s[j] = c.Sload[(long)t * 16];
+  }
+#pragma unroll
+  for (int j = 0; j < kChunk; j++) p.e[j] = c.Et[code[j] * 16];
+}
+
+// n wave-uniform steps with one-chunk-ahead ping-pong prefetch.
+template <typename Step>
+__device__ __forceinline__ void run_phase(const ChainCtx& c, int n, int t0, int dir,
+                                          bool with_s, Step&& step) {
+  Prefetch pa, pb;
+  if (n <= 0) return;
+  load_chunk(c, pa, t0, dir, with_s);
+  for (int base = 0; base < n; base += 2 * kChunk) {
+    load_chunk(c, pb, t0 + dir * (base + kChunk), dir, with_s);
+#pragma unroll
+    for (int j = 0; j < kChunk; j++)
+      if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], j);
+    if (base + kChunk >= n) break;
+    load_chunk(c, pa, t0 + dir * (base + 2 * kChunk), dir, with_s);
+#pragma unroll
+    for (int j = 0; j < kChunk; j++)
+      if (base + kChunk + j < n) step(t0 + dir * (base + kChunk + j), pb.e[j], pb.s[j], j);
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kThreads, 2)
 void chain_fb_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* Et = reinterpret_cast<double*>(smem);                       // [(M+2)][16]
-  uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);    // [8][T]
+  uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);    // [8][Tr]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int y = lane & 15, row = lane >> 4;
-  const bool fwd = wave < 2;
-  const int chain = (wave & 1) * 4 + row;
+  const bool fwd = row < 2;                       // per row (lane-varying)
+  const int seq = wave * 2 + (row & 1);           // 0..7 within the block
   const long b0 = (long)blockIdx.x * kChainsPerBlock;
-  const long b = b0 + chain;
+  const long b = b0 + seq;
   const bool active = b < a.B;
   const int T = a.T, H = a.H;
+  const int Tr = chain_codes_row(T);              // kGuard + T rounded + kGuard
 
   // --- stage the evidence table and this block's observation codes in LDS
   for (int i = tid; i < (a.M + 2) * 16; i += kThreads) Et[i] = a.Etab[i];
-  for (long i = tid; i < (long)kChainsPerBlock * T; i += kThreads) {
-    const int c = (int)(i / T), t = (int)(i - (long)c * T);
-    int code = a.M;                                      // missing
-    if (b0 + c < a.B && a.obs) {
-      const int o = a.obs[(b0 + c) * a.obs_bstride + (long)t * a.obs_tstride + a.obs_col];
-      code = o < 0 ? a.M : (o < a.M ? o : a.M + 1);
-    }
-    codes[c * T + t] = (uint8_t)code;
-  }
-
-  // --- per-lane coefficients: column (fwd) / row (bwd) of A, rotated to
-  //     match the row_gather order
-  int src[16];
-  row_sources(y, src);
-  double C[16], TS[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    C[k] = fwd ? a.A[src[k] * 16 + y] : a.A[y * 16 + src[k]];
-    TS[k] = a.ts[src[k]];
-  }
+  const int nseq = (int)((a.B - b0) < kChainsPerBlock ? (a.B - b0) : kChainsPerBlock);
+  auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
+  for (int i = tid; i < kChainsPerBlock * Tr; i += kThreads) codes[i] = (uint8_t)a.M;  // missing / guard
   __syncthreads();
-
-  const uint8_t* mycodes = codes + chain * T;
-  double* Sb = a.S + (size_t)(active ? b : 0) * T * 16;
-  double* Pb = a.post + (size_t)(active ? b : 0) * a.post_bstride;
-  const bool ystore = active && y < a.N;
-
-  // forward state
-  double vin[16];          // gathered input vector (alpha_{t-1}, scaled)
-  int sc = 0;              // pending power-of-two scale for the next mat-vec
-  double m2 = 1.0, m1 = 1.0;
-  int e2 = 0, e1 = 0;
-  bool dead = false;
-
-  if (fwd) {
-    const double p = a.pi[y];
-    row_gather(p, vin);
-  } else {
-    // beta_{T-1} = 1 on the real states; g = e_{T-1} o beta
-    const double beta = y < a.N ? 1.0 : 0.0;
-    if (active && T - 1 >= H) Sb[(size_t)(T - 1) * 16 + y] = beta;
-    const double g = Et[mycodes[T - 1] * 16 + y] * beta;
-    const double s = row_sum(g);
-    sc = -exp2_of(s);
-    row_gather(g, vin);
+  if (a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kChainsPerBlock) {
+    // contiguous [8][T] int32 block: 16-byte loads, all issued before use
+    const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * (long)T);
+    const int n4 = (kChainsPerBlock * T) >> 2;
+    for (int i0 = tid; i0 < n4; i0 += kThreads * 8) {
+      int4 r[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) if (i0 + k * kThreads < n4) r[k] = src[i0 + k * kThreads];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i4 = i0 + k * kThreads;
+        if (i4 < n4) {
+          const int i = i4 << 2, c = i / T, t = i - c * T;
+          const uint32_t packed = (uint32_t)code_of(r[k].x) | ((uint32_t)code_of(r[k].y) << 8) |
+                                  ((uint32_t)code_of(r[k].z) << 16) | ((uint32_t)code_of(r[k].w) << 24);
+          *reinterpret_cast<uint32_t*>(codes + c * Tr + kGuard + t) = packed;
+        }
+      }
+    }
+  } else if (a.obs) {
+    for (int i = tid; i < nseq * T; i += kThreads) {
+      const int c = i / T, t = i - c * T;
+      codes[c * Tr + kGuard + t] =
+          (uint8_t)code_of(a.obs[(b0 + c) * a.obs_bstride + (long)t * a.obs_tstride + a.obs_col]);
+    }
   }
 
-  // one forward step producing alpha_t; combine with beta_t when `combine`
-  auto fstep = [&](int t, bool combine) {
-    const double e = Et[mycodes[t] * 16 + y];
-    double bt = 0.0;
-    if (combine && active) bt = Sb[(size_t)t * 16 + y];
-    const double u = __builtin_ldexp(dot16(vin, C), sc);
-    const double z1 = __builtin_ldexp(dot16(vin, TS), sc);
-    const double v = u * e;
-    const double z2 = row_sum(v);
+  double C[16];   // fwd rows: column y of A (C[k] = A[k][y]); bwd rows: row y (A[y][k])
+#pragma unroll
+  for (int k = 0; k < 16; k++) C[k] = fwd ? a.A[k * 16 + y] : a.A[y * 16 + k];
+  __syncthreads();
+  const double s_y = Et[a.M * 16 + y];                    // sum_m E[y][m]
+
+  // per-lane pointers; lanes that must not write get a sink with stride 0
+  double* const sink = a.S + (size_t)(a.B + 1) * chain_scratch_row(T) + y;
+  double* const Srow = a.S + (size_t)(active ? b : 0) * chain_scratch_row(T) + (size_t)kGuard * 16 + y;
+  const bool ystore = active && y < a.N && a.post;
+  ChainCtx cx;
+  cx.Et = Et + y;
+  cx.codes = codes + seq * Tr + kGuard;
+  cx.Sload = Srow;
+  cx.Sstore = active ? Srow : sink;
+  cx.Sstride = active ? 16 : 0;
+  cx.Pstore = ystore ? a.post + (size_t)b * a.post_bstride + a.post_off + y : sink;
+  cx.Pstride = ystore ? a.post_tstride : 0;
+
+  // chain state: x = this lane's entry of the next mat-vec input
+  //   fwd: alpha_{t-1} (starts at the prior of prev, nip.c:1431 use_priors)
+  //   bwd: g_{t+1} = e_{t+1} o beta_{t+1}  (starts at e_{T-1} o 1)
+  double x;
+  int sc = 0;
+  double m2 = 1.0, m1 = 1.0;   // fwd: running products of m2 / m1 (mantissas)
+  int e2 = 0, e1 = 0;          //      and their binary exponents
+  bool dead = false;
+  if (fwd) {
+    x = a.pi[y];
+  } else {
+    const double beta = y < a.N ? 1.0 : 0.0;
+    cx.Sstore[(long)(T - 1) * cx.Sstride] = beta;        // beta_{T-1}; T-1 >= H
+    x = Et[cx.codes[T - 1] * 16 + y] * beta;
+  }
+  {
+    const int k = exp2_of(row_sum(x));
+    if (!fwd) sc = -k;
+  }
+
+  // One step of either direction, branch-free.  u = A^T x (fwd) or A x (bwd),
+  // scaled; p = e o u.  fwd: alpha_t = p;  bwd: beta_t = u, next input p.
+  auto step = [&](int t, double e, double other, bool combine, int j) {
+    const double u = __builtin_ldexp(dot_bcast(x, C), sc);
+    const double p = u * e;
+    const double keep = fwd ? p : u;                 // interface vector at time t
+    const double z2 = row_sum(p);                    // fwd: m2 ; bwd: scale
+#ifdef NIPAMD_ABLATE_NO_LL
+    const double z1 = 0.0;
+#else
+    const double z1 = row_sum(u * s_y);              // fwd: m1
+#endif
+#ifdef NIPAMD_ABLATE_NO_STORE     // timing-only ablation build (wrong results)
+    if (0) {
+#else
     if (!combine) {
-      if (active) Sb[(size_t)t * 16 + y] = v;
+#endif
+      cx.Sstore[(long)t * cx.Sstride] = keep;
     } else {
-      const double pr = v * bt;
-      const double c = row_sum(pr);
-      if (ystore) Pb[(size_t)t * a.post_tstride + a.post_off + y] = c != 0.0 ? pr / c : pr;
+      const double pr = keep * other;
+#ifdef NIPAMD_ABLATE_NO_POSTNORM
+      cx.Pstore[(long)t * cx.Pstride] = pr;
+#else
+      cx.Pstore[(long)t * cx.Pstride] = div_by(pr, row_sum(pr));
+#endif
     }
-    // ll: product of z2 / product of z1, as mantissa * 2^exponent
+#ifndef NIPAMD_ABLATE_NO_LL
     dead |= (z2 == 0.0);
     m2 *= z2; m1 *= z1;
-    { const int k2 = exp2_of(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2; }
-    { const int k1 = exp2_of(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1; }
-    sc = -exp2_of(z2);
-    row_gather(v, vin);
-  };
-
-  // one backward step producing beta_{t} from g_{t+1}; combine with alpha_t
-  auto bstep = [&](int t, bool combine) {
-    const double e = Et[mycodes[t] * 16 + y];
-    double at = 0.0;
-    if (combine && active) at = Sb[(size_t)t * 16 + y];
-    const double w = __builtin_ldexp(dot16(vin, C), sc);   // beta_t (scaled)
-    if (!combine) {
-      if (active) Sb[(size_t)t * 16 + y] = w;
-    } else {
-      const double pr = at * w;
-      const double c = row_sum(pr);
-      if (ystore) Pb[(size_t)t * a.post_tstride + a.post_off + y] = c != 0.0 ? pr / c : pr;
+    if ((j & 3) == 3) {                              // renormalise every 4 steps
+      const int k2 = exp2_of(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+      const int k1 = exp2_of(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
     }
-    const double g = e * w;
-    const double s = row_sum(g);
-    sc = -exp2_of(s);
-    row_gather(g, vin);
+#endif
+    sc = -exp2_of(z2);
+    x = p;
   };
 
-  // ---------------- phase A
-  if (fwd) {
-    for (int t = 0; t < H; t++) fstep(t, false);
-  } else {
-    for (int t = T - 2; t >= H; t--) bstep(t, false);
+  const int dir = fwd ? 1 : -1;
+  // phase A: fwd t = 0..H-1 ; bwd t = T-2 .. H  (bwd has one step fewer for even T)
+  {
+    const int nf = H, nb = T - 1 - H, n = nf < nb ? nf : nb;
+    const int t0 = fwd ? 0 : T - 2;
+    run_phase(cx, n, t0, dir, false, [&](int t, double e, double o, int j) { step(t, e, o, false, j); });
+    if (nf != nb && (fwd ? nf : nb) > n) {             // peeled tail: rows with one more step
+      const int t = t0 + dir * n;
+      step(t, cx.Et[cx.codes[t] * 16], 0.0, false, 3);
+    }
   }
-
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-
-  // ---------------- phase B
-  if (fwd) {
-    for (int t = H; t < T; t++) fstep(t, true);
-    if (active && y == 0) {
-      double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
-      if (dead) ll = -DBL_MAX;
-      if (a.ll) a.ll[b] = ll;
-      if (a.status) a.status[b] = dead ? 1u : 0u;
+  // phase B: fwd t = H..T-1 combined with beta_t ; bwd t = H-1..0 combined with alpha_t
+  {
+    const int nf = T - H, nb = H, n = nf < nb ? nf : nb;
+    const int t0 = fwd ? H : H - 1;
+    run_phase(cx, n, t0, dir, true, [&](int t, double e, double o, int j) { step(t, e, o, true, j); });
+    if (nf != nb && (fwd ? nf : nb) > n) {
+      const int t = t0 + dir * n;
+      step(t, cx.Et[cx.codes[t] * 16], cx.Sload[(long)t * 16], true, 3);
     }
-  } else {
-    // beta_{T-1} itself may belong to phase B (only when T == 1, H == 0 ...
-    // handled by the forward side reading S[T-1]); continue from H-1 down
-    for (int t = (T - 2 < H - 1 ? T - 2 : H - 1); t >= 0; t--) bstep(t, true);
+  }
+  if (fwd && active && y == 0) {
+    double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 1u : 0u;
   }
 }
 
 size_t chain_fb_lds_bytes(int M, int T) {
-  return (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kChainsPerBlock * T;
+  return (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kChainsPerBlock * chain_codes_row(T);
 }
 
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream) {

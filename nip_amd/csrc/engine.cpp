@@ -248,7 +248,7 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   if (nipamd::chain_fb_lds_bytes(P.M, T) > 96 * 1024)
     return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
   if (int rc = ensure_tables(mm)) return rc;
-  if (int rc = ensure_scratch(mm, (size_t)B * T * 16 * sizeof(double))) return rc;
+  if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes(B, T))) return rc;
   DevState* d = dev_of(mm);
   nipamd::ChainArgs a{};
   a.obs = d_obs;
