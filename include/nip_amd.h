@@ -96,6 +96,18 @@ int nipamd_model_var_card(const nipamd_model* m, int v);
  */
 int nipamd_model_desc_json(const nipamd_model* m, char* buf, int cap);
 
+/*
+ * Clique array of an explicit DAG through the join-tree compiler alone
+ * (moralise, triangulate: src/nipgraph.c:325-351, 443-515).  edges [2*n_edges]
+ * are (parent, child) node indices; set_parents = 0 reproduces graphs built
+ * without parent lists (test/graphtest.c:182-230).  clique_off [ncliques+1]
+ * CSR offsets into clique_vars (at most cap entries written).  Returns the
+ * number of cliques, or a negated NIP_ERROR_* code (clique_off must hold
+ * n+1 entries).
+ */
+int nipamd_graph_cliques(int n, const int* card, int n_edges, const int* edges,
+                         int set_parents, int* clique_off, int* clique_vars, int cap);
+
 /* Size of the em_learn parameter layout (src/nip.c:2101-2128): for every
  * variable, a table with the child as dimension 0, then v->parents order. */
 int nipamd_model_param_size(const nipamd_model* m);

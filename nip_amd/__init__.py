@@ -44,6 +44,7 @@ EXPORTS = [
     "nipamd_model_desc_json", "nipamd_model_param_size", "nipamd_model_gpu_supported",
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
+    "nipamd_graph_cliques",
 ]
 
 
@@ -85,6 +86,7 @@ def lib():
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
         L.nipamd_model_prior.argtypes = [vp, C.c_int, dp]
         L.nipamd_last_error.restype = C.c_char_p
+        L.nipamd_graph_cliques.argtypes = [C.c_int, ip, C.c_int, ip, C.c_int, ip, ip, C.c_int]
         _lib = L
     return _lib
 
@@ -187,6 +189,20 @@ class Model:
         assert p.size == self.param_size()
         _check(lib().nipamd_m_step(self._h, p.ctypes.data_as(C.POINTER(C.c_double))))
         self._desc = None
+
+
+def graph_cliques(card, edges, set_parents=True):
+    """Clique array of a DAG through the join-tree compiler (index contract)."""
+    n = len(card)
+    flat = [x for e in edges for x in e]
+    off = (C.c_int * (n + 1))()
+    cap = n * n
+    out = (C.c_int * cap)()
+    nc = lib().nipamd_graph_cliques(n, _ints(card), len(edges), _ints(flat), int(set_parents),
+                                    off, out, cap)
+    if nc < 0:
+        raise NipError(-nc, lib().nipamd_last_error().decode())
+    return [[out[j] for j in range(off[i], off[i + 1])] for i in range(nc)]
 
 
 def parse_model(path: str) -> Model:

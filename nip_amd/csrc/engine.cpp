@@ -226,6 +226,25 @@ int nipamd_model_prior(const nipamd_model* mm, int v, double* out) {
   return (int)var.prior.size();
 }
 
+int nipamd_graph_cliques(int n, const int* card, int n_edges, const int* edges,
+                         int set_parents, int* clique_off, int* clique_vars, int cap) {
+  if (n <= 0 || !card || (n_edges > 0 && !edges) || !clique_off) return -NIP_ERROR_INVALID_ARGUMENT;
+  std::vector<int> cd(card, card + n);
+  std::vector<std::pair<int, int>> e;
+  for (int i = 0; i < n_edges; i++) e.emplace_back(edges[2 * i], edges[2 * i + 1]);
+  std::vector<std::vector<int>> cl;
+  std::string err;
+  int nc = nipamd::compile_graph_only(n, cd, e, set_parents != 0, cl, err);
+  if (nc < 0) { g_err = err; return -NIP_ERROR_GENERAL; }
+  int pos = 0;
+  clique_off[0] = 0;
+  for (int c = 0; c < nc; c++) {
+    for (int v : cl[c]) { if (clique_vars && pos < cap) clique_vars[pos] = v; pos++; }
+    clique_off[c + 1] = pos;
+  }
+  return nc;
+}
+
 int nipamd_m_step(nipamd_model* mm, const double* params) {
   if (!mm || !params) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   int rc = nipamd::m_step(mm->m, params);

@@ -139,6 +139,7 @@ class PortOracle:
                                 _f64p, C.c_double, C.c_int, _f64p]
             L.no_original.argtypes = [C.c_void_p, C.c_int, _f64p, C.c_int]
             L.no_prior.argtypes = [C.c_void_p, C.c_int, _f64p]
+            L.no_query.argtypes = [C.c_void_p, C.c_int, C.c_int, _i32p, _f64p, C.c_int, _f64p]
             cls._lib = L
         return cls._lib
 
@@ -214,6 +215,15 @@ class PortOracle:
         n = self.lib().no_prior(self.h, v, out)
         return out if n else None
 
+    def query(self, root, evidence, q):
+        """evidence: {var: vector}; marginal of q after propagation from root."""
+        ev_vars = np.array(list(evidence.keys()), np.int32)
+        ev = np.concatenate([np.asarray(evidence[v], np.float64) for v in evidence]) \
+            if evidence else np.zeros(1)
+        out = np.zeros(self.desc["vars"][q]["card"])
+        self.lib().no_query(self.h, root, len(ev_vars), ev_vars, np.ascontiguousarray(ev), q, out)
+        return out
+
 
 class RefHarness:
     """The reference's own compiled code (oracle/_ref/libnipref.so)."""
@@ -239,6 +249,8 @@ class RefHarness:
                                 _f64p, C.c_double, C.c_int, _f64p]
             L.nh_clique_original.argtypes = [C.c_int, C.c_int, _f64p, C.c_int]
             L.nh_prior.argtypes = [C.c_int, C.c_int, _f64p]
+            L.nh_graph_cliques.argtypes = [C.c_int, _i32p, C.c_int, _i32p, C.c_int, _i32p,
+                                           _i32p, C.c_int]
             cls._lib = L
         return cls._lib
 
@@ -300,3 +312,15 @@ class RefHarness:
         out = np.zeros(self.desc["vars"][v]["card"])
         n = self.lib().nh_prior(self.h, v, out)
         return out if n else None
+
+
+def ref_graph_cliques(card, edges, set_parents=True):
+    """Cliques of a DAG through the reference's own triangulation."""
+    L = RefHarness.lib()
+    n = len(card)
+    off = np.zeros(n + 1, np.int32)
+    out = np.zeros(n * n, np.int32)
+    flat = np.array([x for e in edges for x in e] or [0], np.int32)
+    nc = L.nh_graph_cliques(n, np.asarray(card, np.int32), len(edges), flat, int(set_parents),
+                            off, out, n * n)
+    return [list(out[off[i]:off[i + 1]]) for i in range(nc)]

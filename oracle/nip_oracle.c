@@ -635,3 +635,27 @@ int no_prior(void* mm, int v, double* out){
   memcpy(out, m->prior[v], sizeof(double) * m->d.card[v]);
   return m->d.card[v];
 }
+
+/*
+ * Soft-evidence query on a hand-built join tree, the procedure of the
+ * reference's test/cliquetest.c:182-213: enter each evidence vector
+ * (nip_enter_evidence), collect and distribute from `root`, then the
+ * normalised marginal of q from its family clique.
+ */
+int no_query(void* mm, int root, int nev, const int* ev_vars, const double* ev,
+             int q, double* out){
+  model* m = (model*) mm;
+  int v, i, off = 0;
+  for(v = 0; v < m->d.nvars; v++){
+    for(i = 0; i < m->d.card[v]; i++) m->lik[v][i] = 1;
+  }
+  global_retraction(m);
+  for(i = 0; i < nev; i++){
+    enter_evidence(m, ev_vars[i], ev + off);
+    off += m->d.card[ev_vars[i]];
+  }
+  unmark(m); collect(m, -1, -1, root);
+  unmark(m); distribute(m, root);
+  write_result(m, q, out);
+  return 0;
+}

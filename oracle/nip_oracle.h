@@ -63,5 +63,7 @@ int no_em(void* m, int ns, int T, int nobs, const int* obs_vars, const int* obs,
           const double* init, double threshold, int max_iter, double* curve);
 int no_original(void* m, int c, double* out, int cap);
 int no_prior(void* m, int v, double* out);
+int no_query(void* m, int root, int nev, const int* ev_vars, const double* ev,
+             int q, double* out);
 
 #endif

@@ -793,3 +793,49 @@ int nh_prior(int h, int v, double* out){
   memcpy(out, var->prior, sizeof(double) * var->cardinality);
   return var->cardinality;
 }
+
+/*
+ * Cliques of an explicit graph through the reference's own triangulation
+ * (nip_moralise_graph, nip_make_graph_undirected, nip_triangulate_graph --
+ * the sequence of test/graphtest.c:182-230 Test 6/7).  edges: [2*ne]
+ * (parent, child).  With set_parents == 0 the variables carry no parent lists,
+ * exactly as graphtest builds them.  out: clique variable lists (node
+ * indices), CSR offsets in off[ncliques+1].  Returns ncliques.
+ */
+int nh_graph_cliques(int n, const int* card, int ne, const int* edges, int set_parents,
+                     int* off, int* out, int cap){
+  nip_variable* v = (nip_variable*) calloc(n, sizeof(nip_variable));
+  nip_graph g, gm, gu;
+  nip_clique* cl;
+  char* st[256];
+  int i, j, k, nc, pos = 0;
+  for(i = 0; i < 256; i++){ st[i] = (char*) malloc(8); snprintf(st[i], 8, "%d", i); }
+  for(i = 0; i < n; i++){
+    char sym[16]; snprintf(sym, 16, "G%d", i);
+    v[i] = nip_new_variable(sym, "", st, card[i]);
+  }
+  g = nip_new_graph(n);
+  for(i = 0; i < n; i++) nip_graph_add_node(g, v[i]);
+  for(i = 0; i < ne; i++) nip_graph_add_child(g, v[edges[2*i]], v[edges[2*i+1]]);
+  if(set_parents){
+    for(i = 0; i < n; i++){
+      nip_variable par[64]; int np = 0;
+      for(j = 0; j < ne; j++) if(edges[2*j+1] == i) par[np++] = v[edges[2*j]];
+      if(np) nip_set_parents(v[i], par, np);
+    }
+  }
+  gm = nip_moralise_graph(g);
+  gu = nip_make_graph_undirected(gm);
+  nc = nip_triangulate_graph(gu, &cl);
+  off[0] = 0;
+  for(i = 0; i < nc; i++){
+    for(j = 0; j < NIP_DIMENSIONALITY(cl[i]->p); j++){
+      for(k = 0; k < n; k++) if(cl[i]->variables[j] == v[k]) break;
+      if(pos < cap) out[pos] = k;
+      pos++;
+    }
+    off[i + 1] = pos;
+  }
+  for(i = 0; i < 256; i++) free(st[i]);
+  return nc;
+}
