@@ -41,7 +41,8 @@ extern "C" {
 
 /* Per-sequence status bits written by the batched entry points. */
 #define NIPAMD_STATUS_ZERO_MASS    1u  /* some m2 == 0: ll = -DBL_MAX (src/nip.c:1471-1473) */
-#define NIPAMD_STATUS_BAD_LUCK     2u  /* e_step's m1<=0 || m2<=0 || ll>0 (src/nip.c:1827-1854) */
+#define NIPAMD_STATUS_BAD_LUCK     2u  /* e_step's m1<=0 || m2<=0 || ll>0 (src/nip.c:1827-1854);
+                                          nipamd_estep sets ZERO_MASS|BAD_LUCK */
 
 typedef struct nipamd_model nipamd_model;
 
@@ -156,6 +157,24 @@ int nipamd_fb_host(nipamd_model* m, const int32_t* obs, int n_obs,
 int nipamd_estep(nipamd_model* m, const int32_t* d_obs, int n_obs,
                  const int* obs_vars, int B, int T, double* d_counts,
                  double* d_ll, uint32_t* d_status, void* stream);
+
+/*
+ * The two halves of nipamd_estep, for data-parallel EM (one process per GPU,
+ * util/niptrain.c:142-195 over a sharded sequence set):
+ *   nipamd_estep_partial  B sequences -> d_partial [nipamd_estep_partial_size]
+ *                         (overwritten): the fixed-order binary-tree sum of the
+ *                         per-sequence count slabs, before the model's tables
+ *                         are applied.  Partials of power-of-two shards combine
+ *                         (pairwise, in rank order) into exactly the partial of
+ *                         the whole batch.
+ *   nipamd_estep_finalize d_counts += the e_step families of a partial.
+ */
+int nipamd_estep_partial_size(const nipamd_model* m);
+int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,
+                         const int* obs_vars, int B, int T, double* d_partial,
+                         double* d_ll, uint32_t* d_status, void* stream);
+int nipamd_estep_finalize(nipamd_model* m, const double* d_partial,
+                          double* d_counts, void* stream);
 
 /* m_step() (src/nip.c:2010-2071): normalise params (host, em_learn layout)
  * and re-initialise the model's tables and priors from them. */

@@ -19,7 +19,8 @@ import numpy as np
 from . import build as _build
 
 __all__ = ["NipError", "Model", "parse_model", "lib", "forward_backward_inference",
-           "forward_backward_inference_host", "LIB_PATH"]
+           "forward_backward_inference_host", "e_step", "estep_partial", "estep_finalize",
+           "em_learn", "LIB_PATH"]
 
 LIB_PATH = os.environ.get("NIPAMD_LIB", _build.LIB)
 
@@ -44,7 +45,8 @@ EXPORTS = [
     "nipamd_model_desc_json", "nipamd_model_param_size", "nipamd_model_gpu_supported",
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
-    "nipamd_graph_cliques",
+    "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
+    "nipamd_estep_finalize",
 ]
 
 
@@ -82,6 +84,9 @@ def lib():
         L.nipamd_fb_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, ip,
                                      vp, vp, vp]
         L.nipamd_estep.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
+        L.nipamd_estep_partial_size.argtypes = [vp]
+        L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
+        L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
         L.nipamd_m_step.argtypes = [vp, dp]
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
         L.nipamd_model_prior.argtypes = [vp, C.c_int, dp]
@@ -263,3 +268,70 @@ def forward_backward_inference_host(model: Model, obs, obs_vars, query):
                                 B, T, len(query), _ints(query), post.ctypes.data_as(C.c_void_p),
                                 ll.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
     return post, ll, status
+
+
+def _obs3(obs, obs_vars):
+    import torch
+    if obs.dim() == 2:
+        obs = obs.unsqueeze(-1)
+    assert obs.dtype == torch.int32 and obs.is_cuda and obs.is_contiguous()
+    assert obs.shape[2] == len(obs_vars)
+    return obs
+
+
+def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=None, stream=None):
+    """First half of the batched e_step (src/nip.c:1708): the fixed-order tree
+    sum of the per-sequence count slabs of obs [B, T, n_obs] (CUDA int32).
+    Returns (partial [partial_size] float64, ll [B], status [B]) on the GPU."""
+    import torch
+    obs = _obs3(obs, obs_vars)
+    B, T, nobs = obs.shape
+    S = lib().nipamd_estep_partial_size(model._h)
+    if S < 0:
+        raise NipError(NIPAMD_ERROR_UNSUPPORTED, "model has no GPU e_step plan")
+    dev = obs.device
+    if partial is None:
+        partial = torch.empty((S,), dtype=torch.float64, device=dev)
+    if ll is None:
+        ll = torch.empty((B,), dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    _check(lib().nipamd_estep_partial(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars),
+                                      B, T, C.c_void_p(partial.data_ptr()), C.c_void_p(ll.data_ptr()),
+                                      C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
+    return partial, ll, status
+
+
+def estep_finalize(model: Model, partial, counts, stream=None):
+    """counts (CUDA float64 [param_size], em_learn layout) += families of partial."""
+    assert counts.is_cuda and counts.numel() == model.param_size()
+    _check(lib().nipamd_estep_finalize(model._h, C.c_void_p(partial.data_ptr()),
+                                       C.c_void_p(counts.data_ptr()), _stream_ptr(stream)))
+    return counts
+
+
+def e_step(model: Model, obs, obs_vars, counts=None, ll=None, status=None, stream=None):
+    """Batched e_step() (src/nip.c:1708-2007) of B sequences on the GPU.
+
+    counts: CUDA float64 [param_size] accumulated into (default: ones, the
+    em_learn pseudo-counts of nip.c:2172).  Returns (counts, ll [B], status [B]);
+    status bit NIPAMD_STATUS_BAD_LUCK marks the sequences for which the
+    reference's e_step returns NIP_ERROR_BAD_LUCK.
+    """
+    import torch
+    obs = _obs3(obs, obs_vars)
+    B, T, nobs = obs.shape
+    dev = obs.device
+    if counts is None:
+        counts = torch.ones((model.param_size(),), dtype=torch.float64, device=dev)
+    if ll is None:
+        ll = torch.empty((B,), dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    _check(lib().nipamd_estep(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
+                              C.c_void_p(counts.data_ptr()), C.c_void_p(ll.data_ptr()),
+                              C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
+    return counts, ll, status
+
+
+from .em import em_learn  # noqa: E402

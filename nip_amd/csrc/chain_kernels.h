@@ -24,7 +24,7 @@ struct ChainArgs {
   int post_off;          // offset of the variable's block within a step
   double* ll;            // [B] or nullptr
   unsigned* status;      // [B] or nullptr
-  double* counts;        // E-step only: per-block partial counts
+  double* counts;        // E-step only: per-sequence slabs [B][chain_estep_slab(M)]
 };
 
 // Scratch layout: per sequence kGuard + T + kGuard steps of 16 doubles
@@ -35,7 +35,24 @@ __host__ __device__ inline long chain_scratch_row(int T) { return (long)(T + 2 *
 __host__ __device__ inline int chain_codes_row(int T) { return ((T + 7) & ~7) + 2 * kScratchGuard; }
 inline size_t chain_scratch_bytes(long B, int T) { return (size_t)(B + 2) * chain_scratch_row(T) * sizeof(double); }
 
-size_t chain_fb_lds_bytes(int M, int T);
+// E-step per-sequence slab (doubles): Kf[16][16], Kb[16][16] (xi sums of the
+// forward / backward rows, without the A factor), H[2][M+2][16] (M1 count
+// tables of the two rows), P0[16].
+constexpr int kSlabKf = 0, kSlabKb = 256, kSlabH = 512;
+__host__ __device__ inline int chain_estep_slab(int M) { return 512 + 2 * (M + 2) * 16 + 16; }
+__host__ __device__ inline int chain_slab_p0(int M) { return 512 + 2 * (M + 2) * 16; }
+
+struct ChainFinalize {
+  int N, M;
+  int off_prev, off_cur, off_obs;   // em_learn layout offsets of the three families
+  const double* A;                  // [16][16]
+  const double* Etab;               // [(M+2)][16]
+};
+
+size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
+int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
+int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
+int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
 
 }  // namespace nipamd

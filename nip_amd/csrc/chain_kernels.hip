@@ -87,6 +87,18 @@ __device__ __forceinline__ double dot_bcast(double x, const double (&c)[16]) {
   return (a0 + a1) + (a2 + a3);
 }
 
+// K[k] += (value of lane k of this row) * w, k = 0..15 (E-step outer products)
+__device__ __forceinline__ void acc_bcast(double (&K)[16], double x, double w) {
+  fmac_bcast<0, true>(K[0], x, w);    fmac_bcast<1, false>(K[1], x, w);
+  fmac_bcast<2, false>(K[2], x, w);   fmac_bcast<3, false>(K[3], x, w);
+  fmac_bcast<4, false>(K[4], x, w);   fmac_bcast<5, false>(K[5], x, w);
+  fmac_bcast<6, false>(K[6], x, w);   fmac_bcast<7, false>(K[7], x, w);
+  fmac_bcast<8, false>(K[8], x, w);   fmac_bcast<9, false>(K[9], x, w);
+  fmac_bcast<10, false>(K[10], x, w); fmac_bcast<11, false>(K[11], x, w);
+  fmac_bcast<12, false>(K[12], x, w); fmac_bcast<13, false>(K[13], x, w);
+  fmac_bcast<14, false>(K[14], x, w); fmac_bcast<15, false>(K[15], x, w);
+}
+
 // Sum over the 16 lanes of the row; identical bits in every lane (each level
 // pairs lanes whose partial sums are equal, and IEEE addition commutes).
 __device__ __forceinline__ double row_sum(double x) {
@@ -125,6 +137,7 @@ constexpr int kChunk = 8;   // steps per unrolled chunk; prefetch distance = 1 c
 struct Prefetch {
   double e[kChunk];
   double s[kChunk];
+  int c[kChunk];       // observation codes (E-step: M1 count row)
 };
 
 }  // namespace
@@ -164,7 +177,7 @@ __device__ __forceinline__ void load_chunk(const ChainCtx& c, Prefetch& p, int t
     if (with_s) p.s[j] = c.Sload[(long)t * 16];
   }
 #pragma unroll
-  for (int j = 0; j < kChunk; j++) p.e[j] = c.Et[code[j] * 16];
+  for (int j = 0; j < kChunk; j++) { p.e[j] = c.Et[code[j] * 16]; p.c[j] = code[j]; }
 }
 
 // n wave-uniform steps with one-chunk-ahead ping-pong prefetch.
@@ -178,22 +191,29 @@ __device__ __forceinline__ void run_phase(const ChainCtx& c, int n, int t0, int 
     load_chunk(c, pb, t0 + dir * (base + kChunk), dir, with_s);
 #pragma unroll
     for (int j = 0; j < kChunk; j++)
-      if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], j);
+      if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], pa.c[j], j);
     if (base + kChunk >= n) break;
     load_chunk(c, pa, t0 + dir * (base + 2 * kChunk), dir, with_s);
 #pragma unroll
     for (int j = 0; j < kChunk; j++)
-      if (base + kChunk + j < n) step(t0 + dir * (base + kChunk + j), pb.e[j], pb.s[j], j);
+      if (base + kChunk + j < n) step(t0 + dir * (base + kChunk + j), pb.e[j], pb.s[j], pb.c[j], j);
   }
 }
 
 }  // namespace
 
+// ESTEP = false: forward_backward_inference (posteriors + ll).
+// ESTEP = true:  e_step (nip.c:1708-2007): the same two filters; phase B
+// accumulates the expected counts of every family (see chain_estep_slab).
+template <bool ESTEP>
 __global__ __launch_bounds__(kThreads, 2)
-void chain_fb_kernel(ChainArgs a) {
+void chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* Et = reinterpret_cast<double*>(smem);                       // [(M+2)][16]
   uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);    // [8][Tr]
+  // E-step: per (sequence, direction) M1 count tables [(M+2)][16], lane-owned
+  double* Htab = reinterpret_cast<double*>(
+      codes + (((size_t)kChainsPerBlock * chain_codes_row(a.T) + 15) & ~(size_t)15));
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -211,6 +231,8 @@ void chain_fb_kernel(ChainArgs a) {
   const int nseq = (int)((a.B - b0) < kChainsPerBlock ? (a.B - b0) : kChainsPerBlock);
   auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
   for (int i = tid; i < kChainsPerBlock * Tr; i += kThreads) codes[i] = (uint8_t)a.M;  // missing / guard
+  if (ESTEP)
+    for (int i = tid; i < kChainsPerBlock * 2 * (a.M + 2) * 16; i += kThreads) Htab[i] = 0.0;
   __syncthreads();
   if (a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kChainsPerBlock) {
     // contiguous [8][T] int32 block: 16-byte loads, all issued before use
@@ -278,9 +300,17 @@ void chain_fb_kernel(ChainArgs a) {
     if (!fwd) sc = -k;
   }
 
+  // E-step accumulators.  K[k]: fwd rows (lane y) sum xi(x=k, y); bwd rows
+  // (lane x) sum xi(x, y=k) -- both without the A(x,y) factor, applied once
+  // after the batch reduction.  Hrow: this chain's M1 count table column y.
+  double K[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) K[k] = 0.0;
+  double* Hrow = Htab + ((size_t)(seq * 2 + (fwd ? 0 : 1)) * (a.M + 2)) * 16 + y;
+
   // One step of either direction, branch-free.  u = A^T x (fwd) or A x (bwd),
   // scaled; p = e o u.  fwd: alpha_t = p;  bwd: beta_t = u, next input p.
-  auto step = [&](int t, double e, double other, bool combine, int j) {
+  auto step = [&](int t, double e, double other, int code, bool combine, int j) {
     const double u = __builtin_ldexp(dot_bcast(x, C), sc);
     const double p = u * e;
     const double keep = fwd ? p : u;                 // interface vector at time t
@@ -296,13 +326,26 @@ void chain_fb_kernel(ChainArgs a) {
     if (!combine) {
 #endif
       cx.Sstore[(long)t * cx.Sstride] = keep;
-    } else {
+    } else if (!ESTEP) {
       const double pr = keep * other;
 #ifdef NIPAMD_ABLATE_NO_POSTNORM
       cx.Pstore[(long)t * cx.Pstride] = pr;
 #else
       cx.Pstore[(long)t * cx.Pstride] = div_by(pr, row_sum(pr));
 #endif
+    } else {
+      // e_step families at time t (nip.c:1925-1967), normalised by c_t:
+      //   M1:  post_t(y) at row = observation code (missing -> row M, folded
+      //        into E[y][m]/s(y) after the reduction; invalid -> row M+1)
+      //   P1:  xi_t(x,y) = alpha_{t-1}(x) A(x,y) e_t(y) beta_t(y) / c_t   (fwd, t >= H)
+      //        xi_{t+1}(x,y) = alpha_t(x) A(x,y) g_{t+1}(y) / c_t        (bwd, t+1 < H)
+      const double pr = keep * other;
+      const double c = row_sum(pr);
+      const double q = div_by(pr, c);
+      Hrow[code * 16] += q;
+      const double rc = c != 0.0 ? __builtin_ldexp(div_by(1.0, c), sc) : 0.0;
+      const double w = fwd ? e * other * rc : (t + 1 < a.H ? other * rc : 0.0);
+      acc_bcast(K, x, w);
     }
 #ifndef NIPAMD_ABLATE_NO_LL
     dead |= (z2 == 0.0);
@@ -321,10 +364,10 @@ void chain_fb_kernel(ChainArgs a) {
   {
     const int nf = H, nb = T - 1 - H, n = nf < nb ? nf : nb;
     const int t0 = fwd ? 0 : T - 2;
-    run_phase(cx, n, t0, dir, false, [&](int t, double e, double o, int j) { step(t, e, o, false, j); });
+    run_phase(cx, n, t0, dir, false, [&](int t, double e, double o, int c, int j) { step(t, e, o, c, false, j); });
     if (nf != nb && (fwd ? nf : nb) > n) {             // peeled tail: rows with one more step
       const int t = t0 + dir * n;
-      step(t, cx.Et[cx.codes[t] * 16], 0.0, false, 3);
+      step(t, cx.Et[cx.codes[t] * 16], 0.0, cx.codes[t], false, 3);
     }
   }
   __syncthreads();
@@ -333,28 +376,120 @@ void chain_fb_kernel(ChainArgs a) {
   {
     const int nf = T - H, nb = H, n = nf < nb ? nf : nb;
     const int t0 = fwd ? H : H - 1;
-    run_phase(cx, n, t0, dir, true, [&](int t, double e, double o, int j) { step(t, e, o, true, j); });
+    run_phase(cx, n, t0, dir, true, [&](int t, double e, double o, int c, int j) { step(t, e, o, c, true, j); });
     if (nf != nb && (fwd ? nf : nb) > n) {
       const int t = t0 + dir * n;
-      step(t, cx.Et[cx.codes[t] * 16], cx.Sload[(long)t * 16], true, 3);
+      step(t, cx.Et[cx.codes[t] * 16], cx.Sload[(long)t * 16], cx.codes[t], true, 3);
+    }
+  }
+  if (ESTEP) {
+    // one more backward step with alpha_{-1} = prior of prev: its posterior is
+    // the P0 count (family of the previous-slice variable at t = 0) and its
+    // xi is xi_0 (when the forward rows did not cover t = 0, i.e. H > 0)
+    const double pi_y = a.pi[y];
+    const double u = __builtin_ldexp(dot_bcast(x, C), sc);   // bwd: beta_{-1}
+    const double pr = pi_y * u;
+    const double c = row_sum(pr);
+    const double q = div_by(pr, c);
+    const double rc = c != 0.0 ? __builtin_ldexp(div_by(1.0, c), sc) : 0.0;
+    const double w = (!fwd && a.H > 0) ? pi_y * rc : 0.0;
+    acc_bcast(K, x, w);
+    double* slab = a.counts + (size_t)(active ? b : 0) * chain_estep_slab(a.M);
+    if (active && !fwd) slab[chain_slab_p0(a.M) + y] = q;
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        slab[(fwd ? kSlabKf + k * 16 + y : kSlabKb + y * 16 + k)] = K[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < kChainsPerBlock * 2 * (a.M + 2) * 16; i += kThreads) {
+      const int sq = i / (2 * (a.M + 2) * 16), r = i - sq * 2 * (a.M + 2) * 16;
+      if (b0 + sq < a.B) a.counts[(size_t)(b0 + sq) * chain_estep_slab(a.M) + kSlabH + r] = Htab[i];
     }
   }
   if (fwd && active && y == 0) {
     double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
-    if (a.status) a.status[b] = dead ? 1u : 0u;
+    // e_step's BAD_LUCK (m1 <= 0 || m2 <= 0, nip.c:1827-1854) is the same
+    // event as a zero mass here (m2 <= m1 since e <= s elementwise)
+    if (a.status) a.status[b] = dead ? (ESTEP ? 3u : 1u) : 0u;
   }
 }
 
-size_t chain_fb_lds_bytes(int M, int T) {
-  return (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kChainsPerBlock * chain_codes_row(T);
+size_t chain_lds_bytes(int M, int T, bool estep) {
+  size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kChainsPerBlock * chain_codes_row(T);
+  if (estep) n = ((n + 15) & ~(size_t)15) + (size_t)kChainsPerBlock * 2 * (M + 2) * 16 * sizeof(double);
+  return n;
 }
 
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream) {
   const int blocks = (int)((a.B + kChainsPerBlock - 1) / kChainsPerBlock);
-  const size_t lds = (chain_fb_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
-  hipLaunchKernelGGL(chain_fb_kernel, dim3(blocks), dim3(kThreads), lds, stream, a);
+  const size_t lds = (chain_lds_bytes(a.M, a.T, false) + 15) & ~(size_t)15;
+  hipLaunchKernelGGL(chain_kernel<false>, dim3(blocks), dim3(kThreads), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int chain_estep_launch(const ChainArgs& a, hipStream_t stream) {
+  const int blocks = (int)((a.B + kChainsPerBlock - 1) / kChainsPerBlock);
+  const size_t lds = (chain_lds_bytes(a.M, a.T, true) + 15) & ~(size_t)15;
+  hipLaunchKernelGGL(chain_kernel<true>, dim3(blocks), dim3(kThreads), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic batch reduction: out[g][j] = binary-tree sum of in[64g .. 64g+63][j]
+// (missing rows count as 0; x + 0 == x, so the tree shape is fixed by index).
+// Applied repeatedly, this is one binary tree over all rows, so partials of
+// power-of-two shards combine bit-identically across 1/2/4/8 GPUs.
+__global__ __launch_bounds__(256)
+void tree64_kernel(const double* __restrict__ in, long n, int S, double* __restrict__ out) {
+  const int j = blockIdx.y * 256 + threadIdx.x;
+  const long g = blockIdx.x;
+  if (j >= S) return;
+  double v[64];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    const long r = g * 64 + i;
+    v[i] = r < n ? in[r * S + j] : 0.0;
+  }
+#pragma unroll
+  for (int w = 1; w < 64; w *= 2)
+#pragma unroll
+    for (int i = 0; i < 64; i += 2 * w) v[i] += v[i + w];
+  out[g * S + j] = v[0];
+}
+
+int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream) {
+  const long groups = (n + 63) / 64;
+  hipLaunchKernelGGL(tree64_kernel, dim3((unsigned)groups, (S + 255) / 256), dim3(256), 0, stream,
+                     in, n, S, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// counts[layout] += finalised families from the reduced slab R (em_learn layout,
+// nip.c:2101-2128: child first, then parents).
+__global__ __launch_bounds__(256)
+void estep_finalize_kernel(const double* __restrict__ R, ChainFinalize f, double* __restrict__ counts) {
+  const int N = f.N, M = f.M;
+  for (int i = threadIdx.x; i < N; i += 256) counts[f.off_prev + i] += R[chain_slab_p0(M) + i];
+  for (int i = threadIdx.x; i < N * N; i += 256) {
+    const int y = i % N, x = i / N;                    // index y + N*x
+    counts[f.off_cur + i] += f.A[x * 16 + y] * (R[kSlabKf + x * 16 + y] + R[kSlabKb + x * 16 + y]);
+  }
+  for (int i = threadIdx.x; i < M * N; i += 256) {
+    const int m = i % M, y = i / M;                    // index m + M*y
+    const double* Hf = R + kSlabH;
+    const double* Hb = R + kSlabH + (M + 2) * 16;
+    const double miss = Hf[M * 16 + y] + Hb[M * 16 + y];
+    const double s = f.Etab[M * 16 + y];
+    const double part = s != 0.0 ? miss * f.Etab[m * 16 + y] / s : 0.0;
+    counts[f.off_obs + i] += (Hf[m * 16 + y] + Hb[m * 16 + y]) + part;
+  }
+}
+
+int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream) {
+  hipLaunchKernelGGL(estep_finalize_kernel, dim3(1), dim3(256), 0, stream, R, f, counts);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -50,6 +50,9 @@ struct DevState {
   double* ts = nullptr;
   double* S = nullptr;
   size_t S_bytes = 0;
+  double* R = nullptr;     // E-step partial [chain_estep_slab(M)] of nipamd_estep
+  double* W = nullptr;     // E-step work: slabs + tree levels + chunk results + partial
+  size_t W_bytes = 0;
 };
 
 DevState* dev_of(nipamd_model* mm) {
@@ -60,6 +63,7 @@ DevState* dev_of(nipamd_model* mm) {
 void dev_release(DevState* d) {
   if (!d) return;
   (void)hipFree(d->A); (void)hipFree(d->Etab); (void)hipFree(d->pi); (void)hipFree(d->ts); (void)hipFree(d->S);
+  (void)hipFree(d->W); (void)hipFree(d->R);
   *d = DevState();
 }
 
@@ -94,6 +98,34 @@ int ensure_scratch(nipamd_model* mm, size_t bytes) {
   HIP_OK(hipMalloc(&d->S, bytes));
   d->S_bytes = bytes;
   return 0;
+}
+
+int ensure_work(nipamd_model* mm, size_t bytes) {
+  DevState* d = dev_of(mm);
+  if (d->W_bytes >= bytes) return 0;
+  (void)hipFree(d->W);
+  d->W = nullptr;
+  d->W_bytes = 0;
+  HIP_OK(hipMalloc(&d->W, bytes));
+  d->W_bytes = bytes;
+  return 0;
+}
+
+// Sequences per E-step launch: bounds the slab + scratch memory.  A power of
+// two times 64^k, so chunk trees are subtrees of the one binary tree over the
+// batch (see tree64_kernel).
+constexpr long kEstepChunk = 16384;
+
+// rows [n][S] -> out [S] by repeated radix-64 tree levels (ping-pong tA/tB)
+int reduce_rows(const double* in, long n, int S, double* tA, double* tB, double* out, hipStream_t st) {
+  const double* cur = in;
+  while (n > 64) {
+    double* dst = (cur == tA) ? tB : tA;
+    if (nipamd::tree_reduce_launch(cur, n, S, dst, st)) return -1;
+    cur = dst;
+    n = (n + 63) / 64;
+  }
+  return nipamd::tree_reduce_launch(cur, n, S, out, st);
 }
 
 // Which GPU plan (if any) covers this request.
@@ -264,7 +296,7 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
     return fail(NIPAMD_ERROR_UNSUPPORTED, why);
   const auto& P = mm->m.chain;
   if (P.M + 2 > 255) return fail(NIPAMD_ERROR_UNSUPPORTED, "observation cardinality above 253");
-  if (nipamd::chain_fb_lds_bytes(P.M, T) > 96 * 1024)
+  if (nipamd::chain_lds_bytes(P.M, T, false) > 96 * 1024)
     return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
   if (int rc = ensure_tables(mm)) return rc;
   if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes(B, T))) return rc;
@@ -326,11 +358,99 @@ int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* o
   return rc;
 }
 
+int nipamd_estep_partial_size(const nipamd_model* mm) {
+  if (!mm || !mm->m.chain.valid) return -1;
+  return nipamd::chain_estep_slab(mm->m.chain.M);
+}
+
+int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                         int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
+                         void* stream) {
+  if (!mm || B < 0 || T < 1 || !d_partial || (n_obs > 0 && (!d_obs || !obs_vars)))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  int col = -1;
+  std::string why;
+  if (!check_chain_request(mm, n_obs, obs_vars, 0, nullptr, &col, why))
+    return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+  const auto& P = mm->m.chain;
+  if (P.M + 2 > 255) return fail(NIPAMD_ERROR_UNSUPPORTED, "observation cardinality above 253");
+  if (nipamd::chain_lds_bytes(P.M, T, true) > 96 * 1024)
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long / observation cardinality too large for the LDS count tables");
+  const int S = nipamd::chain_estep_slab(P.M);
+  hipStream_t st = (hipStream_t)stream;
+  if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
+  if (int rc = ensure_tables(mm)) return rc;
+  const long chunk = B < kEstepChunk ? B : kEstepChunk;
+  const long nchunks = (B + kEstepChunk - 1) / kEstepChunk;
+  const long lvl = (chunk + 63) / 64;
+  const size_t work = ((size_t)chunk + 2 * lvl + nchunks + 64) * S * sizeof(double);
+  if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes((int)chunk, T))) return rc;
+  if (int rc = ensure_work(mm, work)) return rc;
+  DevState* d = dev_of(mm);
+  double* slab = d->W;
+  double* tA = slab + (size_t)chunk * S;
+  double* tB = tA + (size_t)lvl * S;
+  double* cres = tB + (size_t)lvl * S;
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  for (long c = 0; c < nchunks; c++) {
+    const long b0 = c * kEstepChunk;
+    const int nb = (int)((B - b0) < kEstepChunk ? (B - b0) : kEstepChunk);
+    nipamd::ChainArgs a{};
+    a.obs = col >= 0 ? d_obs + b0 * T * ocols : nullptr;
+    a.obs_bstride = (long)T * ocols;
+    a.obs_tstride = ocols;
+    a.obs_col = col;
+    a.B = nb; a.T = T; a.H = T / 2; a.N = P.N; a.M = P.M;
+    a.A = d->A; a.Etab = d->Etab; a.pi = d->pi; a.ts = d->ts; a.S = d->S;
+    a.ll = d_ll ? d_ll + b0 : nullptr;
+    a.status = d_status ? d_status + b0 : nullptr;
+    a.counts = slab;
+    if (nipamd::chain_estep_launch(a, st))
+      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
+    if (reduce_rows(slab, nb, S, tA, tB, out, st))
+      return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
+  }
+  if (nchunks > 1 && reduce_rows(cres, nchunks, S, tA, tB, d_partial, st))
+    return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
+  return 0;
+}
+
+int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
+  if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const auto& P = mm->m.chain;
+  if (!P.valid) return fail(NIPAMD_ERROR_UNSUPPORTED, "model slice is not chain-shaped");
+  if (int rc = ensure_tables(mm)) return rc;
+  DevState* d = dev_of(mm);
+  nipamd::ChainFinalize f{};
+  f.N = P.N; f.M = P.M;
+  int off = 0;
+  for (size_t v = 0; v < mm->m.vars.size(); v++) {
+    if ((int)v == P.v_prev) f.off_prev = off;
+    if ((int)v == P.v_cur) f.off_cur = off;
+    if ((int)v == P.v_obs) f.off_obs = off;
+    int s = mm->m.vars[v].card;
+    for (int p : mm->m.vars[v].parents) s *= mm->m.vars[p].card;
+    off += s;
+  }
+  f.A = d->A; f.Etab = d->Etab;
+  if (nipamd::estep_finalize_launch(d_partial, f, d_counts, (hipStream_t)stream))
+    return fail(NIPAMD_ERROR_DEVICE, "finalize launch failed");
+  return 0;
+}
+
 int nipamd_estep(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                  int B, int T, double* d_counts, double* d_ll, uint32_t* d_status, void* stream) {
-  (void)d_obs; (void)n_obs; (void)obs_vars; (void)B; (void)T; (void)d_counts; (void)d_ll; (void)d_status; (void)stream;
-  if (!mm) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
-  return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step not built yet");
+  if (!mm || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const int S = nipamd_estep_partial_size(mm);
+  if (S < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "model slice is not chain-shaped (GPU plan: HMM-shaped DBN)");
+  if (int rc = ensure_tables(mm)) return rc;
+  DevState* d = dev_of(mm);
+  if (!d->R) HIP_OK(hipMalloc(&d->R, (size_t)S * sizeof(double)));
+  double* part = d->R;
+  int rc = nipamd_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, part, d_ll, d_status, stream);
+  if (rc) return rc;
+  return nipamd_estep_finalize(mm, part, d_counts, stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,214 @@
+"""GPU parity of the batched e_step / em_learn (src/nip.c:1708-2243).
+
+Expected counts, per-sequence log-likelihoods and BAD_LUCK flags from the
+gfx950 path (through the C-ABI) against the reference's own outputs
+(tests/golden/fb_*.npz, produced by oracle/_ref) and the CPU oracle.
+Tolerances: counts |gpu - ref| <= 1e-11 * max(1, |ref|) (sums
+of B*T normalised terms, summed in a different order); ll as in
+test_gpu_parity; learning curves 1e-10 relative over <= 12 EM iterations.
+The batch reduction must be bit-reproducible and shard-invariant.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+import nip_amd
+from nip_amd import synth
+from nip_amd.em import tree_sum, em_learn, NIP_NO_ERROR, NIP_ERROR_BAD_LUCK
+from oracle.bind import PortOracle
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CONTRACT = json.load(open(os.path.join(GOLD, "index_contract.json")))
+CNT_RTOL = 1e-11
+LL_RTOL = 1e-12
+CURVE_RTOL = 1e-10
+DBL_MAX = np.finfo(np.float64).max
+
+
+def product_model(name):
+    c = CONTRACT[name]
+    nodes = [tuple(n) for n in c["nodes"]]
+    pots = [(ch, ps, d) for ch, ps, d in c["potentials"]]
+    return nip_amd.Model.from_spec(nodes, pots)
+
+
+def chain_fixtures():
+    out = []
+    for p in sorted(glob.glob(os.path.join(GOLD, "fb_*.npz"))):
+        z = np.load(p)
+        m = product_model(str(z["model"]))
+        if m.gpu_supported(list(z["obs_vars"]), []):
+            out.append(p)
+    return out
+
+
+def gpu_estep(model, obs, obs_vars):
+    o = torch.from_numpy(np.ascontiguousarray(obs, np.int32)).cuda()
+    cnt, ll, st = nip_amd.e_step(model, o, obs_vars)
+    torch.cuda.synchronize()
+    return cnt.cpu().numpy(), ll.cpu().numpy(), st.cpu().numpy()
+
+
+def close(a, b, rtol):
+    return np.all(np.abs(a - b) <= rtol * np.maximum(1.0, np.abs(b)))
+
+
+@pytest.mark.parametrize("path", chain_fixtures(), ids=lambda p: os.path.basename(p))
+def test_estep_matches_reference_fixture(path):
+    z = np.load(path)
+    m = product_model(str(z["model"]))
+    cnt, ll, st = gpu_estep(m, z["obs"], list(z["obs_vars"]))
+    bad = z["estep_bad"]
+    assert np.array_equal((st & nip_amd.STATUS_BAD_LUCK) != 0, bad != 0)
+    ok = bad == 0
+    assert close(ll[ok], z["estep_ll"][ok], LL_RTOL)
+    if ok.all():
+        err = np.abs(cnt - z["counts"]).max()
+        assert close(cnt, z["counts"], CNT_RTOL), err
+
+
+@pytest.mark.parametrize("N,M,B,T", [
+    (16, 16, 9, 64), (16, 16, 8, 1), (16, 16, 8, 2), (16, 16, 3, 3),
+    (4, 5, 13, 33), (7, 3, 17, 17), (2, 2, 1, 5), (16, 8, 70, 40),
+])
+def test_estep_synthetic_vs_oracle(N, M, B, T):
+    nodes, pots = synth.hmm_spec(N, M, seed=200 + N * 7 + M)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = synth.observations(B, T, M, seed=T * 17 + B)
+    ov = [m.variable("M1")]
+    cnt, ll, st = gpu_estep(m, obs, ov)
+    orc = PortOracle(m.desc())
+    rc, rl, rb = orc.estep(obs, ov, np.ones(m.param_size()))
+    assert not rb.any() and not st.any()
+    assert close(ll, rl, LL_RTOL)
+    assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
+
+
+def test_estep_missing_observations_vs_oracle():
+    """Missing values.  Known divergence: at a missing step the
+    reference's m1 and m2 come from two propagations and may differ by
+    rounding, so its running ll can turn positive (+1e-16) and e_step reports
+    BAD_LUCK (nip.c:1838) for data that is fine; here both masses come from
+    one product and the step contributes exactly 0.  Parity is checked on the
+    sequences the reference accepts; ours accepts all."""
+    nodes, pots = synth.hmm_spec(16, 16, seed=9)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    rng = np.random.default_rng(4)
+    obs = rng.integers(0, 16, size=(12, 37, 1)).astype(np.int32)
+    obs[rng.random(obs.shape) < 0.3] = -1
+    obs[0] = -1                                   # a fully missing sequence
+    ov = [m.variable("M1")]
+    _, ll, st = gpu_estep(m, obs, ov)
+    assert not st.any()
+    assert ll[0] == 0.0
+    _, rl, rb = PortOracle(m.desc()).estep(obs, ov, np.ones(m.param_size()))
+    ok = rb == 0
+    assert ok.sum() >= 8
+    assert close(ll[ok], rl[ok], LL_RTOL)
+    cnt, _, _ = gpu_estep(m, obs[ok], ov)
+    rc, _, _ = PortOracle(m.desc()).estep(obs[ok], ov, np.ones(m.param_size()))
+    assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
+
+
+def test_estep_bad_luck_flags():
+    """Invalid codes / impossible data: the reference's e_step BAD_LUCK."""
+    nodes, pots = synth.hmm_spec(16, 16, seed=5)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    rng = np.random.default_rng(3)
+    obs = rng.integers(0, 16, size=(10, 20, 1)).astype(np.int32)
+    obs[2, 7, 0] = 16                              # out of range -> zero likelihood
+    obs[5, 0, 0] = 16
+    ov = [m.variable("M1")]
+    _, ll, st = gpu_estep(m, obs, ov)
+    _, rl, rb = PortOracle(m.desc()).estep(obs, ov, np.ones(m.param_size()))
+    assert np.array_equal((st & nip_amd.STATUS_BAD_LUCK) != 0, rb != 0)
+    ok = rb == 0
+    assert close(ll[ok], rl[ok], LL_RTOL)
+
+
+def test_partial_is_shard_invariant_and_reproducible():
+    """Binary-tree reduction: halves combined == whole batch, bit for bit."""
+    nodes, pots = synth.hmm_spec(16, 16)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = torch.from_numpy(synth.observations(256, 48, 16, seed=8)).cuda().contiguous()
+    ov = [m.variable("M1")]
+    whole, _, _ = nip_amd.estep_partial(m, obs, ov)
+    whole = whole.clone()
+    again, _, _ = nip_amd.estep_partial(m, obs, ov)
+    assert torch.equal(whole, again)
+    parts = []
+    for k in range(4):
+        p, _, _ = nip_amd.estep_partial(m, obs[k * 64:(k + 1) * 64].contiguous(), ov)
+        parts.append(p.clone())
+    assert torch.equal(tree_sum(torch.stack(parts)), whole)
+
+
+def test_chunked_batch_matches_tree():
+    """B above one launch chunk (16384): chunk trees combine exactly."""
+    nodes, pots = synth.hmm_spec(4, 4, seed=3)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    B, T = 32768, 3
+    obs = torch.from_numpy(synth.observations(B, T, 4, seed=12)).cuda().contiguous()
+    ov = [m.variable("M1")]
+    whole, _, _ = nip_amd.estep_partial(m, obs, ov)
+    whole = whole.clone()
+    a, _, _ = nip_amd.estep_partial(m, obs[:16384].contiguous(), ov)
+    a = a.clone()
+    b, _, _ = nip_amd.estep_partial(m, obs[16384:].contiguous(), ov)
+    assert torch.equal(tree_sum(torch.stack([a, b.clone()])), whole)
+
+
+@pytest.mark.parametrize("path", chain_fixtures(), ids=lambda p: os.path.basename(p))
+def test_em_learn_matches_reference_curve(path):
+    z = np.load(path)
+    m = product_model(str(z["model"]))
+    obs = torch.from_numpy(np.ascontiguousarray(z["obs"])).cuda()
+    curve = []
+    rc = em_learn(m, obs, list(z["obs_vars"]), 1e-6, curve, init=z["em_init"], max_iterations=12)
+    it = int(z["em_iters"])
+    ref_curve = z["em_curve"]
+    n = it if it >= 0 else int(np.argmax(np.append(ref_curve, 0.0) == 0.0))
+    assert len(curve) >= n
+    assert close(np.array(curve[:n]), ref_curve[:n], CURVE_RTOL)
+    if it >= 0:
+        assert rc == NIP_NO_ERROR and len(curve) == it
+    elif not (z["obs"] < 0).any():
+        assert rc == NIP_ERROR_BAD_LUCK
+    # else: the reference stopped on the missing-value rounding quirk (see
+    # test_estep_missing_observations_vs_oracle); its recorded prefix agrees
+
+
+def test_estep_config2_scale_properties():
+    """Config-2 size (4096 x 1024, N=M=16): count masses and spot parity."""
+    nodes, pots = synth.hmm_spec(16, 16)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    B, T, N, M = 4096, 1024, 16, 16
+    obs_np = synth.observations(B, T, M)
+    obs = torch.from_numpy(obs_np).cuda()
+    ov = [m.variable("M1")]
+    cnt, ll, st = nip_amd.e_step(m, obs, ov)
+    cnt = cnt.cpu().numpy()
+    assert not st.any().item()
+    d = m.desc()
+    sizes = []
+    for v in d["vars"]:
+        s = v["card"]
+        for p in v["parents"]:
+            s *= d["vars"][p]["card"]
+        sizes.append(s)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    mass = {d["vars"][i]["symbol"]: cnt[offs[i]:offs[i + 1]].sum() for i in range(3)}
+    assert abs(mass["P0"] - (N + B)) <= 1e-9 * (N + B)
+    assert abs(mass["P1"] - (N * N + B * T)) <= 1e-9 * B * T
+    assert abs(mass["M1"] - (N * M + B * T)) <= 1e-9 * B * T
+    sub = 64
+    c64, l64, _ = nip_amd.e_step(m, obs[:sub].contiguous(), ov)
+    rc, rl, _ = PortOracle(d).estep(obs_np[:sub], ov, np.ones(m.param_size()))
+    assert close(c64.cpu().numpy(), rc, CNT_RTOL)
+    assert close(l64.cpu().numpy(), rl, LL_RTOL)
