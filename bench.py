@@ -70,7 +70,7 @@ def cpu_baseline(nodes, pots, obs, budget_s: float = 12.0):
 
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")   # profiles/summarize.py
     try:
         with open(p) as f:
             d = json.load(f)
@@ -90,6 +90,9 @@ def main():
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--N", type=int, default=16)
     ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--workload", choices=["fb", "estep"], default="fb",
+                    help="fb: the headline metric (config 2 smoothing); estep: one batched "
+                         "e_step (config 4 per-GPU shard: counts + ll, no posterior write)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
     args = ap.parse_args()
@@ -114,12 +117,18 @@ def main():
     ov, q = [model.variable("M1")], [model.variable("P1")]
     obs_np = synth.observations(B, T, M, seed=1 + 7919 * rank)
     obs = torch.from_numpy(obs_np).to(dev)
-    post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
     ll = torch.empty((B,), dtype=torch.float64, device=dev)
     st = torch.empty((B,), dtype=torch.int32, device=dev)
+    if args.workload == "fb":
+        post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
 
-    def step():
-        nip_amd.forward_backward_inference(model, obs, ov, q, post, ll, st)
+        def step():
+            nip_amd.forward_backward_inference(model, obs, ov, q, post, ll, st)
+    else:
+        counts = torch.ones((model.param_size(),), dtype=torch.float64, device=dev)
+
+        def step():
+            nip_amd.e_step(model, obs, ov, counts, ll, st)
 
     def barrier():
         if world > 1:
@@ -150,12 +159,20 @@ def main():
     units = B * T * args.steps * world
     value = units / elapsed
     bpu = algorithmic_bytes_per_seq_step(N)
-    achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
+    kname = "chain_kernel<false>"
     workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (N, M, B, T)
+    metric = METRIC
+    if args.workload == "estep":
+        bpu -= 8 * N                  # no posterior write: counts stay on-chip
+        kname = "chain_kernel<true> + tree64 + finalize"
+        workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
+            N, M, B, T)
+        metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
+    achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(workload)
     if rank == 0:
         rec = {
-            "metric": METRIC, "value": value, "unit": "sequence-timesteps/s",
+            "metric": metric, "value": value, "unit": "sequence-timesteps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
@@ -163,10 +180,10 @@ def main():
                        "observed_states": M, "parallelism": "dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": "chain_fb_kernel",
+                         "traffic": traffic, "kernel": kname,
                          "kernel_ms": kern_ms, "bytes_per_unit": bpu},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "fb":
             rec["cpu_baseline"] = cpu_baseline(nodes, pots, obs_np)
         print(json.dumps(rec))
     if world > 1:

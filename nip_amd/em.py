@@ -47,9 +47,9 @@ def combine_partials(partial, group=None):
     if group is None or dist.get_world_size(group) == 1:
         return partial
     W = dist.get_world_size(group)
-    out = torch.empty((W,) + tuple(partial.shape), dtype=partial.dtype, device=partial.device)
-    dist.all_gather_into_tensor(out, partial.contiguous(), group=group)
-    return tree_sum(out)
+    out = [torch.empty_like(partial) for _ in range(W)]
+    dist.all_gather(out, partial.contiguous(), group=group)
+    return tree_sum(torch.stack(out))
 
 
 def gather_sequence_ll(ll, status, group=None):
@@ -60,10 +60,10 @@ def gather_sequence_ll(ll, status, group=None):
     if group is None or dist.get_world_size(group) == 1:
         return ll.cpu().numpy(), status.cpu().numpy()
     W = dist.get_world_size(group)
-    both = torch.stack([ll, status.to(torch.float64)])
-    out = torch.empty((W,) + tuple(both.shape), dtype=both.dtype, device=both.device)
-    dist.all_gather_into_tensor(out, both.contiguous(), group=group)
-    out = out.cpu().numpy()
+    both = torch.stack([ll, status.to(torch.float64)]).contiguous()
+    out = [torch.empty_like(both) for _ in range(W)]
+    dist.all_gather(out, both, group=group)
+    out = torch.stack(out).cpu().numpy()
     return out[:, 0].reshape(-1), out[:, 1].reshape(-1).astype(np.int64)
 
 
