@@ -158,6 +158,12 @@ int nipamd_estep(nipamd_model* m, const int32_t* d_obs, int n_obs,
                  const int* obs_vars, int B, int T, double* d_counts,
                  double* d_ll, uint32_t* d_status, void* stream);
 
+/* Host-buffer form of nipamd_estep (copies in, counts[] += on the host
+ * array, synchronous): the em_learn seam of INTEGRATION.md. */
+int nipamd_estep_host(nipamd_model* m, const int32_t* obs, int n_obs,
+                      const int* obs_vars, int B, int T, double* counts,
+                      double* ll, uint32_t* status);
+
 /*
  * The two halves of nipamd_estep, for data-parallel EM (one process per GPU,
  * util/niptrain.c:142-195 over a sharded sequence set):

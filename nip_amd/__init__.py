@@ -46,7 +46,7 @@ EXPORTS = [
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
-    "nipamd_estep_finalize",
+    "nipamd_estep_finalize", "nipamd_estep_host",
 ]
 
 
@@ -87,6 +87,7 @@ def lib():
         L.nipamd_estep_partial_size.argtypes = [vp]
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
+        L.nipamd_estep_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp]
         L.nipamd_m_step.argtypes = [vp, dp]
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
         L.nipamd_model_prior.argtypes = [vp, C.c_int, dp]

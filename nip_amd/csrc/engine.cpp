@@ -453,4 +453,27 @@ int nipamd_estep(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* o
   return nipamd_estep_finalize(mm, part, d_counts, stream);
 }
 
+int nipamd_estep_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
+                      int B, int T, double* counts, double* ll, uint32_t* status) {
+  if (!mm || B < 0 || T < 1 || !counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const int P = nipamd::param_size(mm->m);
+  int32_t* d_obs = nullptr; double* d_cnt = nullptr; double* d_ll = nullptr; uint32_t* d_st = nullptr;
+  const size_t nob = (size_t)B * T * (n_obs > 0 ? n_obs : 1);
+  HIP_OK(hipMalloc(&d_obs, nob * sizeof(int32_t)));
+  HIP_OK(hipMalloc(&d_cnt, (size_t)P * sizeof(double)));
+  HIP_OK(hipMalloc(&d_ll, (size_t)(B > 0 ? B : 1) * sizeof(double)));
+  HIP_OK(hipMalloc(&d_st, (size_t)(B > 0 ? B : 1) * sizeof(uint32_t)));
+  if (n_obs > 0 && B > 0) HIP_OK(hipMemcpy(d_obs, obs, nob * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_cnt, counts, (size_t)P * sizeof(double), hipMemcpyHostToDevice));
+  int rc = nipamd_estep(mm, d_obs, n_obs, obs_vars, B, T, d_cnt, d_ll, d_st, nullptr);
+  if (rc == 0) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(counts, d_cnt, (size_t)P * sizeof(double), hipMemcpyDeviceToHost));
+    if (ll && B > 0) HIP_OK(hipMemcpy(ll, d_ll, (size_t)B * sizeof(double), hipMemcpyDeviceToHost));
+    if (status && B > 0) HIP_OK(hipMemcpy(status, d_st, (size_t)B * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(d_obs); (void)hipFree(d_cnt); (void)hipFree(d_ll); (void)hipFree(d_st);
+  return rc;
+}
+
 }  // extern "C"

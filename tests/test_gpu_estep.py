@@ -212,3 +212,22 @@ def test_estep_config2_scale_properties():
     rc, rl, _ = PortOracle(d).estep(obs_np[:sub], ov, np.ones(m.param_size()))
     assert close(c64.cpu().numpy(), rc, CNT_RTOL)
     assert close(l64.cpu().numpy(), rl, LL_RTOL)
+
+
+def test_estep_host_buffers_match_device():
+    """nipamd_estep_host (the C em_learn seam) == nipamd_estep on device."""
+    import ctypes as C
+    nodes, pots = synth.hmm_spec(16, 16, seed=21)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = synth.observations(33, 50, 16, seed=4)
+    ov = [m.variable("M1")]
+    cnt, ll, st = gpu_estep(m, obs, ov)
+    hc = np.ones(m.param_size())
+    hl = np.zeros(33)
+    hs = np.zeros(33, np.uint32)
+    o = np.ascontiguousarray(obs, np.int32)
+    rc = nip_amd.lib().nipamd_estep_host(m._h, o.ctypes.data_as(C.c_void_p), 1,
+                                         (C.c_int * 1)(*ov), 33, 50, hc.ctypes.data_as(C.c_void_p),
+                                         hl.ctypes.data_as(C.c_void_p), hs.ctypes.data_as(C.c_void_p))
+    assert rc == 0
+    assert np.array_equal(hc, cnt) and np.array_equal(hl, ll) and not hs.any()
