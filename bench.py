@@ -159,7 +159,7 @@ def main():
     units = B * T * args.steps * world
     value = units / elapsed
     bpu = algorithmic_bytes_per_seq_step(N)
-    kname = "chain_kernel<false>"
+    kname = "chain_fb_mfma_kernel" if os.environ.get("NIPAMD_FB_KERNEL") != "dpp" else "chain_kernel<false>"
     workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (N, M, B, T)
     metric = METRIC
     if args.workload == "estep":

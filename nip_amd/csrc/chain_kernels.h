@@ -51,6 +51,9 @@ struct ChainFinalize {
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
+// matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block
+size_t chain_mfma_lds_bytes(int M, int T);
+int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream);
 int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);

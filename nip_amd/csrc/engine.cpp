@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -126,6 +127,16 @@ int reduce_rows(const double* in, long n, int S, double* tA, double* tB, double*
     n = (n + 63) / 64;
   }
   return nipamd::tree_reduce_launch(cur, n, S, out, st);
+}
+
+// fb kernel choice: the matrix-core kernel unless NIPAMD_FB_KERNEL=dpp
+// (the 16-lane DPP kernel, kept for the e_step and for A/B measurements)
+bool use_mfma() {
+  static const bool v = [] {
+    const char* e = std::getenv("NIPAMD_FB_KERNEL");
+    return !(e && std::string(e) == "dpp");
+  }();
+  return v;
 }
 
 // Which GPU plan (if any) covers this request.
@@ -326,7 +337,10 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   for (int q = 0; q < nq; q++) {
     a.post_off = q * P.N;
     if (q > 0) { a.ll = nullptr; a.status = nullptr; }
-    if (nipamd::chain_fb_launch(a, (hipStream_t)stream))
+    const int rc = use_mfma() && nipamd::chain_mfma_lds_bytes(P.M, T) <= 64 * 1024
+                       ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
+                       : nipamd::chain_fb_launch(a, (hipStream_t)stream);
+    if (rc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   }
   return 0;

@@ -19,7 +19,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-KERNEL = "chain_kernel<false>"
+KERNEL = "chain_fb_mfma_kernel"
 
 
 def per_kernel(path, counter):
