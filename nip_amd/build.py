@@ -19,16 +19,18 @@ def sources():
     return sorted(glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.hip")))
 
 
-def build(verbose: bool = False) -> str:
-    os.makedirs(LIB_DIR, exist_ok=True)
+def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
+    """Compile every csrc source into one gfx950 shared library.  `defines`
+    (e.g. ["NIPAMD_MFMA_RED=1"]) build measurement variants into `out`."""
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result",
+           "-Wall", "-Wno-unused-result", *["-D" + d for d in defines],
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"),
-           *sources(), "-o", LIB]
+           *sources(), "-o", out]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    return LIB
+    return out
 
 
 if __name__ == "__main__":

@@ -33,7 +33,10 @@ struct ChainArgs {
 constexpr int kScratchGuard = 16;   // >= 2 chunks: the deepest prefetch over-run
 __host__ __device__ inline long chain_scratch_row(int T) { return (long)(T + 2 * kScratchGuard) * 16; }
 __host__ __device__ inline int chain_codes_row(int T) { return ((T + 7) & ~7) + 2 * kScratchGuard; }
-inline size_t chain_scratch_bytes(long B, int T) { return (size_t)(B + 2) * chain_scratch_row(T) * sizeof(double); }
+// (B rounded up to the matrix-core kernel's 16-sequence blocks, plus two spare rows)
+inline size_t chain_scratch_bytes(long B, int T) {
+  return (size_t)(((B + 15) & ~15L) + 2) * chain_scratch_row(T) * sizeof(double);
+}
 
 // E-step per-sequence slab (doubles): Kf[16][16], Kb[16][16] (xi sums of the
 // forward / backward rows, without the A factor), H[2][M+2][16] (M1 count

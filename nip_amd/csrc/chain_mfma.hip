@@ -1,32 +1,46 @@
 // chain_mfma.hip -- batched forward-backward on the gfx950 matrix cores.
 //
 // Same recursion as chain_kernels.hip (see the derivation there, nip.c:1320-
-// 1581), laid out for v_mfma_f64_16x16x4_f64: one wavefront carries SIXTEEN
-// chains (sequences) of one direction, and every step's sixteen 16x16
-// mat-vecs are one 16x16x16 product, D = M' X, done as four chained MFMAs.
+// 1581), laid out for v_mfma_f64_16x16x4_f64: sixteen chains (sequences) of
+// one direction share one wavefront, and each step's sixteen 16x16 mat-vecs
+// are one 16x16x16 product, D = M' X, done as four chained MFMAs.
 //
 // Register layout (MI355X_MICROARCH.md, f64 MFMA): D/C lane l, register r =
 // element (row (l>>4) + 4r, column l&15); A operand lane l = (row l&15,
 // k l>>4); B operand lane l = (k l>>4, column l&15).  Columns are chains
 // (j = l&15).  Splitting K = 16 into four MFMAs with k' = (l>>4) + 4r makes
 // register r of D exactly the B operand of MFMA r of the next step, so the
-// state never leaves the lane.  Internal state i' is stored as actual state
-// sigma(i') = 4 (i' mod 4) + (i' div 4): lane (g = l>>4, j) register r then
-// holds actual state 4g + r of chain j, so every lane owns four CONTIGUOUS
-// states -- 32-byte evidence reads from LDS and 32-byte stores to HBM.
+// state never leaves the lane.  Internal state i' = g + 4r is stored as
+// actual state f(g, r) = 2g + r (r < 2), 8 + 2g + (r - 2) (r >= 2): lane
+// (g = l>>4, j) owns states {2g, 2g+1} and {8+2g, 9+2g} of chain j.
 //
-//   A operand of MFMA r, lane l:  M[sigma(l&15)][4(l>>4) + r]
+//   A operand of MFMA r, lane l:  M[f(j & 3, j >> 2)][f(l>>4, r)],  j = l&15
 //   with M = A^T (forward: u = A^T alpha)  or  M = A (backward: u = A g)
 //
 // Sums over a chain's 16 states: three in-lane adds, then v_permlane32_swap
 // and v_permlane16_swap exchanges (lanes l, l^32, l^16), each symmetric, so
 // all four lanes of a chain hold bit-identical sums.
 //
-// Block = 2 waves on the same 16 sequences: wave 0 the forward filter, wave 1
-// the backward filter.  Phase A / barrier / phase B exactly as the 16-lane
-// kernel (two-filter smoothing, S[b][t] holds alpha_t for t < H, beta_t for
-// t >= H).  Each wave runs its own template instance: no per-lane direction
-// selects.
+// On gfx950 the f64 MFMA and f64 VALU work share the SIMD's double-precision
+// pipe (SQ_VALU_MFMA_COEXEC_CYCLES = 0), so a step costs its MFMA cycles PLUS
+// its vector instructions: the compute waves keep only the recursion itself,
+// and everything else moves to a partner wave on another SIMD.  Block = 16
+// sequences, four waves, one per SIMD:
+//   wave 0  forward filter:  alpha_t (scaled) -> LDS ring; ll
+//   wave 1  backward filter: beta_t (scaled)  -> LDS ring
+//   wave 2  forward partner:  phase A alpha -> HBM scratch;
+//                             phase B posterior = normalise(alpha o beta), beta
+//                             read from the scratch, -> HBM
+//   wave 3  backward partner: the same for the backward half
+// The rings hold two 8-step slots per direction; one s_barrier per chunk
+// hands a slot from filter to partner.  Phase A / barrier / phase B as the
+// 16-lane kernel (two-filter smoothing, the scratch holds alpha_t for t < H,
+// beta_t for t >= H).
+//
+// HBM layouts chosen for streaming: the scratch is block-major,
+// S[block][kMG + t][16 chains][16 states], one step of a block = 2 KB
+// contiguous; posteriors (the caller's [B][T][N]) are written per chain as
+// one contiguous 1 KB run of 8 steps per store instruction when N == 16.
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cstdint>
@@ -39,10 +53,27 @@ namespace {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-constexpr int kMSeq = 16;          // sequences (chains per direction) per block
-constexpr int kMThreads = 128;     // wave 0 forward, wave 1 backward
-constexpr int kMChunk = 8;         // steps per unrolled chunk = prefetch distance
+#ifndef NIPAMD_MFMA_ABLATE
+#define NIPAMD_MFMA_ABLATE 0       // timing-only builds: 11 no posterior stores, 12 no phase-B loads
+#endif
+#ifndef NIPAMD_MFMA_PF
+#define NIPAMD_MFMA_PF 1           // partner prefetch distance in chunks (1 or 2)
+#endif
+#ifndef NIPAMD_MFMA_NT
+#define NIPAMD_MFMA_NT 0           // 1: non-temporal posterior stores
+#endif
+
+constexpr int kMSeq = 16;          // sequences per block
+constexpr int kMThreads = 256;     // waves: 0 fwd filter, 1 bwd filter, 2 fwd partner, 3 bwd partner
+constexpr int kMChunk = 8;         // steps per chunk = ring slot
 constexpr int kMG = kScratchGuard;
+constexpr int kStepD = kMSeq * 16;                 // doubles per step (2 KB)
+constexpr int kSlotD = kMChunk * kStepD;           // doubles per ring slot (16 KB)
+constexpr int kOutD = 2 * 2 * kSlotD;              // rings [dir][slot] (64 KB)
+constexpr int kZD = 2 * kMChunk * kMSeq;           // forward z2 ring [slot][step][chain] (2 KB)
+constexpr int kSStep = kMSeq * 16;                 // doubles per step of a block's scratch
+
+__host__ __device__ inline long block_scratch(int T) { return (long)(T + 2 * kMG) * kSStep; }
 
 __device__ __forceinline__ double sum_lanes32(double x) {   // x[l] + x[l ^ 32]
   const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
@@ -61,6 +92,23 @@ __device__ __forceinline__ double sum_lanes16(double x) {   // x[l] + x[l ^ 16]
 // sum of the chain's 16 states, identical in the chain's four lanes
 __device__ __forceinline__ double chain_sum(v4d v) {
   return sum_lanes16(sum_lanes32((v.x + v.y) + (v.z + v.w)));
+}
+
+// DPP move of a double within a 16-lane row (32-bit halves; full row mask)
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// sum over aligned groups of 8 lanes (quad swaps, then row_half_mirror);
+// every level pairs equal partial sums, so all 8 lanes get identical bits
+__device__ __forceinline__ double sum8(double x) {
+  x += dpp64<0xB1>(x);     // quad_perm [1,0,3,2]
+  x += dpp64<0x4E>(x);     // quad_perm [2,3,0,1]
+  x += dpp64<0x141>(x);    // row_half_mirror
+  return x;
 }
 
 __device__ __forceinline__ v4d matvec(const double (&Aop)[4], v4d X) {
@@ -88,175 +136,336 @@ __device__ __forceinline__ double recip(double c) {
   return c != 0.0 ? r : 0.0;
 }
 
+// actual state held by register r of lane group g
+__host__ __device__ constexpr int state_of(int g, int r) { return r < 2 ? 2 * g + r : 6 + 2 * g + r; }
+
+// this lane's four states of a 16-state row; p = row + 2g
 __device__ __forceinline__ v4d load4(const double* p) {
   const double2 a = *reinterpret_cast<const double2*>(p);
-  const double2 b = *reinterpret_cast<const double2*>(p + 2);
+  const double2 b = *reinterpret_cast<const double2*>(p + 8);
   v4d r;
   r.x = a.x; r.y = a.y; r.z = b.x; r.w = b.y;
   return r;
 }
 
-__device__ __forceinline__ void store4(double* p, v4d v) {
-  *reinterpret_cast<double2*>(p) = make_double2(v.x, v.y);
-  *reinterpret_cast<double2*>(p + 2) = make_double2(v.z, v.w);
+// LDS ring layout of one step: chain j's 16 states at j*16, its eight 16-byte
+// pieces XOR-swizzled by (j & 7) so that the filter's writes and the
+// partner's reads are bank-conflict free.
+__device__ __forceinline__ int piece_off(int j, int s) { return j * 16 + ((s ^ (j & 7)) << 1); }
+
+__device__ __forceinline__ void barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 struct WaveCtx {
-  const double* Et;         // LDS evidence table + 4g (row stride 16)
+  const double* Et;         // LDS evidence table + 2g (row stride 16)
   const uint8_t* codes;     // LDS codes of chain j, index t in [-kMG, T + kMG)
-  double* S;                // this chain's scratch row + 4g (index t * 16), or the sink row
-  double* P;                // posterior of this chain + post_off + 4g, or the sink row
-  long Pstride;             // post_tstride, or 0 for the sink
-  int nst;                  // states of this lane that are real (N - 4g, clamped)
+  double* out;              // this direction's LDS ring [2][kMChunk][kStepD]
+  double* zr;               // forward: LDS ring of step masses z2 [2][kMChunk][16], else null
+  int wo0, wo1;             // this lane's two piece offsets within a step
+  bool zw;                  // this lane writes its chain's z2 (lane group 0)
 };
 
-__device__ __forceinline__ v4d evidence(const WaveCtx& c, int t) {
-  return load4(c.Et + c.codes[t] * 16);
-}
-
-// PVEC: N == 16 and 16-byte aligned posterior rows -> two 16-byte stores
-template <bool PVEC>
-__device__ __forceinline__ void store_post(double* p, int nst, v4d q) {
-  if (PVEC) {
-    store4(p, q);
-  } else {
-    if (nst > 0) p[0] = q.x;
-    if (nst > 1) p[1] = q.y;
-    if (nst > 2) p[2] = q.z;
-    if (nst > 3) p[3] = q.w;
-  }
-}
-
-template <bool FWD, bool PVEC>
+template <bool FWD>
 struct Chain {
   double Aop[4];
   v4d X;          // next mat-vec input (fwd: alpha_{t-1}; bwd: e_{t+1} o beta_{t+1})
-  v4d s;          // row sums of the evidence table (m1 weights)
   int sc = 0;     // power-of-two scale applied to the next mat-vec result
-  double m2 = 1.0, m1 = 1.0;
-  int e2 = 0, e1 = 0;
-  double zmin = 1.0;   // min over steps of z2: 0 <=> some zero mass
 
-  // one step; Sp / Pp point at time t's vectors, `other` is the opposite
-  // direction's vector at t
-  template <bool COMBINE>
-  __device__ __forceinline__ void step(double* Sp, double* Pp, int nst, v4d e, v4d other, int j) {
+  // one step: the interface vector (alpha_t or beta_t, scaled) to LDS row L;
+  // the forward filter also publishes its step mass z2 for the partner's ll
+  __device__ __forceinline__ void step(const WaveCtx& c, double* L, double* Z, v4d e) {
     const v4d u = ldexp4(matvec(Aop, X), sc);
     const v4d p = u * e;
     const v4d keep = FWD ? p : u;
+    *reinterpret_cast<double2*>(L + c.wo0) = make_double2(keep.x, keep.y);
+    *reinterpret_cast<double2*>(L + c.wo1) = make_double2(keep.z, keep.w);
     const double z2 = chain_sum(p);
-    const double z1 = chain_sum(u * s);
-    if (!COMBINE) {
-      store4(Sp, keep);
-    } else {
-      const v4d pr = keep * other;
-      // normalise; an all-zero vector stays zero (recip(0) = 0)
-      store_post<PVEC>(Pp, nst, pr * recip(chain_sum(pr)));
-    }
-    zmin = __builtin_fmin(zmin, z2);
-    m2 *= z2; m1 *= z1;
-    if ((j & 3) == 3) {
-      const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
-      const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
-    }
+    if (FWD && c.zw) *Z = z2;
     sc = -__builtin_amdgcn_frexp_exp(z2);   // frexp exponent of 0 is 0
     X = p;
   }
 
-  // n steps starting at t0, moving forward (FWD) or backward in time
-  template <bool COMBINE>
-  __device__ __forceinline__ void run(const WaveCtx& c, int n, int t0) {
+  // a phase of n steps from t0 in nch chunks (uniform over the block); all
+  // eight codes and evidence vectors of a chunk are read from LDS up front
+  __device__ __forceinline__ void run(const WaveCtx& c, int n, int nch, int t0, int lane) {
     constexpr int dir = FWD ? 1 : -1;
-    v4d oa[kMChunk], ob[kMChunk];
-    auto load_other = [&](v4d (&o)[kMChunk], int tb) {
-      const double* q = c.S + (long)tb * 16;
+    for (int ci = 0; ci < nch; ci++) {
+      double* slot = c.out + (ci & 1) * kSlotD;
+      double* zs = FWD ? c.zr + (ci & 1) * kMChunk * kMSeq + (lane & 15) : nullptr;
+      const int base = ci * kMChunk;
+      int code[kMChunk];
 #pragma unroll
-      for (int k = 0; k < kMChunk; k++) o[k] = COMBINE ? load4(q + dir * k * 16) : v4d{};
-    };
-    const long pinc = dir * c.Pstride;
-    int base = 0;
-    if (COMBINE && n >= 2 * kMChunk) load_other(oa, t0);
-    double* Pp = c.P + (long)t0 * c.Pstride;
-    v4d en = evidence(c, t0);
-    for (; base + 2 * kMChunk <= n; base += 2 * kMChunk) {
-      if (COMBINE) load_other(ob, t0 + dir * (base + kMChunk));
-      double* Sc = c.S + (long)(t0 + dir * base) * 16;
+      for (int k = 0; k < kMChunk; k++) code[k] = c.codes[t0 + dir * (base + k)];   // guards cover over-run
+      v4d e[kMChunk];
 #pragma unroll
-      for (int k = 0; k < kMChunk; k++) {
-        const v4d e = en;
-        en = evidence(c, t0 + dir * (base + k + 1));
-        step<COMBINE>(Sc + dir * k * 16, Pp, c.nst, e, oa[k], k);
-        Pp += pinc;
+      for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + code[k] * 16);
+      if (base + kMChunk <= n) {
+#pragma unroll
+        for (int k = 0; k < kMChunk; k++) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kMChunk; k++)
+          if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
       }
-      if (COMBINE) load_other(oa, t0 + dir * (base + 2 * kMChunk));
-#pragma unroll
-      for (int k = 0; k < kMChunk; k++) {
-        const v4d e = en;
-        en = evidence(c, t0 + dir * (base + kMChunk + k + 1));
-        step<COMBINE>(Sc + dir * (kMChunk + k) * 16, Pp, c.nst, e, ob[k], k);
-        Pp += pinc;
-      }
-    }
-    // tail (< 2 chunks): one step at a time, renormalising every step
-    for (; base < n; base++) {
-      const int t = t0 + dir * base;
-      step<COMBINE>(c.S + (long)t * 16, Pp, c.nst, evidence(c, t),
-                    COMBINE ? load4(c.S + (long)t * 16) : v4d{}, 3);
-      Pp += pinc;
+      barrier_lds();
     }
   }
 };
 
-template <bool FWD, bool PVEC>
-__device__ __forceinline__ void run_wave(const ChainArgs& a, const WaveCtx& c, const double* Et,
-                                         int lane, bool active, long b) {
+template <bool FWD>
+__device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c, const double* Et,
+                                            double* Sw, int lane, bool active, long b,
+                                            int nchA, int nchB, unsigned long long* stamps) {
   const int j = lane & 15, g = lane >> 4;
-  const int sj = 4 * (j & 3) + (j >> 2);        // actual state of D row j
+  const int sj = state_of(j & 3, j >> 2);       // actual state of D row j
   const int T = a.T, H = a.H;
-  Chain<FWD, PVEC> ch;
+  Chain<FWD> ch;
 #pragma unroll
   for (int r = 0; r < 4; r++)
-    ch.Aop[r] = FWD ? a.A[(4 * g + r) * 16 + sj] : a.A[sj * 16 + 4 * g + r];
-  ch.s = load4(Et + a.M * 16 + 4 * g);
+    ch.Aop[r] = FWD ? a.A[state_of(g, r) * 16 + sj] : a.A[sj * 16 + state_of(g, r)];
   if (FWD) {
-    ch.X = load4(a.pi + 4 * g);
+    ch.X = load4(a.pi + 2 * g);
   } else {
     v4d beta;                                   // beta_{T-1} = 1 on the real states
-    beta.x = 4 * g + 0 < a.N ? 1.0 : 0.0; beta.y = 4 * g + 1 < a.N ? 1.0 : 0.0;
-    beta.z = 4 * g + 2 < a.N ? 1.0 : 0.0; beta.w = 4 * g + 3 < a.N ? 1.0 : 0.0;
-    store4(c.S + (long)(T - 1) * 16, beta);     // T-1 >= H
-    ch.X = evidence(c, T - 1) * beta;
+    beta.x = state_of(g, 0) < a.N ? 1.0 : 0.0; beta.y = state_of(g, 1) < a.N ? 1.0 : 0.0;
+    beta.z = state_of(g, 2) < a.N ? 1.0 : 0.0; beta.w = state_of(g, 3) < a.N ? 1.0 : 0.0;
+    {                                           // S[T-1] (T-1 >= H): the forward partner's in phase B
+      double* q = Sw + (long)(T - 1) * kSStep;
+      *reinterpret_cast<double2*>(q) = make_double2(beta.x, beta.y);
+      *reinterpret_cast<double2*>(q + 8) = make_double2(beta.z, beta.w);
+    }
+    ch.X = load4(c.Et + c.codes[T - 1] * 16) * beta;
     ch.sc = -__builtin_amdgcn_frexp_exp(chain_sum(ch.X));
   }
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
-  if (FWD) ch.template run<false>(c, H, 0);
-  else ch.template run<false>(c, T - 1 - H, T - 2);
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // phase B: forward alpha_H..alpha_{T-1} with beta from S; backward
-  // beta_{H-1}..beta_0 with alpha from S
-  if (FWD) ch.template run<true>(c, T - H, H);
-  else ch.template run<true>(c, H, H - 1);
-  if (FWD && active && g == 0) {
-    double ll = log(ch.m2) - log(ch.m1) + (double)(ch.e2 - ch.e1) * 0.69314718055994530942;
-    const bool dead = ch.zmin == 0.0;
-    if (dead) ll = -DBL_MAX;
-    if (a.ll) a.ll[b] = ll;
-    if (a.status) a.status[b] = dead ? 1u : 0u;
+  if (FWD) ch.run(c, H, nchA, 0, lane);
+  else ch.run(c, T - 1 - H, nchA, T - 2, lane);
+  if (stamps && lane == 0) stamps[blockIdx.x * 4 + 1] = __builtin_readcyclecounter();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  if (stamps && lane == 0) stamps[blockIdx.x * 4 + 2] = __builtin_readcyclecounter();
+  // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
+  if (FWD) ch.run(c, T - H, nchB, H, lane);
+  else ch.run(c, H, nchB, H - 1, lane);
+  (void)active; (void)b;
+}
+
+// Log-likelihood of the forward filter (nip.c:1461-1474), kept by its
+// partner: ll = sum_t log m2_t - log m1_t with m2_t = z2_t = sum(alpha_t) as
+// published by the filter, and m1_t = sum(u_t o s) = 2^sc_t * y_{t-1},
+// y_t = alpha_t . w (w = A s, the chain plan's `ts`), sc_t = -exp2(z2_{t-1}),
+// y_{-1} = prior . w.  Products of mantissas with exponents carried apart.
+// Lane: chain q*8 + (L >> 3) for q = 0, 1, piece s = L & 7.
+struct LL {
+  double m2[2], m1[2], zmin[2];
+  int e2[2], e1[2];
+  double w0, w1;            // w at this lane's two states
+
+  __device__ __forceinline__ void init(const ChainArgs& a, int s) {
+    w0 = a.ts[2 * s]; w1 = a.ts[2 * s + 1];
+    const double ym = sum8(a.pi[2 * s] * w0 + a.pi[2 * s + 1] * w1);   // y_{-1}
+#pragma unroll
+    for (int q = 0; q < 2; q++) { m2[q] = 1.0; m1[q] = ym; zmin[q] = 1.0; e2[q] = 0; e1[q] = 0; }
   }
+  // step t of chain slot q: alpha piece v, z2 from the filter; last = (t == T-1)
+  __device__ __forceinline__ void step(int q, double2 v, double z2, bool last, bool renorm) {
+    const double y = sum8(v.x * w0 + v.y * w1);
+    zmin[q] = __builtin_fmin(zmin[q], z2);
+    m2[q] *= z2;
+    if (!last) { m1[q] *= y; e1[q] -= __builtin_amdgcn_frexp_exp(z2); }   // 2^sc_{t+1}
+    if (renorm) {
+      const int k2 = __builtin_amdgcn_frexp_exp(m2[q]); m2[q] = __builtin_ldexp(m2[q], -k2); e2[q] += k2;
+      const int k1 = __builtin_amdgcn_frexp_exp(m1[q]); m1[q] = __builtin_ldexp(m1[q], -k1); e1[q] += k1;
+    }
+  }
+  __device__ __forceinline__ void write(const ChainArgs& a, long b0, int lane) {
+    if ((lane & 7) != 0) return;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const long b = b0 + q * 8 + (lane >> 3);
+      if (b >= a.B) continue;
+      double ll = log(m2[q]) - log(m1[q]) + (double)(e2[q] - e1[q]) * 0.69314718055994530942;
+      const bool dead = zmin[q] == 0.0;
+      if (dead) ll = -DBL_MAX;
+      if (a.ll) a.ll[b] = ll;
+      if (a.status) a.status[b] = dead ? 1u : 0u;
+    }
+  }
+};
+
+// Partner wave of one direction.  Phase A: each step's 2 KB of the block's
+// scratch as two contiguous 1 KB instructions (lane L: chain q*8 + (L >> 3),
+// piece L & 7).  Phase B: for chain q, lane L takes step (L >> 3) of the
+// chunk in ADDRESS order and piece s = L & 7 (states 2s, 2s+1): the ring
+// value times the other direction's vector (scratch, one chunk prefetched),
+// normalised over the 8 lanes of its step, and -- when N == 16 with 16-byte
+// rows -- one contiguous 1 KB posterior run per store instruction.
+template <bool FWD>
+__device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* out, const double* zr,
+                                             double* Sblk, int lane, long b0, int nchA, int nchB) {
+  const int T = a.T, H = a.H;
+  const int s = lane & 7, hi = lane >> 3;
+  const bool pvec = a.N == 16 && a.post_tstride == 16 && ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
+  const int nA = FWD ? H : T - 1 - H, nB = FWD ? T - H : H;
+  const int tA = FWD ? 0 : T - 2, tB = FWD ? H : H - 1;
+  constexpr int dir = FWD ? 1 : -1;
+  const bool st0 = 2 * s < a.N, st1 = 2 * s + 1 < a.N;
+  // phase-B geometry of this lane: slot step k, time offset hi in address order
+  const int kB = FWD ? hi : kMChunk - 1 - hi;
+  auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
+
+  LL ll;
+  if (FWD) ll.init(a, s);
+  // forward ll over the chunk's valid steps (chain q*8 + hi, piece s)
+  auto ll_chunk = [&](int ci, int n, int t0) {
+    const double* slot = out + (ci & 1) * kSlotD;
+    const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
+    const bool full = ci * kMChunk + kMChunk <= n;
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++) {
+      const int i = ci * kMChunk + k;
+      if (i >= n) break;
+      const bool last = t0 + i == T - 1;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int jj = q * 8 + hi;
+        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(jj, s));
+        ll.step(q, v, zs[k * kMSeq + jj], last, !full || (k & 3) == 3);
+      }
+    }
+  };
+  auto drainA = [&](int ci) {
+    const double* slot = out + (ci & 1) * kSlotD;
+    if (FWD) ll_chunk(ci, nA, tA);
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++) {
+      const int i = ci * kMChunk + k;
+      if (i >= nA) break;
+      const int t = tA + dir * i;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int jj = q * 8 + hi;
+        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(jj, s));
+        *reinterpret_cast<double2*>(Sblk + (long)t * kSStep + jj * 16 + 2 * s) = v;
+      }
+    }
+  };
+  for (int ci = 0; ci < nchA; ci++) {
+    if (ci > 0) drainA(ci - 1);
+    barrier_lds();
+  }
+  if (nchA > 0) drainA(nchA - 1);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+
+  // other direction's vectors of chunk ci, all 16 chains, this lane's piece
+  double2 oa[kMSeq], ob[kMSeq];
+#if NIPAMD_MFMA_PF == 2
+  double2 oc[kMSeq];
+#endif
+  auto load_other = [&](double2 (&o)[kMSeq], int ci) {
+    const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
+#pragma unroll
+    for (int c = 0; c < kMSeq; c++)
+      o[c] = NIPAMD_MFMA_ABLATE == 12 ? make_double2(1.0 + c, 2.0) : *reinterpret_cast<const double2*>(q + c * 16);
+  };
+  // spare scratch rows past the last block: target of masked lanes' stores
+  double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
+  auto drainB = [&](int ci, const double2 (&o)[kMSeq]) {
+    if (FWD) ll_chunk(ci, nB, tB);
+    if (!a.post) return;
+    const double* slot = out + (ci & 1) * kSlotD;
+    const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;   // valid steps
+    const bool ok = kB < nk;
+    const int t = tlow(ci) + hi;
+    if (pvec) {
+      // branch-free: the 16 chains' work interleaves freely
+#pragma unroll
+      for (int q = 0; q < kMSeq; q++) {
+        const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
+        const double px = v.x * o[q].x, py = v.y * o[q].y;
+        const double r = recip(sum8(px + py));      // an all-zero row stays zero
+        const long bb = b0 + q;
+#if NIPAMD_MFMA_ABLATE == 13     // timing-only: block-major posterior layout (wrong layout)
+        double* p = (ok && bb < a.B)
+                        ? a.post + ((size_t)(b0 / kMSeq) * a.T + t) * kStepD + q * 16 + 2 * s
+                        : sink;
+#else
+        double* p = (ok && bb < a.B)
+                        ? a.post + (size_t)bb * a.post_bstride + (long)t * 16 + a.post_off + 2 * s
+                        : sink;
+#endif
+#if NIPAMD_MFMA_ABLATE == 11
+        if (px == 12345.0)
+#endif
+#if NIPAMD_MFMA_NT
+        {
+          typedef double v2d __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(v2d{px * r, py * r}, reinterpret_cast<v2d*>(p));
+        }
+#else
+        *reinterpret_cast<double2*>(p) = make_double2(px * r, py * r);
+#endif
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kMSeq; q++) {
+        const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
+        const double px = v.x * o[q].x, py = v.y * o[q].y;
+        const double r = recip(sum8(px + py));
+        const long bb = b0 + q;
+        if (!ok || bb >= a.B) continue;
+        double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
+        if (st0) p[0] = px * r;
+        if (st1) p[1] = py * r;
+      }
+    }
+  };
+  // chunk ci is drained right after the barrier that ends it, while the
+  // filter computes chunk ci + 1; its inputs were loaded one chunk earlier
+#if NIPAMD_MFMA_PF == 2
+  if (nchB > 0) load_other(oa, 0);
+  if (nchB > 1) load_other(ob, 1);
+  for (int ci = 0; ci < nchB; ci += 3) {
+    if (ci + 2 < nchB) load_other(oc, ci + 2);
+    barrier_lds();
+    drainB(ci, oa);
+    if (ci + 1 >= nchB) break;
+    if (ci + 3 < nchB) load_other(oa, ci + 3);
+    barrier_lds();
+    drainB(ci + 1, ob);
+    if (ci + 2 >= nchB) break;
+    if (ci + 4 < nchB) load_other(ob, ci + 4);
+    barrier_lds();
+    drainB(ci + 2, oc);
+  }
+#else
+  if (nchB > 0) load_other(oa, 0);
+  for (int ci = 0; ci < nchB; ci += 2) {
+    if (ci + 1 < nchB) load_other(ob, ci + 1);
+    barrier_lds();
+    drainB(ci, oa);
+    if (ci + 1 >= nchB) break;
+    if (ci + 2 < nchB) load_other(oa, ci + 2);
+    barrier_lds();
+    drainB(ci + 1, ob);
+  }
+#endif
+  if (FWD) ll.write(a, b0, lane);
 }
 
 __global__ __launch_bounds__(kMThreads, 1)
 void chain_fb_mfma_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* Et = reinterpret_cast<double*>(smem);                       // [(M+2)][16]
-  uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);    // [16][Tr]
+  double* out = reinterpret_cast<double*>(smem);                      // [2 dirs][2 slots][8][16][16]
+  double* zr = out + kOutD;                                          // [2 slots][8][16]
+  double* Et = zr + kZD;                                             // [(M+2)][16]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * 16);   // [16][Tr]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * kMSeq;
-  const long b = b0 + j;
-  const bool active = b < a.B;
   const int T = a.T;
   const int Tr = chain_codes_row(T);
 
@@ -294,36 +503,53 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   }
   __syncthreads();
 
-  const long row = chain_scratch_row(T);
-  double* const sink = a.S + (size_t)(a.B + 1) * row + kMG * 16 + 4 * g;
-  WaveCtx c;
-  c.Et = Et + 4 * g;
-  c.codes = codes + j * Tr + kMG;
-  c.S = active ? a.S + (size_t)b * row + kMG * 16 + 4 * g : sink;
-  const bool pst = active && a.post;
-  c.P = pst ? a.post + (size_t)b * a.post_bstride + a.post_off + 4 * g : sink;
-  c.Pstride = pst ? a.post_tstride : 0;
-  const bool pvec = a.N == 16 && ((a.post_off | a.post_tstride | (int)(a.post_bstride & 1)) & 1) == 0 &&
-                    ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
-  c.nst = pst ? (a.N - 4 * g < 0 ? 0 : (a.N - 4 * g > 4 ? 4 : a.N - 4 * g)) : 4;
-  if (pvec) {
-    if (wave == 0) run_wave<true, true>(a, c, Et, lane, active, b);
-    else run_wave<false, true>(a, c, Et, lane, active, b);
-  } else {
-    if (wave == 0) run_wave<true, false>(a, c, Et, lane, active, b);
-    else run_wave<false, false>(a, c, Et, lane, active, b);
+  // optional phase timestamps (a.counts != nullptr in fb: NIPAMD_PHASE_TIMES)
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(a.counts);
+  if (stamps && tid == 0) stamps[blockIdx.x * 4 + 0] = __builtin_readcyclecounter();
+  const int H = a.H;
+  const int nA = (H > T - 1 - H ? H : T - 1 - H), nB = (T - H > H ? T - H : H);
+  const int nchA = (nA + kMChunk - 1) / kMChunk, nchB = (nB + kMChunk - 1) / kMChunk;
+  const bool fwd = (wave & 1) == 0;
+  double* ring = out + (fwd ? 0 : 2 * kSlotD);
+  double* Sblk = a.S + (size_t)blockIdx.x * block_scratch(T) + kMG * kSStep;   // t = 0
+  if (wave >= 2) {
+    if (fwd) partner_wave<true>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+    else partner_wave<false>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+    return;
   }
+  const long b = b0 + j;
+  const bool active = b < a.B;
+  double* Sw = Sblk + j * 16 + 2 * g;          // inactive chains compute garbage, never stored
+  WaveCtx c;
+  c.Et = Et + 2 * g;
+  c.codes = codes + j * Tr + kMG;
+  c.out = ring;
+  c.zr = zr;
+  c.zw = g == 0;
+  c.wo0 = piece_off(j, g);
+  c.wo1 = piece_off(j, 4 + g);
+  if (fwd) filter_wave<true>(a, c, Et, Sw, lane, active, b, nchA, nchB, stamps);
+  else filter_wave<false>(a, c, Et, Sw, lane, active, b, nchA, nchB, nullptr);
+  if (stamps && tid == 0) stamps[blockIdx.x * 4 + 3] = __builtin_readcyclecounter();
 }
 
 }  // namespace
 
 size_t chain_mfma_lds_bytes(int M, int T) {
-  return (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kMSeq * chain_codes_row(T);
+  return (size_t)(kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * 16 * sizeof(double) +
+         (size_t)kMSeq * chain_codes_row(T);
 }
 
 int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream) {
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
   const size_t lds = (chain_mfma_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
+  static size_t lds_set = 0;
+  if (lds > 65536 && lds > lds_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_fb_mfma_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return -1;
+    lds_set = lds;
+  }
   hipLaunchKernelGGL(chain_fb_mfma_kernel, dim3(blocks), dim3(kMThreads), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -337,9 +337,33 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   for (int q = 0; q < nq; q++) {
     a.post_off = q * P.N;
     if (q > 0) { a.ll = nullptr; a.status = nullptr; }
-    const int rc = use_mfma() && nipamd::chain_mfma_lds_bytes(P.M, T) <= 64 * 1024
-                       ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
-                       : nipamd::chain_fb_launch(a, (hipStream_t)stream);
+    const bool mf = use_mfma() && nipamd::chain_mfma_lds_bytes(P.M, T) <= 160 * 1024;
+    // diagnostics: NIPAMD_PHASE_TIMES=1 records per-block phase timestamps
+    // (start / end of phase A / start of phase B / end) and prints a summary
+    static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
+    unsigned long long* dst = nullptr;
+    const int nblk = (int)((B + 15) / 16);
+    if (mf && times) {
+      HIP_OK(hipMalloc(&dst, (size_t)nblk * 4 * sizeof(unsigned long long)));
+      a.counts = reinterpret_cast<double*>(dst);
+    }
+    const int rc = mf ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
+                      : nipamd::chain_fb_launch(a, (hipStream_t)stream);
+    a.counts = nullptr;
+    if (dst) {
+      std::vector<unsigned long long> h((size_t)nblk * 4);
+      HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+      HIP_OK(hipMemcpy(h.data(), dst, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      (void)hipFree(dst);
+      double sa = 0, sb = 0, sc = 0;
+      for (int k = 0; k < nblk; k++) {
+        sa += (double)(h[k * 4 + 1] - h[k * 4 + 0]);
+        sb += (double)(h[k * 4 + 2] - h[k * 4 + 1]);
+        sc += (double)(h[k * 4 + 3] - h[k * 4 + 2]);
+      }
+      std::fprintf(stderr, "[nipamd] phase cycles (mean over %d blocks): A %.0f  barrier %.0f  B %.0f\n",
+                   nblk, sa / nblk, sb / nblk, sc / nblk);
+    }
     if (rc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   }
