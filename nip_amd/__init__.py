@@ -178,6 +178,10 @@ class Model:
         return bool(lib().nipamd_model_gpu_supported(self._h, len(obs_vars), _ints(obs_vars),
                                                      len(query), _ints(query)))
 
+    def estep_supported(self) -> bool:
+        """Whether the batched e_step has a GPU plan for this model (the HMM slice)."""
+        return lib().nipamd_estep_partial_size(self._h) >= 0
+
     def original(self, c: int) -> np.ndarray:
         n = lib().nipamd_model_original(self._h, c, None, 0)
         out = np.zeros(n)

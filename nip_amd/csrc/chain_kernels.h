@@ -52,6 +52,33 @@ struct ChainFinalize {
   const double* Etab;               // [(M+2)][16]
 };
 
+// wide interface chains (chain_wide.hip): N <= 64 states, up to 4 observed children
+struct WideArgs {
+  const int* obs;        // int32 observations [B][T][n_obs]
+  long obs_bstride;      // elements between sequences
+  int obs_tstride;       // elements between time steps
+  int ncol;              // observed children used (columns)
+  int col[4];            // their columns in obs
+  int M[4];              // their cardinalities
+  const double* tab[4];  // [(M+2)][64] per column: E, then the row sums, then 0
+  const double* ebase;   // [64] product of the unobserved children's row sums
+  long B;
+  int T, H, N;
+  const double* A;       // [64][64]
+  const double* pi;      // [64]
+  const double* s;       // [64] m1 weights: product of all children's row sums
+  double* S;             // scratch [B][T + 2G][64]
+  double* post;
+  long post_bstride;
+  int post_tstride;
+  int post_off;
+  double* ll;
+  unsigned* status;
+};
+__host__ __device__ inline long chain_scratch_row64(int T) { return (long)(T + 2 * kScratchGuard) * 64; }
+size_t chain_wide_lds_bytes(int ncol, int T);
+int chain_wide_launch(const WideArgs& a, hipStream_t stream);
+
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block

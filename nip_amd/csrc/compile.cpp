@@ -571,55 +571,119 @@ std::string model_desc_json(const Model& m) {
 }
 
 // ------------------------------------------------------------------
-// Chain (HMM) execution plan.
+// Interface-chain execution plan (model.h).
 // ------------------------------------------------------------------
+namespace {
+// flat index of an assignment in a clique table (dimension 0 fastest)
+long clique_index(const Model& m, int c, const std::vector<int>& val_of_var) {
+  long idx = 0, stride = 1;
+  for (int v : m.cliques[c].vars) { idx += val_of_var[v] * stride; stride *= m.vars[v].card; }
+  return idx;
+}
+}  // namespace
+
 void build_chain_plan(Model& m) {
   ChainPlan& P = m.chain;
   P = ChainPlan();
-  if (m.outgoing.size() != 1 || m.cliques.size() != 2 || m.vars.size() != 3) return;
+  if (m.outgoing.size() != 1 || m.previous_outgoing.size() != 1) return;
   const int vp = m.previous_outgoing[0], vc = m.outgoing[0];
-  if (m.in_clique != m.out_clique || m.in_clique < 0) return;
-  const int ct = m.in_clique, ce = 1 - ct;
-  const auto& tv = m.cliques[ct].vars;
-  if (tv.size() != 2 || std::find(tv.begin(), tv.end(), vp) == tv.end() ||
-      std::find(tv.begin(), tv.end(), vc) == tv.end()) return;
-  int vo = -1;
-  for (int v = 0; v < 3; v++) if (v != vp && v != vc) vo = v;
-  const auto& ev = m.cliques[ce].vars;
-  if (ev.size() != 2 || std::find(ev.begin(), ev.end(), vc) == ev.end() ||
-      std::find(ev.begin(), ev.end(), vo) == ev.end()) return;
-  // structural roles: vp independent (prior), vc child of vp, vo child of vc
-  if (!m.vars[vp].parents.empty() || m.vars[vc].parents != std::vector<int>{vp} ||
-      m.vars[vo].parents != std::vector<int>{vc}) return;
-  if (m.vars[vp].family != ct || m.vars[vc].family != ct || m.vars[vo].family != ce) return;
-  const int N = m.vars[vp].card, M = m.vars[vo].card;
-  if (N > 16 || N < 1 || M < 1 || M > 1024) return;
-  P.N = N; P.M = M; P.v_prev = vp; P.v_cur = vc; P.v_obs = vo; P.c_trans = ct; P.c_emit = ce;
-  P.A.assign(256, 0.0);
-  const auto& ot = m.cliques[ct].original;
-  const bool prev_first = tv[0] == vp;       // dimension 0 = lower ID
-  for (int x = 0; x < N; x++)
-    for (int y = 0; y < N; y++) P.A[x * 16 + y] = prev_first ? ot[x + N * y] : ot[y + N * x];
-  const auto& oe = m.cliques[ce].original;
-  const bool cur_first = ev[0] == vc;
-  P.Etab.assign((size_t)(M + 2) * 16, 0.0);
-  std::vector<double> s(16, 0.0);
-  for (int y = 0; y < N; y++) {
-    for (int mm = 0; mm < M; mm++) {
-      double e = cur_first ? oe[y + N * mm] : oe[mm + M * y];
-      P.Etab[(size_t)mm * 16 + y] = e;
-      s[y] += e;   // nip_general_marginalise order over the clique isn't needed: tolerance
+  const auto& V = m.vars;
+  const int N = V[vc].card;
+  if (N < 1 || N > 64 || V[vp].card != N) return;
+  if (!V[vp].parents.empty() || !V[vp].has_prior) return;
+  // the in-clique: the one clique holding prev; it must hold cur too
+  int cin = -1;
+  for (size_t c = 0; c < m.cliques.size(); c++) {
+    const auto& cv = m.cliques[c].vars;
+    if (std::find(cv.begin(), cv.end(), vp) != cv.end()) {
+      if (cin >= 0) return;
+      cin = (int)c;
     }
-    P.Etab[(size_t)M * 16 + y] = s[y];
   }
-  P.pi.assign(16, 0.0);
-  for (int x = 0; x < N; x++) P.pi[x] = m.vars[vp].prior[x];
-  P.ts.assign(16, 0.0);
-  for (int x = 0; x < N; x++) {
-    double acc = 0;
-    for (int y = 0; y < N; y++) acc += P.A[x * 16 + y] * s[y];
-    P.ts[x] = acc;
+  if (cin < 0) return;
+  const auto& inv = m.cliques[cin].vars;
+  if (std::find(inv.begin(), inv.end(), vc) == inv.end()) return;
+  if (V[vc].family != cin) return;
+  // cur's parents: prev plus hidden independent variables living only in the in-clique
+  std::vector<int> hidden;
+  for (int v : inv) {
+    if (v == vp || v == vc) continue;
+    // (an independent parent of cur is flagged INCOMING; its prior is entered every slice)
+    if (!V[v].parents.empty() || !V[v].has_prior || (V[v].ifs & (IF_OUTGOING | IF_OLD_OUTGOING))) return;
+    if (std::find(V[vc].parents.begin(), V[vc].parents.end(), v) == V[vc].parents.end()) return;
+    hidden.push_back(v);
   }
+  if (V[vc].parents.size() != hidden.size() + 1 ||
+      std::find(V[vc].parents.begin(), V[vc].parents.end(), vp) == V[vc].parents.end()) return;
+  long hsize = 1;
+  for (int h : hidden) { hsize *= V[h].card; if (hsize > (1L << 24)) return; }
+  // every other clique: {cur, o}, o a leaf child of cur in no other clique
+  std::vector<int> seen(V.size(), 0);
+  for (int v : inv) seen[v] = 1;
+  std::vector<ChainEmit> emits;
+  for (size_t c = 0; c < m.cliques.size(); c++) {
+    if ((int)c == cin) continue;
+    const auto& cv = m.cliques[c].vars;
+    if (cv.size() != 2 || std::find(cv.begin(), cv.end(), vc) == cv.end()) return;
+    const int o = cv[0] == vc ? cv[1] : cv[0];
+    if (seen[o] || V[o].parents != std::vector<int>{vc} || V[o].family != (int)c ||
+        (V[o].ifs & (IF_OUTGOING | IF_OLD_OUTGOING))) return;
+    seen[o] = 1;
+    ChainEmit E;
+    E.var = o; E.clique = (int)c; E.M = V[o].card;
+    if (E.M < 1 || E.M > 253) return;
+    E.E.assign((size_t)E.M * 64, 0.0);
+    E.s.assign(64, 0.0);
+    std::vector<int> val(V.size(), 0);
+    for (int y = 0; y < N; y++)
+      for (int mm = 0; mm < E.M; mm++) {
+        val[vc] = y; val[o] = mm;
+        const double e = m.cliques[c].original[clique_index(m, (int)c, val)];
+        E.E[(size_t)mm * 64 + y] = e;
+        E.s[y] += e;
+      }
+    emits.push_back(std::move(E));
+  }
+  for (size_t v = 0; v < V.size(); v++) if (!seen[v]) return;   // every variable accounted for
+  // transition with the hidden parents summed out under their priors
+  P.A64.assign(64 * 64, 0.0);
+  std::vector<int> val(V.size(), 0);
+  std::vector<int> hv(hidden.size(), 0);
+  for (long hi = 0; hi < hsize; hi++) {
+    long r = hi;
+    double w = 1.0;
+    for (size_t k = 0; k < hidden.size(); k++) {
+      const int c = V[hidden[k]].card;
+      hv[k] = (int)(r % c); r /= c;
+      val[hidden[k]] = hv[k];
+      w *= V[hidden[k]].prior[hv[k]];
+    }
+    for (int x = 0; x < N; x++)
+      for (int y = 0; y < N; y++) {
+        val[vp] = x; val[vc] = y;
+        P.A64[x * 64 + y] += m.cliques[cin].original[clique_index(m, cin, val)] * w;
+      }
+  }
+  P.N = N; P.v_prev = vp; P.v_cur = vc; P.c_trans = cin;
+  P.hidden = hidden;
+  P.emits = std::move(emits);
+  P.pi64.assign(64, 0.0);
+  for (int x = 0; x < N; x++) P.pi64[x] = V[vp].prior[x];
+  P.s_all64.assign(64, 0.0);
+  for (int y = 0; y < N; y++) {
+    double s = 1.0;
+    for (const auto& E : P.emits) s *= E.s[y];
+    P.s_all64[y] = s;
+  }
+  if (N <= 16) {
+    P.A.assign(256, 0.0);
+    P.pi.assign(16, 0.0);
+    for (int x = 0; x < N; x++) {
+      P.pi[x] = P.pi64[x];
+      for (int y = 0; y < N; y++) P.A[x * 16 + y] = P.A64[x * 64 + y];
+    }
+  }
+  P.hmm = hidden.empty() && P.emits.size() == 1 && V.size() == 3 && N <= 16;
   P.valid = true;
 }
 

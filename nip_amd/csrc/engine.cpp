@@ -42,13 +42,26 @@ int fail(int code, const std::string& msg) {
                                            hipGetErrorString(e_));           \
   } while (0)
 
+// Device tables that depend on which children a request observes.
+struct ReqTables {
+  std::string key;                // emit index per observed column
+  int M0 = 0;                     // narrow kernels: rows of Etab16 are M0 + 2
+  double* Etab16 = nullptr;       // [(M0+2)][16]
+  double* ts16 = nullptr;         // [16] w = A s_all (matrix-core kernel's ll)
+  double* tabw = nullptr;         // wide kernel: per column [(M_k+2)][64], concatenated
+  std::vector<size_t> tabw_off;
+  double* ebase = nullptr;        // [64] product of the unobserved children's row sums
+};
+
 struct DevState {
   int device = -1;
   unsigned version = 0;
-  double* A = nullptr;
-  double* Etab = nullptr;
-  double* pi = nullptr;
-  double* ts = nullptr;
+  double* A = nullptr;            // [16][16]  (N <= 16)
+  double* pi = nullptr;           // [16]
+  double* A64 = nullptr;          // [64][64]
+  double* pi64 = nullptr;         // [64]
+  double* sall64 = nullptr;       // [64]
+  std::vector<ReqTables> reqs;
   double* S = nullptr;
   size_t S_bytes = 0;
   double* R = nullptr;     // E-step partial [chain_estep_slab(M)] of nipamd_estep
@@ -61,11 +74,28 @@ DevState* dev_of(nipamd_model* mm) {
   return static_cast<DevState*>(mm->m.dev);
 }
 
+void free_tables(DevState* d) {
+  (void)hipFree(d->A); (void)hipFree(d->pi); (void)hipFree(d->A64); (void)hipFree(d->pi64);
+  (void)hipFree(d->sall64);
+  d->A = d->pi = d->A64 = d->pi64 = d->sall64 = nullptr;
+  for (auto& r : d->reqs) {
+    (void)hipFree(r.Etab16); (void)hipFree(r.ts16); (void)hipFree(r.tabw); (void)hipFree(r.ebase);
+  }
+  d->reqs.clear();
+}
+
 void dev_release(DevState* d) {
   if (!d) return;
-  (void)hipFree(d->A); (void)hipFree(d->Etab); (void)hipFree(d->pi); (void)hipFree(d->ts); (void)hipFree(d->S);
-  (void)hipFree(d->W); (void)hipFree(d->R);
+  free_tables(d);
+  (void)hipFree(d->S); (void)hipFree(d->W); (void)hipFree(d->R);
   *d = DevState();
+}
+
+template <typename V>
+int upload(double** dst, const V& v) {
+  HIP_OK(hipMalloc(dst, (v.size() ? v.size() : 1) * sizeof(double)));
+  if (v.size()) HIP_OK(hipMemcpy(*dst, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice));
+  return 0;
 }
 
 // Upload the chain plan's tables to the current device (once per version).
@@ -74,19 +104,92 @@ int ensure_tables(nipamd_model* mm) {
   HIP_OK(hipGetDevice(&dev));
   DevState* d = dev_of(mm);
   if (d->device != dev) { dev_release(d); d->device = dev; }
-  if (d->version == mm->version && d->A) return 0;
+  if (d->version == mm->version && d->A64) return 0;
   const auto& P = mm->m.chain;
-  (void)hipFree(d->A); (void)hipFree(d->Etab); (void)hipFree(d->pi); (void)hipFree(d->ts);
-  d->A = d->Etab = d->pi = d->ts = nullptr;
-  HIP_OK(hipMalloc(&d->A, P.A.size() * sizeof(double)));
-  HIP_OK(hipMalloc(&d->Etab, P.Etab.size() * sizeof(double)));
-  HIP_OK(hipMalloc(&d->pi, P.pi.size() * sizeof(double)));
-  HIP_OK(hipMalloc(&d->ts, P.ts.size() * sizeof(double)));
-  HIP_OK(hipMemcpy(d->A, P.A.data(), P.A.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(d->Etab, P.Etab.data(), P.Etab.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(d->pi, P.pi.data(), P.pi.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(d->ts, P.ts.data(), P.ts.size() * sizeof(double), hipMemcpyHostToDevice));
+  free_tables(d);
+  if (P.N <= 16) {
+    if (int rc = upload(&d->A, P.A)) return rc;
+    if (int rc = upload(&d->pi, P.pi)) return rc;
+  }
+  if (int rc = upload(&d->A64, P.A64)) return rc;
+  if (int rc = upload(&d->pi64, P.pi64)) return rc;
+  if (int rc = upload(&d->sall64, P.s_all64)) return rc;
   d->version = mm->version;
+  return 0;
+}
+
+// A request's routing through the chain plan: which emission child each
+// observation column is, and which kernel family serves it.
+struct Route {
+  int ncol = 0;                   // observed emission children
+  int col[4] = {-1, -1, -1, -1};  // their columns in obs
+  int emit[4] = {-1, -1, -1, -1}; // their plan.emits index
+  int primary = -1;               // narrow kernels: the child whose table is used
+  int pcol = -1;                  // its column (or -1: never observed)
+  bool narrow = false;            // N <= 16 and at most one observed child
+};
+
+// Tables of a route (built and uploaded once per model version).
+int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
+  DevState* d = dev_of(mm);
+  const auto& P = mm->m.chain;
+  std::string key;
+  for (int i = 0; i < r.ncol; i++) key += std::to_string(r.emit[i]) + ",";
+  key += "|" + std::to_string(r.primary);
+  for (auto& t : d->reqs) if (t.key == key) { *out = &t; return 0; }
+  ReqTables t;
+  t.key = key;
+  const int N = P.N;
+  if (N <= 16) {
+    // narrow: the primary child's table times the other children's row sums
+    std::vector<double> b(16, 0.0);
+    for (int y = 0; y < N; y++) {
+      double v = 1.0;
+      for (size_t k = 0; k < P.emits.size(); k++) if ((int)k != r.primary) v *= P.emits[k].s[y];
+      b[y] = v;
+    }
+    const int M = r.primary >= 0 ? P.emits[r.primary].M : 0;
+    std::vector<double> E((size_t)(M + 2) * 16, 0.0);
+    for (int y = 0; y < N; y++) {
+      for (int m = 0; m < M; m++) E[(size_t)m * 16 + y] = P.emits[r.primary].E[(size_t)m * 64 + y] * b[y];
+      E[(size_t)M * 16 + y] = (r.primary >= 0 ? P.emits[r.primary].s[y] : 1.0) * b[y];
+    }
+    std::vector<double> ts(16, 0.0);
+    for (int x = 0; x < N; x++) {
+      double acc = 0.0;
+      for (int y = 0; y < N; y++) acc += P.A[x * 16 + y] * E[(size_t)M * 16 + y];
+      ts[x] = acc;
+    }
+    t.M0 = M;
+    if (int rc = upload(&t.Etab16, E)) return rc;
+    if (int rc = upload(&t.ts16, ts)) return rc;
+  }
+  // wide: one unscaled table per observed child, the unobserved ones in ebase
+  std::vector<double> W;
+  for (int i = 0; i < r.ncol; i++) {
+    const auto& em = P.emits[r.emit[i]];
+    t.tabw_off.push_back(W.size());
+    const size_t base = W.size();
+    W.resize(base + (size_t)(em.M + 2) * 64, 0.0);
+    for (int y = 0; y < N; y++) {
+      for (int m = 0; m < em.M; m++) W[base + (size_t)m * 64 + y] = em.E[(size_t)m * 64 + y];
+      W[base + (size_t)em.M * 64 + y] = em.s[y];
+    }
+  }
+  std::vector<double> eb(64, 0.0);
+  for (int y = 0; y < N; y++) {
+    double v = 1.0;
+    for (size_t k = 0; k < P.emits.size(); k++) {
+      bool obs = false;
+      for (int i = 0; i < r.ncol; i++) obs |= r.emit[i] == (int)k;
+      if (!obs) v *= P.emits[k].s[y];
+    }
+    eb[y] = v;
+  }
+  if (int rc = upload(&t.tabw, W)) return rc;
+  if (int rc = upload(&t.ebase, eb)) return rc;
+  d->reqs.push_back(std::move(t));
+  *out = &d->reqs.back();
   return 0;
 }
 
@@ -140,19 +243,28 @@ bool use_mfma() {
 }
 
 // Which GPU plan (if any) covers this request.
-int check_chain_request(const nipamd_model* mm, int n_obs, const int* obs_vars,
-                        int n_query, const int* query, int* obs_col, std::string& why) {
+int route_request(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
+                  const int* query, Route& r, std::string& why) {
   const auto& P = mm->m.chain;
-  if (!P.valid) { why = "model slice is not chain-shaped (GPU plan: HMM-shaped DBN)"; return 0; }
-  int col = -1;
-  for (int i = 0; i < n_obs; i++) {
-    if (obs_vars[i] == P.v_obs) { if (col >= 0) { why = "observed variable listed twice"; return 0; } col = i; }
-    else { why = "evidence on a variable other than the emission variable is not in the GPU plan"; return 0; }
+  if (!P.valid) {
+    why = "model slice is not an interface chain (GPU plan: one interface variable, hidden "
+          "independent parents, leaf children; see DESIGN.md)";
+    return 0;
   }
-  if (col < 0 && n_obs > 0) { why = "no usable observation column"; return 0; }
+  r = Route();
+  for (int i = 0; i < n_obs; i++) {
+    int k = -1;
+    for (size_t e = 0; e < P.emits.size(); e++) if (P.emits[e].var == obs_vars[i]) k = (int)e;
+    if (k < 0) { why = "evidence on a variable that is not a leaf child of the interface variable"; return 0; }
+    for (int j = 0; j < r.ncol; j++) if (r.emit[j] == k) { why = "observed variable listed twice"; return 0; }
+    if (r.ncol == 4) { why = "more than four observed children"; return 0; }
+    r.col[r.ncol] = i; r.emit[r.ncol] = k; r.ncol++;
+  }
   for (int i = 0; i < n_query; i++)
     if (query[i] != P.v_cur) { why = "query variable other than the current-slice interface variable"; return 0; }
-  *obs_col = col;
+  r.narrow = P.N <= 16 && r.ncol <= 1;
+  if (r.ncol == 1) { r.primary = r.emit[0]; r.pcol = r.col[0]; }
+  else if (!P.emits.empty()) { r.primary = 0; r.pcol = -1; }
   return 1;
 }
 
@@ -249,8 +361,8 @@ int nipamd_model_param_size(const nipamd_model* mm) { return mm ? nipamd::param_
 int nipamd_model_gpu_supported(const nipamd_model* mm, int n_obs, const int* obs_vars,
                                int n_query, const int* query) {
   if (!mm) return 0;
-  int col; std::string why;
-  return check_chain_request(mm, n_obs, obs_vars, n_query, query, &col, why);
+  Route r; std::string why;
+  return route_request(mm, n_obs, obs_vars, n_query, query, r, why);
 }
 
 int nipamd_model_original(const nipamd_model* mm, int c, double* out, int cap) {
@@ -301,35 +413,63 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   if (!mm || B < 0 || T < 1 || (n_obs > 0 && (!d_obs || !obs_vars)) || (n_query > 0 && (!query || !d_post)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   if (B == 0) return 0;
-  int col = -1;
+  Route r;
   std::string why;
-  if (!check_chain_request(mm, n_obs, obs_vars, n_query, query, &col, why))
+  if (!route_request(mm, n_obs, obs_vars, n_query, query, r, why))
     return fail(NIPAMD_ERROR_UNSUPPORTED, why);
   const auto& P = mm->m.chain;
-  if (P.M + 2 > 255) return fail(NIPAMD_ERROR_UNSUPPORTED, "observation cardinality above 253");
-  if (nipamd::chain_lds_bytes(P.M, T, false) > 96 * 1024)
-    return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
   if (int rc = ensure_tables(mm)) return rc;
-  if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes(B, T))) return rc;
+  ReqTables* rt = nullptr;
+  if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
   DevState* d = dev_of(mm);
-  nipamd::ChainArgs a{};
-  a.obs = d_obs;
-  a.obs_bstride = (long)T * (n_obs > 0 ? n_obs : 1);
-  a.obs_tstride = n_obs > 0 ? n_obs : 1;
-  a.obs_col = col;
-  static const int32_t kNone = -1;
-  if (col < 0) { a.obs = nullptr; }
-  a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = P.M;
-  a.A = d->A; a.Etab = d->Etab; a.pi = d->pi; a.ts = d->ts; a.S = d->S;
   int stride = 0;
   for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  if (!r.narrow) {
+    // wide interface chain: N <= 64, up to four observed children
+    if (nipamd::chain_wide_lds_bytes(r.ncol, T) > 64 * 1024)
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
+    if (int rc = ensure_scratch(mm, (size_t)(B + 2) * nipamd::chain_scratch_row64(T) * sizeof(double))) return rc;
+    nipamd::WideArgs w{};
+    w.obs = d_obs; w.obs_bstride = (long)T * ocols; w.obs_tstride = (int)ocols;
+    w.ncol = r.ncol;
+    for (int i = 0; i < r.ncol; i++) {
+      w.col[i] = r.col[i];
+      w.M[i] = P.emits[r.emit[i]].M;
+      w.tab[i] = rt->tabw + rt->tabw_off[i];
+    }
+    w.ebase = rt->ebase;
+    w.B = B; w.T = T; w.H = T / 2; w.N = P.N;
+    w.A = d->A64; w.pi = d->pi64; w.s = d->sall64; w.S = d->S;
+    w.post = n_query > 0 ? d_post : nullptr;
+    w.post_bstride = (long)T * stride; w.post_tstride = stride;
+    w.ll = d_ll; w.status = d_status;
+    const int nq = n_query > 0 ? n_query : 1;
+    for (int q = 0; q < nq; q++) {
+      w.post_off = q * P.N;
+      if (q > 0) { w.ll = nullptr; w.status = nullptr; }
+      if (nipamd::chain_wide_launch(w, (hipStream_t)stream))
+        return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    }
+    return 0;
+  }
+  const int M0 = rt->M0;
+  if (nipamd::chain_lds_bytes(M0, T, false) > 96 * 1024)
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
+  if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes(B, T))) return rc;
+  nipamd::ChainArgs a{};
+  a.obs = r.pcol >= 0 ? d_obs : nullptr;
+  a.obs_bstride = (long)T * ocols;
+  a.obs_tstride = (int)ocols;
+  a.obs_col = r.pcol;
+  a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = M0;
+  a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
   a.post = d_post;
   a.post_bstride = (long)T * stride;
   a.post_tstride = stride;
   a.post_off = 0;
   a.ll = d_ll;
   a.status = d_status;
-  (void)kNone;
   if (n_query == 0) { a.post = nullptr; }
   // query variables all equal the chain variable: one launch per copy keeps
   // the kernel simple (the common case is exactly one)
@@ -337,7 +477,7 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   for (int q = 0; q < nq; q++) {
     a.post_off = q * P.N;
     if (q > 0) { a.ll = nullptr; a.status = nullptr; }
-    const bool mf = use_mfma() && nipamd::chain_mfma_lds_bytes(P.M, T) <= 160 * 1024;
+    const bool mf = use_mfma() && nipamd::chain_mfma_lds_bytes(M0, T) <= 160 * 1024;
     // diagnostics: NIPAMD_PHASE_TIMES=1 records per-block phase timestamps
     // (start / end of phase A / start of phase B / end) and prints a summary
     static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
@@ -397,8 +537,8 @@ int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* o
 }
 
 int nipamd_estep_partial_size(const nipamd_model* mm) {
-  if (!mm || !mm->m.chain.valid) return -1;
-  return nipamd::chain_estep_slab(mm->m.chain.M);
+  if (!mm || !mm->m.chain.valid || !mm->m.chain.hmm) return -1;
+  return nipamd::chain_estep_slab(mm->m.chain.emits[0].M);
 }
 
 int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
@@ -406,18 +546,25 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
                          void* stream) {
   if (!mm || B < 0 || T < 1 || !d_partial || (n_obs > 0 && (!d_obs || !obs_vars)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
-  int col = -1;
+  Route r;
   std::string why;
-  if (!check_chain_request(mm, n_obs, obs_vars, 0, nullptr, &col, why))
+  if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why))
     return fail(NIPAMD_ERROR_UNSUPPORTED, why);
   const auto& P = mm->m.chain;
-  if (P.M + 2 > 255) return fail(NIPAMD_ERROR_UNSUPPORTED, "observation cardinality above 253");
-  if (nipamd::chain_lds_bytes(P.M, T, true) > 96 * 1024)
+  if (!P.hmm)
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice (prev, cur, one child)");
+  const int col = r.pcol;
+  const int Mo = P.emits[0].M;
+  if (nipamd::chain_lds_bytes(Mo, T, true) > 96 * 1024)
     return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long / observation cardinality too large for the LDS count tables");
-  const int S = nipamd::chain_estep_slab(P.M);
+  const int S = nipamd::chain_estep_slab(Mo);
   hipStream_t st = (hipStream_t)stream;
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   if (int rc = ensure_tables(mm)) return rc;
+  Route rh;
+  rh.primary = 0;
+  ReqTables* rt = nullptr;
+  if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
   const long chunk = B < kEstepChunk ? B : kEstepChunk;
   const long nchunks = (B + kEstepChunk - 1) / kEstepChunk;
   const long lvl = (chunk + 63) / 64;
@@ -438,8 +585,8 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
     a.obs_bstride = (long)T * ocols;
     a.obs_tstride = ocols;
     a.obs_col = col;
-    a.B = nb; a.T = T; a.H = T / 2; a.N = P.N; a.M = P.M;
-    a.A = d->A; a.Etab = d->Etab; a.pi = d->pi; a.ts = d->ts; a.S = d->S;
+    a.B = nb; a.T = T; a.H = T / 2; a.N = P.N; a.M = Mo;
+    a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.counts = slab;
@@ -457,21 +604,25 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   const auto& P = mm->m.chain;
-  if (!P.valid) return fail(NIPAMD_ERROR_UNSUPPORTED, "model slice is not chain-shaped");
+  if (!P.valid || !P.hmm) return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
   if (int rc = ensure_tables(mm)) return rc;
+  Route rh;
+  rh.primary = 0;
+  ReqTables* rt = nullptr;
+  if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
   DevState* d = dev_of(mm);
   nipamd::ChainFinalize f{};
-  f.N = P.N; f.M = P.M;
+  f.N = P.N; f.M = P.emits[0].M;
   int off = 0;
   for (size_t v = 0; v < mm->m.vars.size(); v++) {
     if ((int)v == P.v_prev) f.off_prev = off;
     if ((int)v == P.v_cur) f.off_cur = off;
-    if ((int)v == P.v_obs) f.off_obs = off;
+    if ((int)v == P.emits[0].var) f.off_obs = off;
     int s = mm->m.vars[v].card;
     for (int p : mm->m.vars[v].parents) s *= mm->m.vars[p].card;
     off += s;
   }
-  f.A = d->A; f.Etab = d->Etab;
+  f.A = d->A; f.Etab = rt->Etab16;
   if (nipamd::estep_finalize_launch(d_partial, f, d_counts, (hipStream_t)stream))
     return fail(NIPAMD_ERROR_DEVICE, "finalize launch failed");
   return 0;

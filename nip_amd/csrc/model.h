@@ -47,22 +47,37 @@ struct NetSpec {
   std::vector<Pot> pots;
 };
 
-// Chain plan: the slice is an HMM over one interface variable
-// (SURVEY 8(d) config 2): transition table A[x][y] = in_clique original over
-// (previous x, current y), emission table E[y][m] = the observation clique's
-// original over (current y, observed m), prior pi over the previous-slice
-// variable.  Padded to 16 states for the gfx950 kernels.
-struct ChainPlan {
-  bool valid = false;
-  int N = 0, M = 0;                 // hidden / observed cardinalities
-  int v_prev = -1, v_cur = -1, v_obs = -1;
-  int c_trans = -1, c_emit = -1;
-  std::vector<double> A;            // [16][16]  A[x*16+y]
-  std::vector<double> Etab;         // [(M+2)][16]: rows 0..M-1 = E[.,m], M = column sums (missing), M+1 = 0
-  std::vector<double> pi;           // [16]
-  std::vector<double> ts;           // [16]  ts[x] = sum_y A[x][y] * s[y]
+// Interface-chain plan: the slice reduces to a chain over its one interface
+// variable (prev -> cur).  The in-clique holds prev, cur and hidden
+// independent parents H of cur, which are summed out with their priors into
+// the transition A[x][y] = sum_H orig(x, y, H) prod_h prior_h; every other
+// clique is {cur, o} for a leaf child o of cur (an "emission" child, observed
+// or not).  SURVEY 8(d) configs 2 (HMM), 3 (demo1, H = {D1}) and 5 (wide
+// clique, H = {Y1, Z1}) are all of this shape.
+struct ChainEmit {
+  int var = -1;                     // the child variable
+  int clique = -1;                  // its clique {cur, o}
+  int M = 0;                        // card(o)
+  std::vector<double> E;            // [M][64]: E[m*64 + y] = clique original at (cur = y, o = m)
+  std::vector<double> s;            // [64]: sum_m E (factor of a missing observation)
 };
 
+struct ChainPlan {
+  bool valid = false;
+  int N = 0;                        // card(prev) == card(cur), <= 64
+  int v_prev = -1, v_cur = -1;
+  int c_trans = -1;                 // the in-clique
+  std::vector<int> hidden;          // H
+  std::vector<ChainEmit> emits;
+  std::vector<double> A64;          // [64][64]
+  std::vector<double> pi64;         // [64] prior of prev
+  std::vector<double> s_all64;      // [64] product of every child's s
+  // the 16-state layout of the same tables (N <= 16 kernels)
+  std::vector<double> A;            // [16][16]
+  std::vector<double> pi;           // [16]
+  // classic HMM (exactly prev, cur and one child): the e_step plan
+  bool hmm = false;
+};
 struct Model {
   std::vector<Var> vars;
   std::vector<Clique> cliques;

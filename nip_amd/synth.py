@@ -60,6 +60,22 @@ def demo1_spec(card: int = 32, seed: int = 12345):
     return nodes, pots
 
 
+def wide_spec(card: int = 64, obs_card: int = 16, seed: int = 12345):
+    """X0 (NIP_next X1), Y1, Z1, X1 at `card` states, O1
+    observed at `obs_card`; potentials (X1 | X0 Y1 Z1), (O1 | X1) and priors
+    X0, Y1, Z1, so the in-clique {X0, Y1, Z1, X1} holds card^4 entries."""
+    nodes = [("X0", card, "X1"), ("Y1", card, None), ("Z1", card, None),
+             ("X1", card, None), ("O1", obs_card, None)]
+    pots = [
+        ("X1", ["X0", "Y1", "Z1"], cpt(seed, card, card ** 3)),
+        ("O1", ["X1"], cpt(seed + 1, obs_card, card)),
+        ("X0", [], cpt(seed + 2, card, 1)),
+        ("Y1", [], cpt(seed + 3, card, 1)),
+        ("Z1", [], cpt(seed + 4, card, 1)),
+    ]
+    return nodes, pots
+
+
 def observations(B: int, T: int, card: int, seed: int = 1, n_obs: int = 1) -> np.ndarray:
     """int32 [B, T, n_obs] uniform states."""
     u = splitmix64(seed, B * T * n_obs) % np.uint64(card)

@@ -157,7 +157,8 @@ class PortOracle:
 
     def fb(self, obs, obs_vars, vint, filter_only=False):
         obs_vars = np.asarray(obs_vars, np.int32)
-        T = int(np.asarray(obs).size // max(len(obs_vars), 1))
+        a = np.asarray(obs)
+        T = a.shape[0] if a.ndim == 2 else int(a.size // max(len(obs_vars), 1))
         o = _obs2d(obs, T, len(obs_vars))
         vint = np.asarray(vint, np.int32)
         post = np.zeros((T, _post_stride(self.desc, vint)))
@@ -266,7 +267,8 @@ class RefHarness:
 
     def fb(self, obs, obs_vars, vint, filter_only=False):
         obs_vars = np.asarray(obs_vars, np.int32)
-        T = int(np.asarray(obs).size // max(len(obs_vars), 1))
+        a = np.asarray(obs)
+        T = a.shape[0] if a.ndim == 2 else int(a.size // max(len(obs_vars), 1))
         o = _obs2d(obs, T, len(obs_vars))
         vint = np.asarray(vint, np.int32)
         post = np.zeros((T, _post_stride(self.desc, vint)))

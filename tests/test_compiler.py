@@ -81,4 +81,15 @@ def test_chain_plan_recognition():
     m = nip_amd.Model.from_spec(*synth.hmm_spec(16, 16))
     assert m.gpu_supported([m.variable("M1")], [m.variable("P1")])
     d = nip_amd.Model.from_net(os.path.join(GOLD, "demo1.net"))
-    assert not d.gpu_supported([d.variable("A1")], [d.variable("C1")])
+    # demo1: interface C, hidden independent parent D1 folded into the
+    # transition, observed leaf children A1, B1 (SURVEY 8(d) config 3 shape)
+    assert d.gpu_supported([d.variable("A1"), d.variable("B1")], [d.variable("C1")])
+    assert d.gpu_supported([d.variable("B1")], [d.variable("C1")])
+    assert not d.gpu_supported([d.variable("A1")], [d.variable("D1")])      # query off the chain
+    assert not d.gpu_supported([d.variable("D1")], [d.variable("C1")])      # evidence on a folded parent
+    # a slice with two interface variables is not an interface chain
+    nodes = [("a0", 2, "a1"), ("b0", 2, "b1"), ("a1", 2, None), ("b1", 2, None), ("o", 2, None)]
+    pots = [("a0", [], None), ("b0", [], None), ("a1", ["a0"], None), ("b1", ["b0", "a1"], None),
+            ("o", ["b1"], None)]
+    w = nip_amd.Model.from_spec(nodes, pots)
+    assert not w.gpu_supported([w.variable("o")], [w.variable("a1")])

@@ -43,7 +43,7 @@ def chain_fixtures():
     for p in sorted(glob.glob(os.path.join(GOLD, "fb_*.npz"))):
         z = np.load(p)
         m = product_model(str(z["model"]))
-        if m.gpu_supported(list(z["obs_vars"]), []):
+        if m.estep_supported() and m.gpu_supported(list(z["obs_vars"]), []):
             out.append(p)
     return out
 

@@ -1,0 +1,132 @@
+"""GPU parity of the interface-chain plan beyond the plain HMM: hidden
+independent parents folded into the transition, several observed children,
+and up to 64 interface states (SURVEY 8(d) configs 3 and 5 shapes).
+
+Reference: the reference's own outputs (tests/golden/fb_demo1*.npz) and the
+CPU oracle.  Tolerances as test_gpu_parity: posteriors 1e-12 absolute, ll
+1e-12 relative (configs with 32/64 states: 1e-11, longer fp64 sums).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+import nip_amd
+from nip_amd import synth
+from oracle.bind import PortOracle
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DBL_MAX = np.finfo(np.float64).max
+
+
+def gpu_fb(model, obs, ov, q):
+    o = torch.from_numpy(np.ascontiguousarray(obs, np.int32)).cuda()
+    post, ll, st = nip_amd.forward_backward_inference(model, o, ov, q)
+    torch.cuda.synchronize()
+    return post.cpu().numpy(), ll.cpu().numpy(), st.cpu().numpy()
+
+
+def check_vs_oracle(m, obs, ov, q, ptol=1e-12, ltol=1e-12):
+    post, ll, st = gpu_fb(m, obs, ov, q)
+    orc = PortOracle(m.desc())
+    for b in range(obs.shape[0]):
+        rp, rl = orc.fb(obs[b], ov, q)
+        err = np.abs(post[b] - rp).max()
+        assert err <= ptol, "sequence %d: posterior error %g" % (b, err)
+        if rl == -DBL_MAX:
+            assert ll[b] == -DBL_MAX and st[b]
+        else:
+            assert abs(ll[b] - rl) <= ltol * max(1.0, abs(rl)), (b, ll[b], rl)
+
+
+@pytest.mark.parametrize("fixture", ["fb_demo1.npz", "fb_demo1_card4.npz"])
+def test_demo1_vs_reference_fixture(fixture):
+    """Both observed children (A1, B1), the reference's own posteriors of C1."""
+    z = np.load(os.path.join(GOLD, fixture))
+    name = str(z["model"])
+    if name == "demo1":
+        m = nip_amd.Model.from_net(os.path.join(GOLD, "demo1.net"))
+    else:
+        m = nip_amd.Model.from_spec(*synth.demo1_spec(4))
+    c1 = m.variable("C1")
+    q = [int(x) for x in z["query"]]
+    assert q[0] == c1
+    post, ll, st = gpu_fb(m, z["obs"], list(z["obs_vars"]), [c1])
+    N = m.card(c1)
+    assert np.abs(post - z["post"][:, :, :N]).max() <= 1e-12
+    assert np.all(np.abs(ll - z["ll"]) <= 1e-12 * np.maximum(1, np.abs(z["ll"])))
+
+
+@pytest.mark.parametrize("observed", [["A1", "B1"], ["B1", "A1"], ["B1"], ["A1"], []])
+def test_demo1_observed_subsets(observed):
+    m = nip_amd.Model.from_net(os.path.join(GOLD, "demo1.net"))
+    ov = [m.variable(s) for s in observed]
+    rng = np.random.default_rng(len(observed) * 7 + 1)
+    cards = [m.card(v) for v in ov]
+    obs = np.stack([rng.integers(-1, c, size=(9, 29)) for c in cards], axis=2) if ov else \
+        np.zeros((9, 29, 0), np.int32)
+    check_vs_oracle(m, obs.astype(np.int32), ov, [m.variable("C1")])
+
+
+def test_demo1_card32_config3_shape():
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(32))
+    ov = [m.variable("A1"), m.variable("B1")]
+    obs = synth.observations(5, 24, 32, seed=3, n_obs=2)
+    obs[0, 3, 1] = -1
+    check_vs_oracle(m, obs, ov, [m.variable("C1")], 1e-12, 1e-11)
+
+
+@pytest.mark.parametrize("card,ocard,B,T", [(8, 5, 6, 19), (16, 16, 3, 12)])
+def test_wide_clique_config5_shape(card, ocard, B, T):
+    m = nip_amd.Model.from_spec(*synth.wide_spec(card, ocard))
+    ov = [m.variable("O1")]
+    obs = synth.observations(B, T, ocard, seed=card)
+    check_vs_oracle(m, obs, ov, [m.variable("X1")], 1e-12, 1e-11)
+
+
+def test_wide_clique_32_states_vs_oracle():
+    """Config 5 shape at 32 states: 32^4-entry in-clique through the oracle."""
+    m = nip_amd.Model.from_spec(*synth.wide_spec(32, 16))
+    ov = [m.variable("O1")]
+    obs = synth.observations(2, 4, 16, seed=5)
+    check_vs_oracle(m, obs, ov, [m.variable("X1")], 1e-12, 1e-11)
+
+
+def test_wide_clique_64_states_properties():
+    """Config 5 at full width (64 states, 64^4-entry in-clique): B=256, T=128."""
+    m = nip_amd.Model.from_spec(*synth.wide_spec(64, 16))
+    ov = [m.variable("O1")]
+    obs = torch.from_numpy(synth.observations(256, 128, 16, seed=6)).cuda()
+    post, ll, st = nip_amd.forward_backward_inference(m, obs, ov, [m.variable("X1")])
+    torch.cuda.synchronize()
+    assert not st.any().item()
+    s = post.sum(dim=2)
+    assert torch.allclose(s, torch.ones_like(s), atol=1e-12, rtol=0)
+    assert bool((ll <= 0).all()) and bool(torch.isfinite(ll).all())
+    # time reversal of a single step sequence: posterior of T=1 = prior-propagated evidence
+    one = obs[:4, :1].contiguous()
+    p1, l1, _ = nip_amd.forward_backward_inference(m, one, ov, [m.variable("X1")])
+    torch.cuda.synchronize()
+    assert torch.allclose(p1.sum(dim=2), torch.ones(4, 1, dtype=torch.float64, device="cuda"), atol=1e-12)
+
+
+def test_config3_scale_properties():
+    """demo1 @ 32 states, 2048 sequences x T=256: normalised posteriors, ll <= 0."""
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(32))
+    ov = [m.variable("A1"), m.variable("B1")]
+    obs = torch.from_numpy(synth.observations(2048, 256, 32, seed=9, n_obs=2)).cuda()
+    post, ll, st = nip_amd.forward_backward_inference(m, obs, ov, [m.variable("C1")])
+    torch.cuda.synchronize()
+    assert not st.any().item()
+    s = post.sum(dim=2)
+    assert torch.allclose(s, torch.ones_like(s), atol=1e-12, rtol=0)
+    assert bool((ll <= 0).all()) and bool(torch.isfinite(ll).all())
+    orc = PortOracle(m.desc())
+    o = obs.cpu().numpy()
+    for b in (0, 2047):
+        rp, rl = orc.fb(o[b], ov, [m.variable("C1")])
+        assert np.abs(post[b].cpu().numpy() - rp).max() <= 1e-12
+        assert abs(ll[b].item() - rl) <= 1e-11 * abs(rl)
