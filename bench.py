@@ -26,36 +26,48 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from nip_amd import synth  # noqa: E402  (numpy only; the HIP library loads on first use)
+
 METRIC = "sequence-timesteps/s fwd-bwd smoothing, 16-state DBN; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0            # MI355X spec (MI355X_MICROARCH.md chip table)
 
 
-def algorithmic_bytes_per_seq_step(N: int) -> int:
-    """What the path must move per sequence-timestep (Roofline):
-    observation int32 read once (4 B), one 16-wide fp64 interface message
-    written and read back (alpha for t < T/2, beta for t >= T/2: 2 x 128 B),
-    the N-wide fp64 posterior written (8N B)."""
-    return 4 + 2 * 16 * 8 + 8 * N
+def algorithmic_bytes_per_seq_step(N: int, n_obs: int = 1, posterior: bool = True) -> int:
+    """What the path must move per sequence-timestep:
+    the int32 observations read once (4 B per observed variable), one N-wide
+    fp64 interface message written and read back (alpha for t < T/2, beta for
+    t >= T/2: 2 x 8N B), the N-wide fp64 posterior written (8N B, fb only)."""
+    return 4 * n_obs + 2 * 8 * N + (8 * N if posterior else 0)
 
 
-def cpu_baseline(nodes, pots, obs, budget_s: float = 12.0):
-    """Reference CPU path on this host, single core, bounded sample."""
+# name -> (SURVEY 8(d) config, spec builder, observed vars, query var, default B, T)
+WORKLOADS = {
+    "fb": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 4096, 1024),
+    "estep": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024),
+    "config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256),
+    "config5": ("config5", lambda a: synth.wide_spec(64, 16), ["O1"], "X1", 256, 128),
+}
+
+
+def cpu_baseline(nodes, pots, obs, ov, q, budget_s: float = 12.0, t_sample: int = 0):
+    """Reference CPU path on this host, single core, bounded sample.  ov / q are
+    variable indices in declaration order; t_sample > 0 times only the first
+    t_sample slices of each sequence (config 5's 16.7M-entry clique)."""
     from oracle import bind
-    from nip_amd import synth
     kind = "reference"
     try:
         if not bind.ref_available():
             raise RuntimeError("oracle/_ref not built")
-        orc = bind.RefHarness(synth.spec_to_replay(nodes, pots))
+        orc = bind.RefHarness(synth.spec_to_replay(nodes, pots), cards=[n[1] for n in nodes])
     except Exception:
         kind = "port"
         import nip_amd
         orc = bind.PortOracle(nip_amd.Model.from_spec(nodes, pots).desc())
-    T = obs.shape[1]
+    T = t_sample or obs.shape[1]
     t0 = time.perf_counter()
     n = 0
     while True:
-        orc.fb(obs[n], [2], [1])
+        orc.fb(obs[n][:T], ov, [q])
         n += 1
         el = time.perf_counter() - t0
         if el >= budget_s or n >= obs.shape[0]:
@@ -86,13 +98,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="sequences per GPU")
-    ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=0, help="sequences per GPU (0: the workload's)")
+    ap.add_argument("--T", type=int, default=0, help="time slices (0: the workload's)")
     ap.add_argument("--N", type=int, default=16)
     ap.add_argument("--M", type=int, default=16)
-    ap.add_argument("--workload", choices=["fb", "estep"], default="fb",
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb",
                     help="fb: the headline metric (config 2 smoothing); estep: one batched "
-                         "e_step (config 4 per-GPU shard: counts + ll, no posterior write)")
+                         "e_step (config 4 per-GPU shard: counts + ll, no posterior write); "
+                         "config3: demo1 @ 32 states smoothing; config5: wide-clique smoothing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
     args = ap.parse_args()
@@ -100,7 +113,6 @@ def main():
     import torch
     import torch.distributed as dist
     import nip_amd
-    from nip_amd import synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,19 +123,22 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    B, T, N, M = args.batch, args.T, args.N, args.M
-    nodes, pots = synth.hmm_spec(N, M)
+    cfg, spec, ov_names, q_name, B0, T0 = WORKLOADS[args.workload]
+    B, T = args.batch or B0, args.T or T0
+    nodes, pots = spec(args)
     model = nip_amd.Model.from_spec(nodes, pots)
-    ov, q = [model.variable("M1")], [model.variable("P1")]
-    obs_np = synth.observations(B, T, M, seed=1 + 7919 * rank)
+    ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
+    N, M = model.card(q), model.card(ov[0])
+    obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
+                             for i, v in enumerate(ov)], axis=2)
     obs = torch.from_numpy(obs_np).to(dev)
     ll = torch.empty((B,), dtype=torch.float64, device=dev)
     st = torch.empty((B,), dtype=torch.int32, device=dev)
-    if args.workload == "fb":
+    if args.workload != "estep":
         post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
 
         def step():
-            nip_amd.forward_backward_inference(model, obs, ov, q, post, ll, st)
+            nip_amd.forward_backward_inference(model, obs, ov, [q], post, ll, st)
     else:
         counts = torch.ones((model.param_size(),), dtype=torch.float64, device=dev)
 
@@ -158,16 +173,31 @@ def main():
 
     units = B * T * args.steps * world
     value = units / elapsed
-    bpu = algorithmic_bytes_per_seq_step(N)
-    kname = "chain_fb_mfma_kernel" if os.environ.get("NIPAMD_FB_KERNEL") != "dpp" else "chain_kernel<false>"
-    workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (N, M, B, T)
+    bpu = algorithmic_bytes_per_seq_step(N, len(ov), args.workload != "estep")
+    narrow = N <= 16 and len(ov) <= 1
+    if not narrow:
+        kname = "chain_wide_kernel<%d>" % (16 if N <= 16 else 32 if N <= 32 else 64)
+    elif os.environ.get("NIPAMD_FB_KERNEL") != "dpp":
+        kname = "chain_fb_mfma_kernel"
+    else:
+        kname = "chain_kernel<false>"
     metric = METRIC
-    if args.workload == "estep":
-        bpu -= 8 * N                  # no posterior write: counts stay on-chip
+    if args.workload == "fb":
+        workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (
+            N, M, B, T)
+    elif args.workload == "estep":
         kname = "chain_kernel<true> + tree64 + finalize"
         workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
             N, M, B, T)
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
+    elif args.workload == "config3":
+        workload = "config3: demo1.net structure, 5 vars x 32 states, A1 B1 observed, C1 posterior, " \
+                   "B=%d seq/GPU x T=%d" % (B, T)
+        metric = "sequence-timesteps/s fwd-bwd smoothing, demo1 @ 32 states"
+    else:
+        workload = "config5: wide clique {X0,Y1,Z1,X1} 64^4 entries, O1 16 states observed, X1 posterior, " \
+                   "B=%d seq/GPU x T=%d" % (B, T)
+        metric = "sequence-timesteps/s fwd-bwd smoothing, wide-clique DBN (64^4 in-clique)"
     achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(workload)
     if rank == 0:
@@ -177,14 +207,17 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload, "B_per_gpu": B, "T": T, "hidden_states": N,
-                       "observed_states": M, "parallelism": "dp%d" % world},
+                       "observed_states": M, "observed_vars": len(ov), "parallelism": "dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel": kname,
                          "kernel_ms": kern_ms, "bytes_per_unit": bpu},
         }
-        if world == 1 and not args.no_cpu_baseline and args.workload == "fb":
-            rec["cpu_baseline"] = cpu_baseline(nodes, pots, obs_np)
+        if world == 1 and not args.no_cpu_baseline and args.workload != "estep":
+            names = [n[0] for n in nodes]
+            rec["cpu_baseline"] = cpu_baseline(
+                nodes, pots, obs_np, [names.index(v) for v in ov_names], names.index(q_name),
+                t_sample=2 if args.workload == "config5" else 0)
         print(json.dumps(rec))
     if world > 1:
         dist.destroy_process_group()

@@ -255,15 +255,30 @@ class RefHarness:
             cls._lib = L
         return cls._lib
 
-    def __init__(self, replay: str):
+    def __init__(self, replay: str, cards=None):
+        """cards: the variables' cardinalities in declaration order, when known;
+        then the JSON description (which prints every clique table -- 16.7M
+        entries for the wide-clique model) is only produced if .desc is read."""
         self.h = self.lib().nh_build(replay.encode())
         if self.h < 0:
             raise RuntimeError("reference harness failed to build the model")
+        self._desc = None if cards is not None else self._load_desc()
+        self._cards = list(cards) if cards is not None else [v["card"] for v in self._desc["vars"]]
+
+    def _load_desc(self):
         cap = 1 << 26
-        buf = C.create_string_buffer(cap)
-        n = self.lib().nh_desc(self.h, buf, cap)
-        assert n < cap
-        self.desc = json.loads(buf.value.decode())
+        while True:
+            buf = C.create_string_buffer(cap)
+            n = self.lib().nh_desc(self.h, buf, cap)
+            if n < cap:
+                return json.loads(buf.value.decode())
+            cap *= 4
+
+    @property
+    def desc(self):
+        if self._desc is None:
+            self._desc = self._load_desc()
+        return self._desc
 
     def fb(self, obs, obs_vars, vint, filter_only=False):
         obs_vars = np.asarray(obs_vars, np.int32)
@@ -271,7 +286,7 @@ class RefHarness:
         T = a.shape[0] if a.ndim == 2 else int(a.size // max(len(obs_vars), 1))
         o = _obs2d(obs, T, len(obs_vars))
         vint = np.asarray(vint, np.int32)
-        post = np.zeros((T, _post_stride(self.desc, vint)))
+        post = np.zeros((T, int(sum(self._cards[v] for v in vint))))
         ll = C.c_double(0)
         fn = self.lib().nh_filter if filter_only else self.lib().nh_fb
         fn(self.h, T, len(obs_vars), obs_vars, o, len(vint), vint, post, C.byref(ll))
