@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cstdint>
+#include <utility>
 
 #include "chain_kernels.h"
 
@@ -52,12 +53,17 @@ namespace nipamd {
 namespace {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
 
 #ifndef NIPAMD_MFMA_ABLATE
-#define NIPAMD_MFMA_ABLATE 0       // timing-only builds: 11 no posterior stores, 12 no phase-B loads
+#define NIPAMD_MFMA_ABLATE 0       // timing-only builds: 11 no posterior stores, 12 no phase-B loads,
+                                   // 14 no phase-B ll, 15 filter step sums every 4th step only
 #endif
 #ifndef NIPAMD_MFMA_PF
 #define NIPAMD_MFMA_PF 1           // partner prefetch distance in chunks (1 or 2)
+#endif
+#ifndef NIPAMD_MFMA_DMA
+#define NIPAMD_MFMA_DMA 1          // phase-B prefetch by LDS-DMA when the LDS budget allows
 #endif
 #ifndef NIPAMD_MFMA_NT
 #define NIPAMD_MFMA_NT 0           // 1: non-temporal posterior stores
@@ -111,6 +117,31 @@ __device__ __forceinline__ double sum8(double x) {
   return x;
 }
 
+// sum8 of n independent values, level by level so the n dependency chains
+// interleave (one wave per SIMD: nothing else hides the f64 latency)
+template <int n>
+__device__ __forceinline__ void sum8_n(double (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += dpp64<0xB1>(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += dpp64<0x4E>(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += dpp64<0x141>(x[i]);
+}
+
+// 1/c for n values, staged like sum8_n; 0 where c == 0
+template <int n>
+__device__ __forceinline__ void recip_n(const double (&c)[n], double (&r)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = __builtin_amdgcn_rcp(c[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = __builtin_fma(r[i], __builtin_fma(-c[i], r[i], 1.0), r[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = __builtin_fma(r[i], __builtin_fma(-c[i], r[i], 1.0), r[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = c[i] != 0.0 ? r[i] : 0.0;
+}
+
 __device__ __forceinline__ v4d matvec(const double (&Aop)[4], v4d X) {
   v4d d = {0.0, 0.0, 0.0, 0.0};
   d = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0], X.x, d, 0, 0, 0);
@@ -153,8 +184,48 @@ __device__ __forceinline__ v4d load4(const double* p) {
 // partner's reads are bank-conflict free.
 __device__ __forceinline__ int piece_off(int j, int s) { return j * 16 + ((s ^ (j & 7)) << 1); }
 
-__device__ __forceinline__ void barrier_lds() {
+#ifndef NIPAMD_WAIT_TIMES
+#define NIPAMD_WAIT_TIMES 0        // diagnostics build: per-wave barrier wait cycles into the stamps
+#endif
+struct WaitAcc {
+  unsigned long long cyc = 0;
+};
+
+__device__ __forceinline__ void barrier_lds(WaitAcc* w = nullptr) {
+#if NIPAMD_WAIT_TIMES
+  const unsigned long long t0 = __builtin_readcyclecounter();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (w) w->cyc += __builtin_readcyclecounter() - t0;
+#else
+  (void)w;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
+// LDS-DMA prefetch of the other direction's vectors (phase B).  Sixteen
+// global_load_lds_dwordx4, one per chain c: lane L reads q + 128 B * c and the
+// 1 KB lands lane-linearly at dst + 1 KB * c, where the drain reads it back
+// with the same lane mapping (conflict-free).  No VGPR is written, so the
+// compiler has nothing to reorder; the completions are counted by hand with
+// s_waitcnt vmcnt (the DMA is invisible to the compiler's own waits).
+template <int C>
+__device__ __forceinline__ void dma1(const double* q, unsigned lds_base) {
+  unsigned keep;
+  // the instruction offset would move the LDS address too: the global address
+  // carries the 128 B * C instead
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(q + C * 16), "s"(lds_base + C * 1024u)
+               : "memory");
+}
+template <int... C>
+__device__ __forceinline__ void dma16(const double* q, unsigned lds_base, std::integer_sequence<int, C...>) {
+  (dma1<C>(q, lds_base), ...);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
 struct WaveCtx {
@@ -174,21 +245,26 @@ struct Chain {
 
   // one step: the interface vector (alpha_t or beta_t, scaled) to LDS row L;
   // the forward filter also publishes its step mass z2 for the partner's ll
+  template <bool SUM = true>
   __device__ __forceinline__ void step(const WaveCtx& c, double* L, double* Z, v4d e) {
     const v4d u = ldexp4(matvec(Aop, X), sc);
     const v4d p = u * e;
     const v4d keep = FWD ? p : u;
     *reinterpret_cast<double2*>(L + c.wo0) = make_double2(keep.x, keep.y);
     *reinterpret_cast<double2*>(L + c.wo1) = make_double2(keep.z, keep.w);
-    const double z2 = chain_sum(p);
-    if (FWD && c.zw) *Z = z2;
-    sc = -__builtin_amdgcn_frexp_exp(z2);   // frexp exponent of 0 is 0
+    if (NIPAMD_MFMA_ABLATE != 15 || SUM) {
+      const double z2 = chain_sum(p);
+      if (FWD && c.zw) *Z = z2;
+      sc = -__builtin_amdgcn_frexp_exp(z2);   // frexp exponent of 0 is 0
+    } else {
+      sc = 0;
+    }
     X = p;
   }
 
   // a phase of n steps from t0 in nch chunks (uniform over the block); all
   // eight codes and evidence vectors of a chunk are read from LDS up front
-  __device__ __forceinline__ void run(const WaveCtx& c, int n, int nch, int t0, int lane) {
+  __device__ __forceinline__ void run(const WaveCtx& c, int n, int nch, int t0, int lane, WaitAcc* w) {
     constexpr int dir = FWD ? 1 : -1;
     for (int ci = 0; ci < nch; ci++) {
       double* slot = c.out + (ci & 1) * kSlotD;
@@ -202,13 +278,16 @@ struct Chain {
       for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + code[k] * 16);
       if (base + kMChunk <= n) {
 #pragma unroll
-        for (int k = 0; k < kMChunk; k++) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+        for (int k = 0; k < kMChunk; k++) {
+          if ((k & 3) == 3) step<true>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+          else step<false>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < kMChunk; k++)
           if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
       }
-      barrier_lds();
+      barrier_lds(w);
     }
   }
 };
@@ -238,15 +317,21 @@ __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c
     ch.X = load4(c.Et + c.codes[T - 1] * 16) * beta;
     ch.sc = -__builtin_amdgcn_frexp_exp(chain_sum(ch.X));
   }
+  WaitAcc wa, wb;
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
-  if (FWD) ch.run(c, H, nchA, 0, lane);
-  else ch.run(c, T - 1 - H, nchA, T - 2, lane);
+  if (FWD) ch.run(c, H, nchA, 0, lane, &wa);
+  else ch.run(c, T - 1 - H, nchA, T - 2, lane, &wa);
   if (stamps && lane == 0) stamps[blockIdx.x * 4 + 1] = __builtin_readcyclecounter();
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   if (stamps && lane == 0) stamps[blockIdx.x * 4 + 2] = __builtin_readcyclecounter();
   // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
-  if (FWD) ch.run(c, T - H, nchB, H, lane);
-  else ch.run(c, H, nchB, H - 1, lane);
+  if (FWD) ch.run(c, T - H, nchB, H, lane, &wb);
+  else ch.run(c, H, nchB, H - 1, lane, &wb);
+  if (NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 4;
+    st[blockIdx.x * 8 + (FWD ? 0 : 1)] = wa.cyc;
+    st[blockIdx.x * 8 + 4 + (FWD ? 0 : 1)] = wb.cyc;
+  }
   (void)active; (void)b;
 }
 
@@ -267,9 +352,8 @@ struct LL {
 #pragma unroll
     for (int q = 0; q < 2; q++) { m2[q] = 1.0; m1[q] = ym; zmin[q] = 1.0; e2[q] = 0; e1[q] = 0; }
   }
-  // step t of chain slot q: alpha piece v, z2 from the filter; last = (t == T-1)
-  __device__ __forceinline__ void step(int q, double2 v, double z2, bool last, bool renorm) {
-    const double y = sum8(v.x * w0 + v.y * w1);
+  // step t of chain slot q: y = alpha_t . w (sum8'd), z2 from the filter; last = (t == T-1)
+  __device__ __forceinline__ void step(int q, double y, double z2, bool last, bool renorm) {
     zmin[q] = __builtin_fmin(zmin[q], z2);
     m2[q] *= z2;
     if (!last) { m1[q] *= y; e1[q] -= __builtin_amdgcn_frexp_exp(z2); }   // 2^sc_{t+1}
@@ -300,13 +384,12 @@ struct LL {
 // value times the other direction's vector (scratch, one chunk prefetched),
 // normalised over the 8 lanes of its step, and -- when N == 16 with 16-byte
 // rows -- one contiguous 1 KB posterior run per store instruction.
-template <bool FWD>
+template <bool FWD, bool PVEC, bool DMA>
 __device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* out, const double* zr,
-                                             double* Sblk, int lane, long b0, int nchA, int nchB) {
+                                             double* Sblk, double* ob_lds, int lane, long b0, int nchA, int nchB) {
   const int T = a.T, H = a.H;
   const int s = lane & 7, hi = lane >> 3;
-  const bool pvec = a.N == 16 && a.post_tstride == 16 && ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
-                    ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
+  constexpr bool pvec = PVEC;        // posterior rows of 16 contiguous, 16-byte aligned doubles
   const int nA = FWD ? H : T - 1 - H, nB = FWD ? T - H : H;
   const int tA = FWD ? 0 : T - 2, tB = FWD ? H : H - 1;
   constexpr int dir = FWD ? 1 : -1;
@@ -322,17 +405,23 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* o
     const double* slot = out + (ci & 1) * kSlotD;
     const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
     const bool full = ci * kMChunk + kMChunk <= n;
+    double y[2 * kMChunk];
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(q * 8 + hi, s));
+        y[2 * k + q] = v.x * ll.w0 + v.y * ll.w1;
+      }
+    sum8_n(y);
 #pragma unroll
     for (int k = 0; k < kMChunk; k++) {
       const int i = ci * kMChunk + k;
       if (i >= n) break;
       const bool last = t0 + i == T - 1;
 #pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int jj = q * 8 + hi;
-        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(jj, s));
-        ll.step(q, v, zs[k * kMSeq + jj], last, !full || (k & 3) == 3);
-      }
+      for (int q = 0; q < 2; q++)
+        ll.step(q, y[2 * k + q], zs[k * kMSeq + q * 8 + hi], last, !full || (k & 3) == 3);
     }
   };
   auto drainA = [&](int ci) {
@@ -351,62 +440,84 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* o
       }
     }
   };
+  WaitAcc wa, wb;
   for (int ci = 0; ci < nchA; ci++) {
     if (ci > 0) drainA(ci - 1);
-    barrier_lds();
+    barrier_lds(&wa);
   }
   if (nchA > 0) drainA(nchA - 1);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 
   // other direction's vectors of chunk ci, all 16 chains, this lane's piece
-  double2 oa[kMSeq], ob[kMSeq];
+  v2d oa[kMSeq], ob[kMSeq];
 #if NIPAMD_MFMA_PF == 2
-  double2 oc[kMSeq];
+  v2d oc[kMSeq];
 #endif
-  auto load_other = [&](double2 (&o)[kMSeq], int ci) {
+  auto load_other = [&](v2d (&o)[kMSeq], int ci) {
     const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
 #pragma unroll
     for (int c = 0; c < kMSeq; c++)
-      o[c] = NIPAMD_MFMA_ABLATE == 12 ? make_double2(1.0 + c, 2.0) : *reinterpret_cast<const double2*>(q + c * 16);
+      o[c] = NIPAMD_MFMA_ABLATE == 12 ? v2d{1.0 + c, 2.0} : *reinterpret_cast<const v2d*>(q + c * 16);
+  };
+  // DMA: buffer k of this partner's two 16 KB LDS buffers
+  const unsigned ob_base = (unsigned)(uintptr_t)ob_lds;
+  auto dma_other = [&](int k, int ci) {
+    const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
+    dma16(q, __builtin_amdgcn_readfirstlane(ob_base + (unsigned)k * (kMSeq * 1024u)),
+          std::make_integer_sequence<int, kMSeq>{});
+  };
+  auto read_other = [&](v2d (&o)[kMSeq], int k) {
+    const double* src = ob_lds + k * (kMSeq * 128) + 2 * lane;
+#pragma unroll
+    for (int c = 0; c < kMSeq; c++) o[c] = *reinterpret_cast<const v2d*>(src + c * 128);
   };
   // spare scratch rows past the last block: target of masked lanes' stores
   double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
-  auto drainB = [&](int ci, const double2 (&o)[kMSeq]) {
-    if (FWD) ll_chunk(ci, nB, tB);
-    if (!a.post) return;
+  auto drainB = [&](int ci, const v2d (&o)[kMSeq]) {
+    if (FWD && NIPAMD_MFMA_ABLATE != 14) ll_chunk(ci, nB, tB);
+    if (!PVEC && !a.post) return;
     const double* slot = out + (ci & 1) * kSlotD;
     const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;   // valid steps
     const bool ok = kB < nk;
     const int t = tlow(ci) + hi;
-    if (pvec) {
-      // branch-free: the 16 chains' work interleaves freely
+    if constexpr (pvec) {
+      // branch-free, eight chains at a time with their dependency chains interleaved
 #pragma unroll
-      for (int q = 0; q < kMSeq; q++) {
-        const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
-        const double px = v.x * o[q].x, py = v.y * o[q].y;
-        const double r = recip(sum8(px + py));      // an all-zero row stays zero
-        const long bb = b0 + q;
+      for (int q0 = 0; q0 < kMSeq; q0 += 8) {
+        double px[8], py[8], z[8], r[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q0 + i, s));
+          px[i] = v.x * o[q0 + i].x; py[i] = v.y * o[q0 + i].y;
+          z[i] = px[i] + py[i];
+        }
+        sum8_n(z);
+        recip_n(z, r);                                   // an all-zero row stays zero
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const long bb = b0 + q0 + i;
 #if NIPAMD_MFMA_ABLATE == 13     // timing-only: block-major posterior layout (wrong layout)
-        double* p = (ok && bb < a.B)
-                        ? a.post + ((size_t)(b0 / kMSeq) * a.T + t) * kStepD + q * 16 + 2 * s
-                        : sink;
+          double* p = (ok && bb < a.B)
+                          ? a.post + ((size_t)(b0 / kMSeq) * a.T + t) * kStepD + (q0 + i) * 16 + 2 * s
+                          : sink;
 #else
-        double* p = (ok && bb < a.B)
-                        ? a.post + (size_t)bb * a.post_bstride + (long)t * 16 + a.post_off + 2 * s
-                        : sink;
+          double* p = (ok && bb < a.B)
+                          ? a.post + (size_t)bb * a.post_bstride + (long)t * 16 + a.post_off + 2 * s
+                          : sink;
 #endif
 #if NIPAMD_MFMA_ABLATE == 11
-        if (px == 12345.0)
+          if (px[i] == 12345.0)
 #endif
 #if NIPAMD_MFMA_NT
-        {
-          typedef double v2d __attribute__((ext_vector_type(2)));
-          __builtin_nontemporal_store(v2d{px * r, py * r}, reinterpret_cast<v2d*>(p));
-        }
+          {
+            typedef double v2d __attribute__((ext_vector_type(2)));
+            __builtin_nontemporal_store(v2d{px[i] * r[i], py[i] * r[i]}, reinterpret_cast<v2d*>(p));
+          }
 #else
-        *reinterpret_cast<double2*>(p) = make_double2(px * r, py * r);
+          *reinterpret_cast<double2*>(p) = make_double2(px[i] * r[i], py[i] * r[i]);
 #endif
+        }
       }
     } else {
 #pragma unroll
@@ -441,26 +552,59 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* o
     drainB(ci + 2, oc);
   }
 #else
-  if (nchB > 0) load_other(oa, 0);
-  for (int ci = 0; ci < nchB; ci += 2) {
-    if (ci + 1 < nchB) load_other(ob, ci + 1);
-    barrier_lds();
-    drainB(ci, oa);
-    if (ci + 1 >= nchB) break;
-    if (ci + 2 < nchB) load_other(oa, ci + 2);
-    barrier_lds();
-    drainB(ci + 1, ob);
+  // prefetches are unconditional (an over-run reloads the last chunk) so the
+  // loop body is straight-line code and the compiler's vmcnt waits stay exact
+  if constexpr (DMA) {
+    // The phase barrier drained every memory operation.  Before the first
+    // drain, chunk 1's sixteen DMAs follow chunk 0's (vmcnt 16); before every
+    // later drain, its DMAs are followed by the previous drain's sixteen
+    // posterior stores and the next chunk's sixteen DMAs (vmcnt 32).  The
+    // counter retires in order; anything extra issued in between only makes a
+    // wait stricter.
+    const int last = nchB > 0 ? nchB - 1 : 0;
+    dma_other(0, 0);
+    for (int ci = 0; ci < nchB; ci++) {
+      dma_other((ci + 1) & 1, ci + 1 < last ? ci + 1 : last);   // over-run reloads the last chunk
+      barrier_lds(&wb);
+      if (ci == 0) wait_vm<16>();
+      else wait_vm<32>();
+      read_other(oa, ci & 1);
+      drainB(ci, oa);
+    }
+    wait_vm<0>();                    // no DMA left in flight
+  } else {
+    // prefetches are unconditional (an over-run reloads the last chunk)
+    const int last = nchB > 0 ? nchB - 1 : 0;
+    load_other(oa, 0);
+    for (int ci = 0; ci < nchB; ci += 2) {
+      load_other(ob, ci + 1 < last ? ci + 1 : last);
+      barrier_lds(&wb);
+      drainB(ci, oa);
+      if (ci + 1 >= nchB) break;
+      load_other(oa, ci + 2 < last ? ci + 2 : last);
+      barrier_lds(&wb);
+      drainB(ci + 1, ob);
+    }
   }
 #endif
   if (FWD) ll.write(a, b0, lane);
+  if (NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 4;
+    st[blockIdx.x * 8 + 2 + (FWD ? 0 : 1)] = wa.cyc;
+    st[blockIdx.x * 8 + 6 + (FWD ? 0 : 1)] = wb.cyc;
+  }
 }
 
+constexpr int kOBD = 2 * 2 * kMSeq * 128;          // DMA buffers [2 partners][2][16 chains][1 KB] (64 KB)
+
+template <bool DMA>
 __global__ __launch_bounds__(kMThreads, 1)
 void chain_fb_mfma_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* out = reinterpret_cast<double*>(smem);                      // [2 dirs][2 slots][8][16][16]
   double* zr = out + kOutD;                                          // [2 slots][8][16]
-  double* Et = zr + kZD;                                             // [(M+2)][16]
+  double* obuf = zr + kZD;                                           // DMA ? [2][2][16][128] : none
+  double* Et = obuf + (DMA ? kOBD : 0);                              // [(M+2)][16]
   uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * 16);   // [16][Tr]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -513,8 +657,17 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   double* ring = out + (fwd ? 0 : 2 * kSlotD);
   double* Sblk = a.S + (size_t)blockIdx.x * block_scratch(T) + kMG * kSStep;   // t = 0
   if (wave >= 2) {
-    if (fwd) partner_wave<true>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
-    else partner_wave<false>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+    const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
+                      ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
+    double* ob = obuf + (fwd ? 0 : kOBD / 2);
+    if (pvec) {
+      if (fwd) partner_wave<true, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+      else partner_wave<false, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+    } else {
+      if (fwd) partner_wave<true, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+      else partner_wave<false, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+    }
     return;
   }
   const long b = b0 + j;
@@ -535,23 +688,33 @@ void chain_fb_mfma_kernel(ChainArgs a) {
 
 }  // namespace
 
-size_t chain_mfma_lds_bytes(int M, int T) {
+size_t chain_mfma_lds_bytes(int M, int T) {       // without the DMA buffers
   return (size_t)(kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * 16 * sizeof(double) +
          (size_t)kMSeq * chain_codes_row(T);
 }
 
-int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream) {
-  const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
-  const size_t lds = (chain_mfma_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
+namespace {
+template <bool DMA>
+int launch_mfma(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set = 0;
   if (lds > 65536 && lds > lds_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_fb_mfma_kernel),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return -1;
     lds_set = lds;
   }
-  hipLaunchKernelGGL(chain_fb_mfma_kernel, dim3(blocks), dim3(kMThreads), lds, stream, a);
+  const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
+  hipLaunchKernelGGL(chain_fb_mfma_kernel<DMA>, dim3(blocks), dim3(kMThreads), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace
+
+int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream) {
+  const size_t base = (chain_mfma_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
+  const size_t with_dma = base + (size_t)kOBD * sizeof(double);
+  if (NIPAMD_MFMA_DMA && NIPAMD_MFMA_PF == 1 && NIPAMD_MFMA_ABLATE != 12 && with_dma <= 160 * 1024)
+    return launch_mfma<true>(a, with_dma, stream);
+  return launch_mfma<false>(a, base, stream);
 }
 
 }  // namespace nipamd

@@ -484,14 +484,15 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
     unsigned long long* dst = nullptr;
     const int nblk = (int)((B + 15) / 16);
     if (mf && times) {
-      HIP_OK(hipMalloc(&dst, (size_t)nblk * 4 * sizeof(unsigned long long)));
+      HIP_OK(hipMalloc(&dst, (size_t)nblk * 12 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(dst, 0, (size_t)nblk * 12 * sizeof(unsigned long long), (hipStream_t)stream));
       a.counts = reinterpret_cast<double*>(dst);
     }
     const int rc = mf ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
                       : nipamd::chain_fb_launch(a, (hipStream_t)stream);
     a.counts = nullptr;
     if (dst) {
-      std::vector<unsigned long long> h((size_t)nblk * 4);
+      std::vector<unsigned long long> h((size_t)nblk * 12);
       HIP_OK(hipStreamSynchronize((hipStream_t)stream));
       HIP_OK(hipMemcpy(h.data(), dst, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
       (void)hipFree(dst);
@@ -503,6 +504,13 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
       }
       std::fprintf(stderr, "[nipamd] phase cycles (mean over %d blocks): A %.0f  barrier %.0f  B %.0f\n",
                    nblk, sa / nblk, sb / nblk, sc / nblk);
+      double w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < nblk; k++)
+        for (int i = 0; i < 8; i++) w[i] += (double)h[(size_t)nblk * 4 + k * 8 + i];
+      if (w[0] + w[4] > 0)
+        std::fprintf(stderr, "[nipamd] barrier wait cycles A/B: fwd filter %.0f/%.0f  bwd filter %.0f/%.0f  "
+                     "fwd partner %.0f/%.0f  bwd partner %.0f/%.0f\n", w[0] / nblk, w[4] / nblk, w[1] / nblk,
+                     w[5] / nblk, w[2] / nblk, w[6] / nblk, w[3] / nblk, w[7] / nblk);
     }
     if (rc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
