@@ -175,7 +175,9 @@ def main():
     value = units / elapsed
     bpu = algorithmic_bytes_per_seq_step(N, len(ov), args.workload != "estep")
     narrow = N <= 16 and len(ov) <= 1
-    if not narrow:
+    if not narrow and N <= 32 and os.environ.get("NIPAMD_FB_KERNEL") != "wide":
+        kname = "chain_mfma_wide_kernel<%d>" % (1 if N <= 16 else 2)
+    elif not narrow:
         kname = "chain_wide_kernel<%d>" % (16 if N <= 16 else 32 if N <= 32 else 64)
     elif os.environ.get("NIPAMD_FB_KERNEL") != "dpp":
         kname = "chain_fb_mfma_kernel"

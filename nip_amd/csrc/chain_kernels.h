@@ -79,6 +79,35 @@ __host__ __device__ inline long chain_scratch_row64(int T) { return (long)(T + 2
 size_t chain_wide_lds_bytes(int ncol, int T);
 int chain_wide_launch(const WideArgs& a, hipStream_t stream);
 
+// matrix-core interface chains (chain_mfma_wide.hip): N <= 16 * NT states (NT = 1, 2),
+// up to four observed children, 16 sequences per 4-wave block
+struct WideMfmaArgs {
+  const int* obs;        // int32 observations [B][T][n_obs]
+  long obs_bstride;
+  int obs_tstride;
+  int ncol;              // observed children (0: evidence = the unobserved row sums only)
+  int col[4];
+  int M[4];
+  int tab_off[4];        // doubles: column k's table [(M_k + 2)][16 NT] within tab
+  int tab_rows;          // total rows of tab (>= 2)
+  const double* tab;     // column 0 carries the unobserved children's row sums
+  long B;
+  int T, H, N;
+  const double* A;       // [64][64]
+  const double* pi;      // [64]
+  const double* w;       // [64] = A s_all (ll weights)
+  double* S;             // chain_mfma_wide_scratch_bytes
+  double* post;
+  long post_bstride;
+  int post_tstride;
+  int post_off;
+  double* ll;
+  unsigned* status;
+};
+size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T);
+size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T);
+int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, hipStream_t stream);
+
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block

@@ -1,0 +1,541 @@
+// chain_mfma_wide.hip -- matrix-core forward-backward for interface chains of
+// up to 32 states with up to four observed children (SURVEY 8(d) config 3:
+// demo1 @ 32 states, after the host folds D1 into the transition; and N <= 16
+// chains observed through several children).
+//
+// The recursion is the one in chain_kernels.hip / chain_mfma.hip (two-filter
+// smoothing, nip.c:1320-1581), with the evidence of step t the product of one
+// LDS table row per observed child (the unobserved children's row sums are
+// folded into the first table by the host):
+//   e_t[y] = prod_k T_k[code_k(t)][y]
+//
+// Layout: NT = N / 16 state tiles.  Sixteen chains of one direction share a
+// wave; the 16 x 16 tile (qo, qi) of the mat-vec is four v_mfma_f64_16x16x4
+// whose D registers are the next step's B operands (see chain_mfma.hip for the
+// register algebra).  Internal row g + 4r of tile q is state
+// 16q + state_of(g, r), so lane (g = l >> 4, j = l & 15) owns states
+// 16q + {2g, 2g+1, 8+2g, 9+2g} of chain j in every tile q.
+// Block = 16 sequences, four waves, one per SIMD (f64 MFMA and VALU do not
+// co-execute, so the filters keep only the recursion):
+//   wave 0 forward filter, wave 1 backward filter  (MFMA + evidence)
+//   wave 2 forward partner: scratch copy, ll, posteriors of t >= H
+//   wave 3 backward partner: scratch copy, posteriors of t < H
+// LDS rings hold two chunks of CH steps per direction (CH = 8 / NT, a slot is
+// 16 KB); one s_barrier per chunk hands a slot from filter to partner.
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cstdint>
+
+#include "chain_kernels.h"
+
+namespace nipamd {
+
+namespace {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+#ifndef NIPAMD_MW_ABLATE
+#define NIPAMD_MW_ABLATE 0     // timing-only builds: 1 partners only keep the barriers,
+#endif                         // 2 filters skip the mat-vec, 3 filters skip the evidence
+constexpr int kWSeq = 16;
+constexpr int kWThreads = 256;
+constexpr int kWG = kScratchGuard;
+
+__host__ __device__ constexpr int state_of(int g, int r) { return r < 2 ? 2 * g + r : 6 + 2 * g + r; }
+
+__device__ __forceinline__ double swap32_sum(double x) {     // x[l] + x[l ^ 32]
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+
+__device__ __forceinline__ double swap16_sum(double x) {     // x[l] + x[l ^ 16]
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// sums over aligned groups of L = 8 or 16 lanes, level by level over n
+// independent values; every level pairs equal partial sums (or adds a value
+// to its mirror), so all lanes of a group hold identical bits
+template <int L, int n>
+__device__ __forceinline__ void sumL_n(double (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += dpp64<0xB1>(x[i]);     // quad_perm [1,0,3,2]
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += dpp64<0x4E>(x[i]);     // quad_perm [2,3,0,1]
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += dpp64<0x141>(x[i]);    // row_half_mirror
+  if (L == 16) {
+#pragma unroll
+    for (int i = 0; i < n; i++) x[i] += dpp64<0x140>(x[i]);  // row_mirror
+  }
+}
+
+template <int n>
+__device__ __forceinline__ void recip_n(const double (&c)[n], double (&r)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = __builtin_amdgcn_rcp(c[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = __builtin_fma(r[i], __builtin_fma(-c[i], r[i], 1.0), r[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = __builtin_fma(r[i], __builtin_fma(-c[i], r[i], 1.0), r[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) r[i] = c[i] != 0.0 ? r[i] : 0.0;   // all-zero rows stay zero
+}
+
+__device__ __forceinline__ v4d ldexp4(v4d v, int k) {
+  v4d r;
+  r.x = __builtin_ldexp(v.x, k); r.y = __builtin_ldexp(v.y, k);
+  r.z = __builtin_ldexp(v.z, k); r.w = __builtin_ldexp(v.w, k);
+  return r;
+}
+
+__device__ __forceinline__ v4d load4(const double* p) {      // p = row + 16q + 2g
+  const v2d a = *reinterpret_cast<const v2d*>(p);
+  const v2d b = *reinterpret_cast<const v2d*>(p + 8);
+  return v4d{a.x, a.y, b.x, b.y};
+}
+
+__device__ __forceinline__ void barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int NT>
+struct Geo {
+  static constexpr int NP = 16 * NT;          // states per chain row
+  static constexpr int LPC = NP / 2;          // partner lanes per chain (2 states each)
+  static constexpr int CH = 64 / LPC;         // steps per chunk (= chains per partner pass)
+  static constexpr int QN = kWSeq / CH;       // partner passes over the 16 chains
+  static constexpr int kStep = kWSeq * NP;    // doubles per step of 16 chains
+  static constexpr int kSlot = CH * kStep;    // doubles per ring slot (16 KB)
+  // chain j's piece p (16 bytes) within a step, XOR-swizzled by j & 7
+  __device__ static int piece_off(int j, int p) { return j * NP + ((p ^ (j & 7)) << 1); }
+};
+
+__host__ __device__ inline long wblock_scratch(int NT, int T) { return (long)(T + 2 * kWG) * kWSeq * 16 * NT; }
+
+struct WCtx {
+  const double* tab;       // LDS tables
+  const uint8_t* codes;    // LDS codes [ncol][16][Tr] + chain j + kWG (t = 0)
+  int tab_off[4];          // per column: LDS offset of its table + 2g
+  int ncol, Tr;
+  double* out;             // this direction's ring [2][kSlot]
+  double* zr;              // forward: z2 ring [2][CH][16]
+  int wo[2][2];            // [tile][half] piece offsets of this lane
+  bool zw;
+};
+
+template <bool FWD, int NT>
+struct WChain {
+  using G = Geo<NT>;
+  double Aop[NT][NT][4];
+  v4d X[NT];
+  int sc = 0;
+
+  __device__ __forceinline__ void evidence(const WCtx& c, int t, v4d (&e)[NT]) const {
+    const int NP = G::NP;
+    int code = c.codes[t];
+#pragma unroll
+    for (int q = 0; q < NT; q++) e[q] = load4(c.tab + c.tab_off[0] + code * NP + 16 * q);
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+      if (k >= c.ncol) break;
+      code = c.codes[k * kWSeq * c.Tr + t];
+#pragma unroll
+      for (int q = 0; q < NT; q++) e[q] *= load4(c.tab + c.tab_off[k] + code * NP + 16 * q);
+    }
+  }
+
+  __device__ __forceinline__ void step(const WCtx& c, double* L, double* Z, const v4d (&e)[NT]) {
+    v4d d[NT];
+#pragma unroll
+    for (int qo = 0; qo < NT; qo++) d[qo] = v4d{0.0, 0.0, 0.0, 0.0};
+#if NIPAMD_MW_ABLATE == 2
+#pragma unroll
+    for (int qo = 0; qo < NT; qo++) d[qo] = X[qo] * 0.5;
+    if (0)
+#endif
+    // the NT output tiles' accumulation chains interleave
+#pragma unroll
+    for (int qi = 0; qi < NT; qi++) {
+      d[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0][qi][0], X[qi].x, d[0], 0, 0, 0);
+      if (NT > 1) d[NT - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[NT - 1][qi][0], X[qi].x, d[NT - 1], 0, 0, 0);
+      d[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0][qi][1], X[qi].y, d[0], 0, 0, 0);
+      if (NT > 1) d[NT - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[NT - 1][qi][1], X[qi].y, d[NT - 1], 0, 0, 0);
+      d[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0][qi][2], X[qi].z, d[0], 0, 0, 0);
+      if (NT > 1) d[NT - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[NT - 1][qi][2], X[qi].z, d[NT - 1], 0, 0, 0);
+      d[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0][qi][3], X[qi].w, d[0], 0, 0, 0);
+      if (NT > 1) d[NT - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[NT - 1][qi][3], X[qi].w, d[NT - 1], 0, 0, 0);
+    }
+    double part = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+      const v4d u = ldexp4(d[q], sc);
+      const v4d p = u * e[q];
+      const v4d keep = FWD ? p : u;
+      *reinterpret_cast<v2d*>(L + c.wo[q][0]) = v2d{keep.x, keep.y};
+      *reinterpret_cast<v2d*>(L + c.wo[q][1]) = v2d{keep.z, keep.w};
+      part += (p.x + p.y) + (p.z + p.w);
+      X[q] = p;
+    }
+    const double z2 = swap16_sum(swap32_sum(part));
+    if (FWD && c.zw) *Z = z2;
+    sc = -__builtin_amdgcn_frexp_exp(z2);
+  }
+
+  __device__ __forceinline__ void run(const WCtx& c, int n, int nch, int t0, int lane) {
+    constexpr int dir = FWD ? 1 : -1;
+    constexpr int CH = G::CH;
+    for (int ci = 0; ci < nch; ci++) {
+      double* slot = c.out + (ci & 1) * G::kSlot;
+      double* zs = FWD ? c.zr + (ci & 1) * CH * kWSeq + (lane & 15) : nullptr;
+      const int base = ci * CH;
+      v4d e[CH][NT];
+#pragma unroll
+      for (int k = 0; k < CH; k++) {
+#if NIPAMD_MW_ABLATE == 3
+#pragma unroll
+        for (int q = 0; q < NT; q++) e[k][q] = v4d{0.5, 0.5, 0.5, 0.5};
+#else
+        evidence(c, t0 + dir * (base + k), e[k]);   // guards cover over-run
+#endif
+      }
+      if (base + CH <= n) {
+#pragma unroll
+        for (int k = 0; k < CH; k++) step(c, slot + k * G::kStep, zs + k * kWSeq, e[k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < CH; k++)
+          if (base + k < n) step(c, slot + k * G::kStep, zs + k * kWSeq, e[k]);
+      }
+      barrier_lds();
+    }
+  }
+};
+
+template <bool FWD, int NT>
+__device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, double* Sblk, int lane,
+                                        int nchA, int nchB) {
+  using G = Geo<NT>;
+  const int j = lane & 15, g = lane >> 4;
+  const int T = a.T, H = a.H;
+  WChain<FWD, NT> ch;
+#pragma unroll
+  for (int qo = 0; qo < NT; qo++)
+#pragma unroll
+    for (int qi = 0; qi < NT; qi++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int out = 16 * qo + state_of(j & 3, j >> 2), in = 16 * qi + state_of(g, r);
+        ch.Aop[qo][qi][r] = FWD ? a.A[in * 64 + out] : a.A[out * 64 + in];
+      }
+  if (FWD) {
+#pragma unroll
+    for (int q = 0; q < NT; q++) ch.X[q] = load4(a.pi + 16 * q + 2 * g);
+  } else {
+    v4d e[NT];
+    ch.evidence(c, T - 1, e);
+    double part = 0.0;
+    double* row = Sblk + (long)(T - 1) * G::kStep + j * G::NP;   // beta_{T-1} (T-1 >= H)
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+      v4d beta;
+      beta.x = 16 * q + state_of(g, 0) < a.N ? 1.0 : 0.0; beta.y = 16 * q + state_of(g, 1) < a.N ? 1.0 : 0.0;
+      beta.z = 16 * q + state_of(g, 2) < a.N ? 1.0 : 0.0; beta.w = 16 * q + state_of(g, 3) < a.N ? 1.0 : 0.0;
+      *reinterpret_cast<v2d*>(row + 16 * q + 2 * g) = v2d{beta.x, beta.y};
+      *reinterpret_cast<v2d*>(row + 16 * q + 8 + 2 * g) = v2d{beta.z, beta.w};
+      ch.X[q] = e[q] * beta;
+      part += (ch.X[q].x + ch.X[q].y) + (ch.X[q].z + ch.X[q].w);
+    }
+    ch.sc = -__builtin_amdgcn_frexp_exp(swap16_sum(swap32_sum(part)));
+  }
+  if (FWD) ch.run(c, H, nchA, 0, lane);
+  else ch.run(c, T - 1 - H, nchA, T - 2, lane);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  if (FWD) ch.run(c, T - H, nchB, H, lane);
+  else ch.run(c, H, nchB, H - 1, lane);
+}
+
+// ll of the forward filter (nip.c:1461-1474), kept by the forward partner:
+// ll = sum_t log m2_t - log m1_t with m2_t = z2_t (published by the filter)
+// and m1_t = 2^sc_t * y_{t-1}, y_t = alpha_t . w, w = A s (s: the product of
+// every child's row sums), y_{-1} = prior . w.  Lane: chain q * CH + (L / LPC),
+// piece s = L % LPC.
+template <int NT>
+struct WLL {
+  using G = Geo<NT>;
+  double m2[G::QN], m1[G::QN], zmin[G::QN];
+  int e2[G::QN], e1[G::QN];
+  double w0, w1;
+
+  __device__ __forceinline__ void init(const WideMfmaArgs& a, int s) {
+    w0 = a.w[2 * s]; w1 = a.w[2 * s + 1];
+    double y[1] = {a.pi[2 * s] * w0 + a.pi[2 * s + 1] * w1};
+    sumL_n<G::LPC>(y);
+#pragma unroll
+    for (int q = 0; q < G::QN; q++) { m2[q] = 1.0; m1[q] = y[0]; zmin[q] = 1.0; e2[q] = 0; e1[q] = 0; }
+  }
+  __device__ __forceinline__ void step(int q, double y, double z2, bool last, bool renorm) {
+    zmin[q] = __builtin_fmin(zmin[q], z2);
+    m2[q] *= z2;
+    if (!last) { m1[q] *= y; e1[q] -= __builtin_amdgcn_frexp_exp(z2); }
+    if (renorm) {
+      const int k2 = __builtin_amdgcn_frexp_exp(m2[q]); m2[q] = __builtin_ldexp(m2[q], -k2); e2[q] += k2;
+      const int k1 = __builtin_amdgcn_frexp_exp(m1[q]); m1[q] = __builtin_ldexp(m1[q], -k1); e1[q] += k1;
+    }
+  }
+  __device__ __forceinline__ void write(const WideMfmaArgs& a, long b0, int lane) {
+    if (lane % G::LPC != 0) return;
+#pragma unroll
+    for (int q = 0; q < G::QN; q++) {
+      const long b = b0 + q * G::CH + lane / G::LPC;
+      if (b >= a.B) continue;
+      double ll = log(m2[q]) - log(m1[q]) + (double)(e2[q] - e1[q]) * 0.69314718055994530942;
+      const bool dead = zmin[q] == 0.0;
+      if (dead) ll = -DBL_MAX;
+      if (a.ll) a.ll[b] = ll;
+      if (a.status) a.status[b] = dead ? 1u : 0u;
+    }
+  }
+};
+
+// Partner wave of one direction.  Phase A: the slot's steps to the block's
+// scratch S[t][16 chains][NP] (coalesced, 1 KB per store instruction).  Phase
+// B: lane (hi = L / LPC, s = L % LPC) takes step hi of the chunk in address
+// order and states 2s, 2s+1 of every chain: ring value times the other
+// direction's vector (scratch, one chunk prefetched), normalised over the
+// chain's LPC lanes; with N == NP and dense rows, one contiguous 1 KB
+// posterior run per store instruction.
+template <bool FWD, bool PVEC, int NT>
+__device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* out, const double* zr,
+                                         double* Sblk, int lane, long b0, int nchA, int nchB) {
+  using G = Geo<NT>;
+  constexpr int NP = G::NP, LPC = G::LPC, CH = G::CH, QN = G::QN;
+  const int T = a.T, H = a.H;
+  const int s = lane % LPC, hi = lane / LPC;
+  const int nA = FWD ? H : T - 1 - H, nB = FWD ? T - H : H;
+  const int tA = FWD ? 0 : T - 2, tB = FWD ? H : H - 1;
+  constexpr int dir = FWD ? 1 : -1;
+  const int kB = FWD ? hi : CH - 1 - hi;
+  auto tlow = [&](int ci) { return FWD ? tB + ci * CH : tB - ci * CH - (CH - 1); };
+
+  WLL<NT> ll;
+  if (FWD) ll.init(a, s);
+  auto ll_chunk = [&](int ci, int n, int t0) {
+    const double* slot = out + (ci & 1) * G::kSlot;
+    const double* zs = zr + (ci & 1) * CH * kWSeq;
+    const bool full = ci * CH + CH <= n;
+    double y[CH * QN];
+#pragma unroll
+    for (int k = 0; k < CH; k++)
+#pragma unroll
+      for (int q = 0; q < QN; q++) {
+        const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(q * CH + hi, s));
+        y[k * QN + q] = v.x * ll.w0 + v.y * ll.w1;
+      }
+    sumL_n<LPC>(y);
+#pragma unroll
+    for (int k = 0; k < CH; k++) {
+      const int i = ci * CH + k;
+      if (i >= n) break;
+      const bool last = t0 + i == T - 1;
+#pragma unroll
+      for (int q = 0; q < QN; q++)
+        ll.step(q, y[k * QN + q], zs[k * kWSeq + q * CH + hi], last, !full || (k & 3) == 3);
+    }
+  };
+  // phase A copy: 16 * LPC pieces per step, 64 per store instruction
+  auto drainA = [&](int ci) {
+    if (NIPAMD_MW_ABLATE == 1) return;
+    const double* slot = out + (ci & 1) * G::kSlot;
+    if (FWD) ll_chunk(ci, nA, tA);
+#pragma unroll
+    for (int k = 0; k < CH; k++) {
+      const int i = ci * CH + k;
+      if (i >= nA) break;
+      const int t = tA + dir * i;
+#pragma unroll
+      for (int u0 = 0; u0 < kWSeq * LPC; u0 += 64) {
+        const int u = u0 + lane, jj = u / LPC, p = u % LPC;
+        const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(jj, p));
+        *reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u) = v;
+      }
+    }
+  };
+  for (int ci = 0; ci < nchA; ci++) {
+    if (ci > 0) drainA(ci - 1);
+    barrier_lds();
+  }
+  if (nchA > 0) drainA(nchA - 1);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+
+  v2d oa[kWSeq], ob[kWSeq];
+  auto load_other = [&](v2d (&o)[kWSeq], int ci) {
+    if (NIPAMD_MW_ABLATE == 1) return;
+    const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
+#pragma unroll
+    for (int c = 0; c < kWSeq; c++) o[c] = *reinterpret_cast<const v2d*>(q + c * NP);
+  };
+  double* const sink = a.S + (size_t)((a.B + kWSeq - 1) / kWSeq) * wblock_scratch(NT, T) + 2 * s;
+  const bool st0 = 2 * s < a.N, st1 = 2 * s + 1 < a.N;
+  auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {
+    if (NIPAMD_MW_ABLATE == 1) return;
+    if (FWD) ll_chunk(ci, nB, tB);
+    if (!PVEC && !a.post) return;
+    const double* slot = out + (ci & 1) * G::kSlot;
+    const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
+    const bool ok = kB < nk;
+    const int t = tlow(ci) + hi;
+#pragma unroll
+    for (int q0 = 0; q0 < kWSeq; q0 += 8) {
+      double px[8], py[8], z[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const v2d v = *reinterpret_cast<const v2d*>(slot + kB * G::kStep + G::piece_off(q0 + i, s));
+        px[i] = v.x * o[q0 + i].x; py[i] = v.y * o[q0 + i].y;
+        z[i] = px[i] + py[i];
+      }
+      sumL_n<LPC>(z);
+      recip_n(z, r);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const long bb = b0 + q0 + i;
+        if constexpr (PVEC) {
+          double* p = (ok && bb < a.B) ? a.post + (size_t)bb * a.post_bstride + (long)t * NP + a.post_off + 2 * s
+                                       : sink;
+          *reinterpret_cast<v2d*>(p) = v2d{px[i] * r[i], py[i] * r[i]};
+        } else {
+          if (ok && bb < a.B) {
+            double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
+            if (st0) p[0] = px[i] * r[i];
+            if (st1) p[1] = py[i] * r[i];
+          }
+        }
+      }
+    }
+  };
+  const int last = nchB > 0 ? nchB - 1 : 0;
+  load_other(oa, 0);
+  for (int ci = 0; ci < nchB; ci += 2) {
+    load_other(ob, ci + 1 < last ? ci + 1 : last);
+    barrier_lds();
+    drainB(ci, oa);
+    if (ci + 1 >= nchB) break;
+    load_other(oa, ci + 2 < last ? ci + 2 : last);
+    barrier_lds();
+    drainB(ci + 1, ob);
+  }
+  if (FWD) ll.write(a, b0, lane);
+}
+
+template <int NT>
+__global__ __launch_bounds__(kWThreads, 1)
+void chain_mfma_wide_kernel(WideMfmaArgs a) {
+  using G = Geo<NT>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* out = reinterpret_cast<double*>(smem);            // [2 dirs][2 slots][kSlot]
+  double* zr = out + 4 * G::kSlot;                          // [2 slots][CH][16]
+  double* tab = zr + 2 * G::CH * kWSeq;                     // [sum (M_k + 2)][NP]
+  const int ncol = a.ncol > 0 ? a.ncol : 1;
+  uint8_t* codes = reinterpret_cast<uint8_t*>(tab + a.tab_rows * G::NP);   // [ncol][16][Tr]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const long b0 = (long)blockIdx.x * kWSeq;
+  const int T = a.T, Tr = chain_codes_row(T);
+
+  for (int i = tid; i < a.tab_rows * G::NP; i += kWThreads) tab[i] = a.tab[i];
+  const int nseq = (int)((a.B - b0) < kWSeq ? (a.B - b0) : kWSeq);
+  for (int k = 0; k < ncol; k++) {
+    const int M = a.ncol > 0 ? a.M[k] : 0;
+    uint8_t* ck = codes + (size_t)k * kWSeq * Tr;
+    for (int i = tid; i < kWSeq * Tr; i += kWThreads) {
+      const int cq = i / Tr, t = i - cq * Tr - kWG;
+      int c = M;                                            // missing / guard / absent sequence
+      if (a.ncol > 0 && cq < nseq && t >= 0 && t < T) {
+        const int o = a.obs[(b0 + cq) * a.obs_bstride + (long)t * a.obs_tstride + a.col[k]];
+        c = o < 0 ? M : (o < M ? o : M + 1);
+      }
+      ck[i] = (uint8_t)c;
+    }
+  }
+  __syncthreads();
+
+  const int H = a.H;
+  const int nA = (H > T - 1 - H ? H : T - 1 - H), nB = (T - H > H ? T - H : H);
+  const int nchA = (nA + G::CH - 1) / G::CH, nchB = (nB + G::CH - 1) / G::CH;
+  const bool fwd = (wave & 1) == 0;
+  double* ring = out + (fwd ? 0 : 2 * G::kSlot);
+  double* Sblk = a.S + (size_t)blockIdx.x * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;   // t = 0
+  if (wave >= 2) {
+    const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
+                      (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
+    if (pvec) {
+      if (fwd) wpartner<true, true, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, true, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+    } else {
+      if (fwd) wpartner<true, false, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, false, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+    }
+    return;
+  }
+  WCtx c;
+  c.tab = tab;
+  c.codes = codes + j * Tr + kWG;
+  c.ncol = ncol;
+  c.Tr = Tr;
+#pragma unroll
+  for (int k = 0; k < 4; k++) c.tab_off[k] = (k < ncol ? a.tab_off[k] : 0) + 2 * g;
+  c.out = ring;
+  c.zr = zr;
+  c.zw = g == 0;
+#pragma unroll
+  for (int q = 0; q < NT; q++) {
+    c.wo[q][0] = Geo<NT>::piece_off(j, 8 * q + g);
+    c.wo[q][1] = Geo<NT>::piece_off(j, 8 * q + 4 + g);
+  }
+  if (fwd) wfilter<true, NT>(a, c, Sblk, lane, nchA, nchB);
+  else wfilter<false, NT>(a, c, Sblk, lane, nchA, nchB);
+}
+
+}  // namespace
+
+size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T) {
+  const size_t slot = 2048;                                  // doubles per ring slot
+  const size_t ch = 8 / NT;
+  return (4 * slot + 2 * ch * kWSeq + (size_t)tab_rows * 16 * NT) * sizeof(double) +
+         (size_t)(ncol > 0 ? ncol : 1) * kWSeq * chain_codes_row(T);
+}
+
+size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
+  return (size_t)((B + kWSeq - 1) / kWSeq + 1) * wblock_scratch(NT, T) * sizeof(double);
+}
+
+int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, hipStream_t stream) {
+  const size_t lds = (chain_mfma_wide_lds_bytes(NT, a.tab_rows, a.ncol, a.T) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024) return -1;
+  const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
+  const void* fn = NT == 1 ? reinterpret_cast<const void*>(&chain_mfma_wide_kernel<1>)
+                           : reinterpret_cast<const void*>(&chain_mfma_wide_kernel<2>);
+  static size_t set[3] = {0, 0, 0};
+  if (lds > 65536 && lds > set[NT]) {
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
+    set[NT] = lds;
+  }
+  if (NT == 1) hipLaunchKernelGGL(chain_mfma_wide_kernel<1>, dim3(blocks), dim3(kWThreads), lds, stream, a);
+  else hipLaunchKernelGGL(chain_mfma_wide_kernel<2>, dim3(blocks), dim3(kWThreads), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace nipamd

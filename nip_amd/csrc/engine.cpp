@@ -51,6 +51,12 @@ struct ReqTables {
   double* tabw = nullptr;         // wide kernel: per column [(M_k+2)][64], concatenated
   std::vector<size_t> tabw_off;
   double* ebase = nullptr;        // [64] product of the unobserved children's row sums
+  // matrix-core wide kernel: per column [(M_k+2)][NP], column 0 times ebase
+  // (a single [2][NP] pseudo column = ebase when nothing is observed)
+  double* mtab = nullptr;
+  int mtab_rows = 0;
+  int mtab_off[4] = {0, 0, 0, 0};
+  double* wv = nullptr;           // [64] A s_all
 };
 
 struct DevState {
@@ -80,6 +86,7 @@ void free_tables(DevState* d) {
   d->A = d->pi = d->A64 = d->pi64 = d->sall64 = nullptr;
   for (auto& r : d->reqs) {
     (void)hipFree(r.Etab16); (void)hipFree(r.ts16); (void)hipFree(r.tabw); (void)hipFree(r.ebase);
+    (void)hipFree(r.mtab); (void)hipFree(r.wv);
   }
   d->reqs.clear();
 }
@@ -188,6 +195,36 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
   }
   if (int rc = upload(&t.tabw, W)) return rc;
   if (int rc = upload(&t.ebase, eb)) return rc;
+  if (N <= 32) {
+    const int NP = N <= 16 ? 16 : 32;
+    std::vector<double> MT;
+    const int nc = r.ncol > 0 ? r.ncol : 1;
+    for (int i = 0; i < nc; i++) {
+      const int M = r.ncol > 0 ? P.emits[r.emit[i]].M : 0;
+      t.mtab_off[i] = (int)MT.size();
+      const size_t base = MT.size();
+      MT.resize(base + (size_t)(M + 2) * NP, 0.0);
+      for (int y = 0; y < N; y++) {
+        const double f = i == 0 ? eb[y] : 1.0;
+        if (r.ncol > 0) {
+          const auto& em = P.emits[r.emit[i]];
+          for (int m = 0; m < M; m++) MT[base + (size_t)m * NP + y] = em.E[(size_t)m * 64 + y] * f;
+          MT[base + (size_t)M * NP + y] = em.s[y] * f;
+        } else {
+          MT[base + y] = f;
+        }
+      }
+    }
+    t.mtab_rows = (int)(MT.size() / NP);
+    std::vector<double> wv(64, 0.0);
+    for (int x = 0; x < N; x++) {
+      double acc = 0.0;
+      for (int y = 0; y < N; y++) acc += P.A64[(size_t)x * 64 + y] * P.s_all64[y];
+      wv[x] = acc;
+    }
+    if (int rc = upload(&t.mtab, MT)) return rc;
+    if (int rc = upload(&t.wv, wv)) return rc;
+  }
   d->reqs.push_back(std::move(t));
   *out = &d->reqs.back();
   return 0;
@@ -425,6 +462,39 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   int stride = 0;
   for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
   const long ocols = n_obs > 0 ? n_obs : 1;
+  static const bool force_wide = [] {
+    const char* e = std::getenv("NIPAMD_FB_KERNEL");
+    return e && std::string(e) == "wide";
+  }();
+  if (!r.narrow && P.N <= 32 && !force_wide) {
+    // matrix-core interface chain: N <= 32, up to four observed children
+    const int NT = P.N <= 16 ? 1 : 2;
+    if (nipamd::chain_mfma_wide_lds_bytes(NT, rt->mtab_rows, r.ncol, T) > 160 * 1024)
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
+    if (int rc = ensure_scratch(mm, nipamd::chain_mfma_wide_scratch_bytes(NT, B, T))) return rc;
+    nipamd::WideMfmaArgs w{};
+    w.obs = d_obs; w.obs_bstride = (long)T * ocols; w.obs_tstride = (int)ocols;
+    w.ncol = r.ncol;
+    for (int i = 0; i < 4; i++) {
+      w.col[i] = i < r.ncol ? r.col[i] : 0;
+      w.M[i] = i < r.ncol ? P.emits[r.emit[i]].M : 0;
+      w.tab_off[i] = rt->mtab_off[i];
+    }
+    w.tab_rows = rt->mtab_rows; w.tab = rt->mtab;
+    w.B = B; w.T = T; w.H = T / 2; w.N = P.N;
+    w.A = d->A64; w.pi = d->pi64; w.w = rt->wv; w.S = d->S;
+    w.post = n_query > 0 ? d_post : nullptr;
+    w.post_bstride = (long)T * stride; w.post_tstride = stride;
+    w.ll = d_ll; w.status = d_status;
+    const int nq = n_query > 0 ? n_query : 1;
+    for (int q = 0; q < nq; q++) {
+      w.post_off = q * P.N;
+      if (q > 0) { w.ll = nullptr; w.status = nullptr; }
+      if (nipamd::chain_mfma_wide_launch(w, NT, (hipStream_t)stream))
+        return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    }
+    return 0;
+  }
   if (!r.narrow) {
     // wide interface chain: N <= 64, up to four observed children
     if (nipamd::chain_wide_lds_bytes(r.ncol, T) > 64 * 1024)
