@@ -149,6 +149,21 @@ int nipamd_fb_host(nipamd_model* m, const int32_t* obs, int n_obs,
                    uint32_t* status);
 
 /*
+ * Batched forward_inference() (src/nip.c:1103-1315): filtered marginals
+ * P(X_t | y_0..y_t) of the query variables, same buffers and conventions as
+ * nipamd_fb (d_ll = the same sum over t; the filter pass alone yields it).
+ * Replaces forward_inference(ts, vars, nvars, &ll) (nip.h:382-383) batched.
+ */
+int nipamd_filter(nipamd_model* m, const int32_t* d_obs, int n_obs,
+                  const int* obs_vars, int B, int T, int n_query,
+                  const int* query, double* d_post, double* d_ll,
+                  uint32_t* d_status, void* stream);
+int nipamd_filter_host(nipamd_model* m, const int32_t* obs, int n_obs,
+                       const int* obs_vars, int B, int T, int n_query,
+                       const int* query, double* post, double* ll,
+                       uint32_t* status);
+
+/*
  * Batched e_step() (src/nip.c:1708-2007): expected counts of B sequences
  * summed into d_counts (double [param_size], em_learn layout, caller
  * initialised -- em_learn starts from 1.0, nip.c:2172).  Summation over the

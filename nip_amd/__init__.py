@@ -46,7 +46,7 @@ EXPORTS = [
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
-    "nipamd_estep_finalize", "nipamd_estep_host",
+    "nipamd_estep_finalize", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
 ]
 
 
@@ -83,6 +83,8 @@ def lib():
                                 vp, vp, vp, vp]
         L.nipamd_fb_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, ip,
                                      vp, vp, vp]
+        L.nipamd_filter.argtypes = L.nipamd_fb.argtypes
+        L.nipamd_filter_host.argtypes = L.nipamd_fb_host.argtypes
         L.nipamd_estep.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_partial_size.argtypes = [vp]
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
@@ -229,15 +231,7 @@ def _stream_ptr(stream):
     return C.c_void_p(stream.cuda_stream)
 
 
-def forward_backward_inference(model: Model, obs, obs_vars, query, post=None, ll=None,
-                               status=None, stream=None):
-    """Batched forward_backward_inference() (src/nip.c:1320) on the GPU.
-
-    obs: torch int32 CUDA tensor [B, T, n_obs] (state index, <0 missing).
-    Returns (post [B, T, sum card(query)] float64, ll [B] float64, status [B] int32),
-    all CUDA tensors, computed asynchronously on ``stream`` (default: torch's
-    current stream).  ll is the SUM over t, as the reference returns it.
-    """
+def _run_device(fn, model, obs, obs_vars, query, post, ll, status, stream):
     import torch
     if obs.dim() == 2:
         obs = obs.unsqueeze(-1)
@@ -252,15 +246,13 @@ def forward_backward_inference(model: Model, obs, obs_vars, query, post=None, ll
         ll = torch.empty((B,), dtype=torch.float64, device=dev)
     if status is None:
         status = torch.empty((B,), dtype=torch.int32, device=dev)
-    _check(lib().nipamd_fb(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
-                           len(query), _ints(query), C.c_void_p(post.data_ptr()),
-                           C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()),
-                           _stream_ptr(stream)))
+    _check(fn(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
+              len(query), _ints(query), C.c_void_p(post.data_ptr()),
+              C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
     return post, ll, status
 
 
-def forward_backward_inference_host(model: Model, obs, obs_vars, query):
-    """Same, from host numpy buffers (PCIe-inclusive, synchronous)."""
+def _run_host(fn, model, obs, obs_vars, query):
     obs = np.ascontiguousarray(np.asarray(obs, np.int32))
     if obs.ndim == 2:
         obs = obs[:, :, None]
@@ -269,10 +261,40 @@ def forward_backward_inference_host(model: Model, obs, obs_vars, query):
     post = np.zeros((B, T, width))
     ll = np.zeros(B)
     status = np.zeros(B, np.uint32)
-    _check(lib().nipamd_fb_host(model._h, obs.ctypes.data_as(C.c_void_p), nobs, _ints(obs_vars),
-                                B, T, len(query), _ints(query), post.ctypes.data_as(C.c_void_p),
-                                ll.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
+    _check(fn(model._h, obs.ctypes.data_as(C.c_void_p), nobs, _ints(obs_vars),
+              B, T, len(query), _ints(query), post.ctypes.data_as(C.c_void_p),
+              ll.ctypes.data_as(C.c_void_p), status.ctypes.data_as(C.c_void_p)))
     return post, ll, status
+
+
+def forward_backward_inference(model: Model, obs, obs_vars, query, post=None, ll=None,
+                               status=None, stream=None):
+    """Batched forward_backward_inference() (src/nip.c:1320) on the GPU.
+
+    obs: torch int32 CUDA tensor [B, T, n_obs] (state index, <0 missing).
+    Returns (post [B, T, sum card(query)] float64, ll [B] float64, status [B] int32),
+    all CUDA tensors, computed asynchronously on ``stream`` (default: torch's
+    current stream).  ll is the SUM over t, as the reference returns it.
+    """
+    return _run_device(lib().nipamd_fb, model, obs, obs_vars, query, post, ll, status, stream)
+
+
+def forward_inference(model: Model, obs, obs_vars, query, post=None, ll=None, status=None,
+                      stream=None):
+    """Batched forward_inference() (src/nip.c:1103-1315) on the GPU: filtered
+    marginals P(X_t | y_0..y_t) of the query variables, and the same ll (sum
+    over t).  Buffers and conventions as forward_backward_inference."""
+    return _run_device(lib().nipamd_filter, model, obs, obs_vars, query, post, ll, status, stream)
+
+
+def forward_backward_inference_host(model: Model, obs, obs_vars, query):
+    """Same, from host numpy buffers (PCIe-inclusive, synchronous)."""
+    return _run_host(lib().nipamd_fb_host, model, obs, obs_vars, query)
+
+
+def forward_inference_host(model: Model, obs, obs_vars, query):
+    """forward_inference from host numpy buffers (PCIe-inclusive, synchronous)."""
+    return _run_host(lib().nipamd_filter_host, model, obs, obs_vars, query)
 
 
 def _obs3(obs, obs_vars):

@@ -74,6 +74,7 @@ struct WideArgs {
   int post_off;
   double* ll;
   unsigned* status;
+  int filter;            // forward_inference: H = 0, filtered posteriors, no scratch reads
 };
 __host__ __device__ inline long chain_scratch_row64(int T) { return (long)(T + 2 * kScratchGuard) * 64; }
 size_t chain_wide_lds_bytes(int ncol, int T);
@@ -106,7 +107,9 @@ struct WideMfmaArgs {
 };
 size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T);
 size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T);
-int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, hipStream_t stream);
+// filter_only: forward_inference (filtered posteriors + ll), requires H == T, no scratch
+// beyond one sink row (S needs >= 64 doubles)
+int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, bool filter_only, hipStream_t stream);
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);

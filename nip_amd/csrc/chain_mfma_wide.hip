@@ -317,7 +317,7 @@ struct WLL {
 // direction's vector (scratch, one chunk prefetched), normalised over the
 // chain's LPC lanes; with N == NP and dense rows, one contiguous 1 KB
 // posterior run per store instruction.
-template <bool FWD, bool PVEC, int NT>
+template <bool FWD, bool PVEC, int NT, bool FILT>
 __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* out, const double* zr,
                                          double* Sblk, int lane, long b0, int nchA, int nchB) {
   using G = Geo<NT>;
@@ -355,55 +355,17 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
         ll.step(q, y[k * QN + q], zs[k * kWSeq + q * CH + hi], last, !full || (k & 3) == 3);
     }
   };
-  // phase A copy: 16 * LPC pieces per step, 64 per store instruction
-  auto drainA = [&](int ci) {
-    if (NIPAMD_MW_ABLATE == 1) return;
-    const double* slot = out + (ci & 1) * G::kSlot;
-    if (FWD) ll_chunk(ci, nA, tA);
-#pragma unroll
-    for (int k = 0; k < CH; k++) {
-      const int i = ci * CH + k;
-      if (i >= nA) break;
-      const int t = tA + dir * i;
-#pragma unroll
-      for (int u0 = 0; u0 < kWSeq * LPC; u0 += 64) {
-        const int u = u0 + lane, jj = u / LPC, p = u % LPC;
-        const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(jj, p));
-        *reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u) = v;
-      }
-    }
-  };
-  for (int ci = 0; ci < nchA; ci++) {
-    if (ci > 0) drainA(ci - 1);
-    barrier_lds();
-  }
-  if (nchA > 0) drainA(nchA - 1);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-
-  v2d oa[kWSeq], ob[kWSeq];
-  auto load_other = [&](v2d (&o)[kWSeq], int ci) {
-    if (NIPAMD_MW_ABLATE == 1) return;
-    const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
-#pragma unroll
-    for (int c = 0; c < kWSeq; c++) o[c] = *reinterpret_cast<const v2d*>(q + c * NP);
-  };
-  double* const sink = a.S + (size_t)((a.B + kWSeq - 1) / kWSeq) * wblock_scratch(NT, T) + 2 * s;
+  double* const sink = FILT ? a.S + 2 * s
+                            : a.S + (size_t)((a.B + kWSeq - 1) / kWSeq) * wblock_scratch(NT, T) + 2 * s;
   const bool st0 = 2 * s < a.N, st1 = 2 * s + 1 < a.N;
-  auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {
-    if (NIPAMD_MW_ABLATE == 1) return;
-    if (FWD) ll_chunk(ci, nB, tB);
-    if (!PVEC && !a.post) return;
-    const double* slot = out + (ci & 1) * G::kSlot;
-    const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
-    const bool ok = kB < nk;
-    const int t = tlow(ci) + hi;
+  // normalised posteriors of ring step kk (time t) times o, for the 16 chains
+  auto emit = [&](const double* slot, int kk, int t, bool ok, const v2d (&o)[kWSeq]) {
 #pragma unroll
     for (int q0 = 0; q0 < kWSeq; q0 += 8) {
       double px[8], py[8], z[8], r[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        const v2d v = *reinterpret_cast<const v2d*>(slot + kB * G::kStep + G::piece_off(q0 + i, s));
+        const v2d v = *reinterpret_cast<const v2d*>(slot + kk * G::kStep + G::piece_off(q0 + i, s));
         px[i] = v.x * o[q0 + i].x; py[i] = v.y * o[q0 + i].y;
         z[i] = px[i] + py[i];
       }
@@ -426,6 +388,60 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
       }
     }
   };
+  // phase A copy: 16 * LPC pieces per step, 64 per store instruction
+  // (filtering: the normalised alpha_t are the posteriors, nip.c:1103-1315)
+  auto drainA = [&](int ci) {
+    if (NIPAMD_MW_ABLATE == 1) return;
+    const double* slot = out + (ci & 1) * G::kSlot;
+    if (FWD) ll_chunk(ci, nA, tA);
+    if constexpr (FILT) {
+      if (!PVEC && !a.post) return;
+      v2d ones[kWSeq];
+#pragma unroll
+      for (int q = 0; q < kWSeq; q++) ones[q] = v2d{1.0, 1.0};
+      emit(slot, hi, ci * CH + hi, ci * CH + hi < nA, ones);
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < CH; k++) {
+      const int i = ci * CH + k;
+      if (i >= nA) break;
+      const int t = tA + dir * i;
+#pragma unroll
+      for (int u0 = 0; u0 < kWSeq * LPC; u0 += 64) {
+        const int u = u0 + lane, jj = u / LPC, p = u % LPC;
+        const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(jj, p));
+        *reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u) = v;
+      }
+    }
+  };
+  for (int ci = 0; ci < nchA; ci++) {
+    if (ci > 0) drainA(ci - 1);
+    barrier_lds();
+  }
+  if (nchA > 0) drainA(nchA - 1);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+
+  if constexpr (FILT) {
+    if (FWD) ll.write(a, b0, lane);
+    return;
+  }
+  v2d oa[kWSeq], ob[kWSeq];
+  auto load_other = [&](v2d (&o)[kWSeq], int ci) {
+    if (NIPAMD_MW_ABLATE == 1) return;
+    const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
+#pragma unroll
+    for (int c = 0; c < kWSeq; c++) o[c] = *reinterpret_cast<const v2d*>(q + c * NP);
+  };
+  auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {
+    if (NIPAMD_MW_ABLATE == 1) return;
+    if (FWD) ll_chunk(ci, nB, tB);
+    if (!PVEC && !a.post) return;
+    const double* slot = out + (ci & 1) * G::kSlot;
+    const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
+    emit(slot, kB, tlow(ci) + hi, kB < nk, o);
+  };
   const int last = nchB > 0 ? nchB - 1 : 0;
   load_other(oa, 0);
   for (int ci = 0; ci < nchB; ci += 2) {
@@ -440,9 +456,11 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   if (FWD) ll.write(a, b0, lane);
 }
 
-template <int NT>
-__global__ __launch_bounds__(kWThreads, 1)
+// FILT: forward_inference (filtering only): waves 0 (filter) and 1 (partner), H = T
+template <int NT, bool FILT>
+__global__ __launch_bounds__(FILT ? kWThreads / 2 : kWThreads, 1)
 void chain_mfma_wide_kernel(WideMfmaArgs a) {
+  constexpr int kThreads = FILT ? kWThreads / 2 : kWThreads;
   using G = Geo<NT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* out = reinterpret_cast<double*>(smem);            // [2 dirs][2 slots][kSlot]
@@ -455,12 +473,12 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   const long b0 = (long)blockIdx.x * kWSeq;
   const int T = a.T, Tr = chain_codes_row(T);
 
-  for (int i = tid; i < a.tab_rows * G::NP; i += kWThreads) tab[i] = a.tab[i];
+  for (int i = tid; i < a.tab_rows * G::NP; i += kThreads) tab[i] = a.tab[i];
   const int nseq = (int)((a.B - b0) < kWSeq ? (a.B - b0) : kWSeq);
   for (int k = 0; k < ncol; k++) {
     const int M = a.ncol > 0 ? a.M[k] : 0;
     uint8_t* ck = codes + (size_t)k * kWSeq * Tr;
-    for (int i = tid; i < kWSeq * Tr; i += kWThreads) {
+    for (int i = tid; i < kWSeq * Tr; i += kThreads) {
       const int cq = i / Tr, t = i - cq * Tr - kWG;
       int c = M;                                            // missing / guard / absent sequence
       if (a.ncol > 0 && cq < nseq && t >= 0 && t < T) {
@@ -474,19 +492,19 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
 
   const int H = a.H;
   const int nA = (H > T - 1 - H ? H : T - 1 - H), nB = (T - H > H ? T - H : H);
-  const int nchA = (nA + G::CH - 1) / G::CH, nchB = (nB + G::CH - 1) / G::CH;
-  const bool fwd = (wave & 1) == 0;
+  const int nchA = (nA + G::CH - 1) / G::CH, nchB = FILT ? 0 : (nB + G::CH - 1) / G::CH;
+  const bool fwd = FILT || (wave & 1) == 0;
   double* ring = out + (fwd ? 0 : 2 * G::kSlot);
-  double* Sblk = a.S + (size_t)blockIdx.x * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;   // t = 0
-  if (wave >= 2) {
+  double* Sblk = FILT ? nullptr : a.S + (size_t)blockIdx.x * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;
+  if (FILT ? wave == 1 : wave >= 2) {
     const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
                       (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
     if (pvec) {
-      if (fwd) wpartner<true, true, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
-      else wpartner<false, true, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, true, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, true, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
     } else {
-      if (fwd) wpartner<true, false, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
-      else wpartner<false, false, NT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, false, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, false, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
     }
     return;
   }
@@ -506,7 +524,7 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
     c.wo[q][1] = Geo<NT>::piece_off(j, 8 * q + 4 + g);
   }
   if (fwd) wfilter<true, NT>(a, c, Sblk, lane, nchA, nchB);
-  else wfilter<false, NT>(a, c, Sblk, lane, nchA, nchB);
+  else if (!FILT) wfilter<false, NT>(a, c, Sblk, lane, nchA, nchB);
 }
 
 }  // namespace
@@ -522,20 +540,28 @@ size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
   return (size_t)((B + kWSeq - 1) / kWSeq + 1) * wblock_scratch(NT, T) * sizeof(double);
 }
 
-int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, hipStream_t stream) {
-  const size_t lds = (chain_mfma_wide_lds_bytes(NT, a.tab_rows, a.ncol, a.T) + 15) & ~(size_t)15;
-  if (lds > 160 * 1024) return -1;
-  const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
-  const void* fn = NT == 1 ? reinterpret_cast<const void*>(&chain_mfma_wide_kernel<1>)
-                           : reinterpret_cast<const void*>(&chain_mfma_wide_kernel<2>);
-  static size_t set[3] = {0, 0, 0};
-  if (lds > 65536 && lds > set[NT]) {
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
-    set[NT] = lds;
+namespace {
+template <int NT, bool FILT>
+int launch_wide(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
+  static size_t set = 0;
+  if (lds > 65536 && lds > set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return -1;
+    set = lds;
   }
-  if (NT == 1) hipLaunchKernelGGL(chain_mfma_wide_kernel<1>, dim3(blocks), dim3(kWThreads), lds, stream, a);
-  else hipLaunchKernelGGL(chain_mfma_wide_kernel<2>, dim3(blocks), dim3(kWThreads), lds, stream, a);
+  const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
+  hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
+                     lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace
+
+int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, bool filter_only, hipStream_t stream) {
+  const size_t lds = (chain_mfma_wide_lds_bytes(NT, a.tab_rows, a.ncol, a.T) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024 || (filter_only && a.H != a.T)) return -1;
+  if (NT == 1) return filter_only ? launch_wide<1, true>(a, lds, stream) : launch_wide<1, false>(a, lds, stream);
+  return filter_only ? launch_wide<2, true>(a, lds, stream) : launch_wide<2, false>(a, lds, stream);
 }
 
 }  // namespace nipamd

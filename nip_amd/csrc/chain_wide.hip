@@ -114,6 +114,10 @@ struct WideChain {
 template <bool FWD, int NP>
 __device__ void wide_wave(const WideArgs& a, const uint8_t* codes, int Tr, double* xb, int y, long b) {
   const int T = a.T, H = a.H;
+  if (a.filter && !FWD) {                  // forward_inference: H = 0, no backward filter
+    __syncthreads();
+    return;
+  }
   WideChain<FWD, NP> ch;
 #pragma unroll
   for (int x = 0; x < NP; x++) ch.Acol[x] = FWD ? a.A[x * 64 + y] : a.A[y * 64 + x];
@@ -144,7 +148,7 @@ __device__ void wide_wave(const WideArgs& a, const uint8_t* codes, int Tr, doubl
       for (int k = 0; k < kWChunk; k++) {
         const int t = t0 + dir * (base + k);            // guards cover the over-run
         e[k] = evidence(t);
-        o[k] = COMBINE ? Srow[(long)t * 64] : 0.0;
+        o[k] = COMBINE ? (a.filter ? 1.0 : Srow[(long)t * 64]) : 0.0;
       }
 #pragma unroll
       for (int k = 0; k < kWChunk; k++) {

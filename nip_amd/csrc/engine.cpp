@@ -444,9 +444,10 @@ int nipamd_m_step(nipamd_model* mm, const double* params) {
   return rc;
 }
 
-int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
-              int B, int T, int n_query, const int* query, double* d_post,
-              double* d_ll, uint32_t* d_status, void* stream) {
+// forward_backward_inference (filt = false) / forward_inference (filt = true)
+static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                   int B, int T, int n_query, const int* query, double* d_post,
+                   double* d_ll, uint32_t* d_status, void* stream, bool filt) {
   if (!mm || B < 0 || T < 1 || (n_obs > 0 && (!d_obs || !obs_vars)) || (n_query > 0 && (!query || !d_post)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   if (B == 0) return 0;
@@ -466,12 +467,13 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
     const char* e = std::getenv("NIPAMD_FB_KERNEL");
     return e && std::string(e) == "wide";
   }();
-  if (!r.narrow && P.N <= 32 && !force_wide) {
+  if ((!r.narrow || filt) && P.N <= 32 && !force_wide) {
     // matrix-core interface chain: N <= 32, up to four observed children
     const int NT = P.N <= 16 ? 1 : 2;
     if (nipamd::chain_mfma_wide_lds_bytes(NT, rt->mtab_rows, r.ncol, T) > 160 * 1024)
       return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
-    if (int rc = ensure_scratch(mm, nipamd::chain_mfma_wide_scratch_bytes(NT, B, T))) return rc;
+    if (int rc = ensure_scratch(mm, filt ? 64 * sizeof(double) : nipamd::chain_mfma_wide_scratch_bytes(NT, B, T)))
+      return rc;
     nipamd::WideMfmaArgs w{};
     w.obs = d_obs; w.obs_bstride = (long)T * ocols; w.obs_tstride = (int)ocols;
     w.ncol = r.ncol;
@@ -481,7 +483,7 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
       w.tab_off[i] = rt->mtab_off[i];
     }
     w.tab_rows = rt->mtab_rows; w.tab = rt->mtab;
-    w.B = B; w.T = T; w.H = T / 2; w.N = P.N;
+    w.B = B; w.T = T; w.H = filt ? T : T / 2; w.N = P.N;
     w.A = d->A64; w.pi = d->pi64; w.w = rt->wv; w.S = d->S;
     w.post = n_query > 0 ? d_post : nullptr;
     w.post_bstride = (long)T * stride; w.post_tstride = stride;
@@ -490,7 +492,7 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
     for (int q = 0; q < nq; q++) {
       w.post_off = q * P.N;
       if (q > 0) { w.ll = nullptr; w.status = nullptr; }
-      if (nipamd::chain_mfma_wide_launch(w, NT, (hipStream_t)stream))
+      if (nipamd::chain_mfma_wide_launch(w, NT, filt, (hipStream_t)stream))
         return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     }
     return 0;
@@ -499,8 +501,11 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
     // wide interface chain: N <= 64, up to four observed children
     if (nipamd::chain_wide_lds_bytes(r.ncol, T) > 64 * 1024)
       return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
-    if (int rc = ensure_scratch(mm, (size_t)(B + 2) * nipamd::chain_scratch_row64(T) * sizeof(double))) return rc;
+    if (int rc = ensure_scratch(mm, filt ? 64 * sizeof(double)
+                                         : (size_t)(B + 2) * nipamd::chain_scratch_row64(T) * sizeof(double)))
+      return rc;
     nipamd::WideArgs w{};
+    w.filter = filt ? 1 : 0;
     w.obs = d_obs; w.obs_bstride = (long)T * ocols; w.obs_tstride = (int)ocols;
     w.ncol = r.ncol;
     for (int i = 0; i < r.ncol; i++) {
@@ -509,7 +514,7 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
       w.tab[i] = rt->tabw + rt->tabw_off[i];
     }
     w.ebase = rt->ebase;
-    w.B = B; w.T = T; w.H = T / 2; w.N = P.N;
+    w.B = B; w.T = T; w.H = filt ? 0 : T / 2; w.N = P.N;
     w.A = d->A64; w.pi = d->pi64; w.s = d->sall64; w.S = d->S;
     w.post = n_query > 0 ? d_post : nullptr;
     w.post_bstride = (long)T * stride; w.post_tstride = stride;
@@ -588,9 +593,22 @@ int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_
   return 0;
 }
 
-int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
-                   int B, int T, int n_query, const int* query, double* post,
-                   double* ll, uint32_t* status) {
+int nipamd_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+              int B, int T, int n_query, const int* query, double* d_post,
+              double* d_ll, uint32_t* d_status, void* stream) {
+  return fb_impl(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_status, stream, false);
+}
+
+int nipamd_filter(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                  int B, int T, int n_query, const int* query, double* d_post,
+                  double* d_ll, uint32_t* d_status, void* stream) {
+  return fb_impl(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_status, stream, true);
+}
+
+// host-buffer form of fb_impl (PCIe-inclusive, synchronous)
+static int fb_host_impl(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
+                        int B, int T, int n_query, const int* query, double* post,
+                        double* ll, uint32_t* status, bool filt) {
   if (!mm || B < 0 || T < 1) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   if (B == 0) return 0;
   int stride = 0;
@@ -603,7 +621,7 @@ int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* o
   HIP_OK(hipMalloc(&d_ll, (size_t)B * sizeof(double)));
   HIP_OK(hipMalloc(&d_st, (size_t)B * sizeof(uint32_t)));
   if (n_obs > 0) HIP_OK(hipMemcpy(d_obs, obs, nob * sizeof(int32_t), hipMemcpyHostToDevice));
-  int rc = nipamd_fb(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_st, nullptr);
+  int rc = fb_impl(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_st, nullptr, filt);
   if (rc == 0) {
     HIP_OK(hipDeviceSynchronize());
     if (post && stride > 0) HIP_OK(hipMemcpy(post, d_post, npo * sizeof(double), hipMemcpyDeviceToHost));
@@ -612,6 +630,18 @@ int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* o
   }
   (void)hipFree(d_obs); (void)hipFree(d_post); (void)hipFree(d_ll); (void)hipFree(d_st);
   return rc;
+}
+
+int nipamd_fb_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
+                   int B, int T, int n_query, const int* query, double* post,
+                   double* ll, uint32_t* status) {
+  return fb_host_impl(mm, obs, n_obs, obs_vars, B, T, n_query, query, post, ll, status, false);
+}
+
+int nipamd_filter_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
+                       int B, int T, int n_query, const int* query, double* post,
+                       double* ll, uint32_t* status) {
+  return fb_host_impl(mm, obs, n_obs, obs_vars, B, T, n_query, query, post, ll, status, true);
 }
 
 int nipamd_estep_partial_size(const nipamd_model* mm) {
