@@ -86,8 +86,9 @@ def load_traffic(workload: str):
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+        e = d.get("entries", {}).get(workload)
+        if e:
+            return e.get("hbm_bytes_per_launch")
     except Exception:
         pass
     return None

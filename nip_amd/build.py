@@ -25,6 +25,7 @@ def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-result", *["-D" + d for d in defines],
+           *os.environ.get("NIPAMD_HIPFLAGS", "").split(),
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"),
            *sources(), "-o", out]
     if verbose:

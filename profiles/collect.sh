@@ -1,19 +1,28 @@
 #!/bin/bash
 # rocprofv3 collection for the bench workloads: kernel-trace stats passes plus
 # separate PMC passes (counters never combined with sys/runtime traces).
-# Usage (on the GPU box, from the repo root):  bash profiles/collect.sh <tag>
+# Usage (on the GPU box, from the repo root):  bash profiles/collect.sh <tag> [workloads...]
 # then, back in the build container:  python profiles/summarize.py <tag>
+# Workloads: fb (config 2, the headline), config3, config5, estep (config 4 shard).
 set -euo pipefail
 TAG=${1:-run}
+shift || true
+WLS=${*:-fb config3 config5 estep}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
-mkdir -p $OUT
+mkdir -p $OUT; for W in ${*:-fb config3 config5 estep}; do mkdir -p $OUT/$W; done
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 5 --warmup 1 --no-cpu-baseline"
-EST="$R/bench.py --workload estep --batch 131072 --steps 3 --warmup 1"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH > $OUT/trace.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_estep -o run --output-format csv -- python3 $EST > $OUT/trace_estep.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc2 -o run --output-format csv -- python3 $BENCH > $OUT/pmc2.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc3 -o run --output-format csv -- python3 $BENCH > $OUT/pmc3.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $OUT/pmc1 -o run --output-format csv -- python3 $BENCH > $OUT/pmc1.log 2>&1
-echo done
+for W in $WLS; do
+  case $W in
+    estep) ARGS="--workload estep --batch 131072 --steps 3 --warmup 1" ;;
+    *) ARGS="--workload $W --steps 5 --warmup 1 --no-cpu-baseline" ;;
+  esac
+  B="$R/bench.py $ARGS"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$W/trace -o run --output-format csv -- python3 $B > $OUT/$W/trace.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/$W/pmc2 -o run --output-format csv -- python3 $B > $OUT/$W/pmc2.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/$W/pmc3 -o run --output-format csv -- python3 $B > $OUT/$W/pmc3.log 2>&1
+  if [ "$W" = fb ]; then
+    timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $OUT/$W/pmc1 -o run --output-format csv -- python3 $B > $OUT/$W/pmc1.log 2>&1
+  fi
+  echo "$W done"
+done

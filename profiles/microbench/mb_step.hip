@@ -55,12 +55,48 @@ __global__ __launch_bounds__(64, 1) void k(const double* in, double* out, unsign
   const int l = threadIdx.x;
   double A[4] = {in[l] * 0.1, in[l + 64] * 0.1, in[l + 128] * 0.1, in[l + 192] * 0.1};
   v4d X = {in[l + 256], in[l + 320], in[l + 384], in[l + 448]};
-  v4d e = {0.5, 0.25, 0.125, 0.0625};
+  v4d e = {in[l + 512], in[l + 576], in[l + 640], in[l + 704]};   // not constant-folded
   v4d s = {1, 1, 1, 1};
   int sc = 0; double m2 = 1, m1 = 1;
   unsigned long long t0 = __builtin_readcyclecounter();
   v4d D = matvec(A, X);
   for (int i = 0; i < n; i++) {
+    if (V == 11 || V == 12 || V == 13) {         // next MFMAs interleaved with this step's VALU
+      v4d u = ldexp4(D, sc);
+      v4d p = u * e;
+      v4d d = {0, 0, 0, 0};
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      d = __builtin_amdgcn_mfma_f64_16x16x4f64(A[0], p.x, d, 0, 0, 0);
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      const double loc = (p.x + p.y) + (p.z + p.w);
+      const double h = sum_lanes32(loc);
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      d = __builtin_amdgcn_mfma_f64_16x16x4f64(A[1], p.y, d, 0, 0, 0);
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      const double z2 = sum_lanes16(h);
+      sc = -__builtin_amdgcn_frexp_exp(z2); m2 *= z2;
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      d = __builtin_amdgcn_mfma_f64_16x16x4f64(A[2], p.z, d, 0, 0, 0);
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      *reinterpret_cast<double2*>(lds + (l * 2 + (i & 3) * 128)) = make_double2(p.x, p.y);
+      *reinterpret_cast<double2*>(lds + (l * 2 + (i & 3) * 128 + 256)) = make_double2(p.z, p.w);
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      d = __builtin_amdgcn_mfma_f64_16x16x4f64(A[3], p.w, d, 0, 0, 0);
+      if (V == 13) __builtin_amdgcn_sched_barrier(0);
+      if (V == 12) {
+        // MFMA, VALU x4, MFMA, VALU x6, MFMA, DS write x2, MFMA
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      D = d;
+      X = p;
+      continue;
+    }
     if (V >= 5 && V < 8) {                       // software-pipelined: next MFMAs issued before this step's sums
       v4d u = ldexp4(D, sc);
       v4d p = u * e;
@@ -124,6 +160,9 @@ int main() {
     run<8>("MFMA: two chains of two + add", din, dout, dc, blocks);
     run<9>("MFMA: four independent + adds", din, dout, dc, blocks);
     run<10>("ldexp,*e + z2 via ones-MFMA (cf. row 3)", din, dout, dc, blocks);
+    run<11>("interleaved source order (row 4 work)", din, dout, dc, blocks);
+    run<12>("interleaved + sched_group_barrier", din, dout, dc, blocks);
+    run<13>("interleaved, pinned by sched_barrier", din, dout, dc, blocks);
   }
   return 0;
 }

@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
 """Summarise a profiles/collect.sh run into committed files under profiles/.
 
-  python profiles/summarize.py <tag>     (reads gpurun_out/prof_<tag>/)
+  python profiles/summarize.py <tag>     (reads gpurun_out/prof_<tag>/<workload>/)
 
-Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats of the bench),
-profiles/<tag>_estep_kernel_stats.csv, profiles/<tag>_counters.json, and
-profiles/pmc_traffic.json (HBM bytes per launch of the dominant kernel, read
-by bench.py).  HBM bytes follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE
-and WRITE_SIZE are in KiB; FETCH_SIZE is doubled on gfx950 (it tallies 128-B
-requests at 64 B), WRITE_SIZE is taken as is.
+For every workload collected, writes profiles/<tag>_<workload>_kernel_stats.csv
+(rocprofv3 --stats) and profiles/<tag>_<workload>_counters.json, and records in
+profiles/pmc_traffic.json the HBM bytes per launch of the workload's dominant
+kernel (read by bench.py, keyed by the bench's config.workload string).  HBM
+bytes follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE and WRITE_SIZE are
+in KiB; FETCH_SIZE is doubled on gfx950 (it tallies 128-B requests at 64 B),
+WRITE_SIZE is taken as is.
 """
 import collections
 import csv
@@ -19,7 +20,6 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-KERNEL = "chain_fb_mfma_kernel"
 
 
 def per_kernel(path, counter):
@@ -30,39 +30,58 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def bench_line(log):
+    for line in open(log):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
+def dominant(stats_csv):
+    rows = list(csv.DictReader(open(stats_csv)))
+    rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+    return rows[0]["Name"]
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
-    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
-                os.path.join(HERE, tag + "_kernel_stats.csv"))
-    est = os.path.join(src, "trace_estep", "run_kernel_stats.csv")
-    if os.path.exists(est):
-        shutil.copy(est, os.path.join(HERE, tag + "_estep_kernel_stats.csv"))
-    counters = {}
-    for pas in ("pmc1", "pmc2", "pmc3"):
-        f = os.path.join(src, pas, "run_counter_collection.csv")
-        if not os.path.exists(f):
+    tp = os.path.join(HERE, "pmc_traffic.json")
+    try:
+        table = json.load(open(tp))
+        if "entries" not in table:
+            table = {"entries": {}}
+    except Exception:
+        table = {"entries": {}}
+    for w in sorted(os.listdir(src)):
+        d = os.path.join(src, w)
+        stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+        if not os.path.isdir(d) or not os.path.exists(stats):
             continue
-        names = {r["Counter_Name"] for r in csv.DictReader(open(f))}
-        for n in names:
-            for k, v in per_kernel(f, n).items():
-                if KERNEL in k:
-                    counters[n] = v
-    fetch = counters.get("FETCH_SIZE")
-    write = counters.get("WRITE_SIZE")
-    with open(os.path.join(HERE, tag + "_counters.json"), "w") as f:
-        json.dump({"kernel": KERNEL, "per_launch_mean": counters}, f, indent=1)
-    if fetch is not None and write is not None:
-        rd = 2 * fetch * 1024
-        wr = write * 1024
-        d = {"workload": "config2: HMM-shaped DBN, 16 hidden x 16 observed states, B=4096 seq/GPU x T=1024",
-             "kernel": KERNEL, "tag": tag,
-             "fetch_size_kib": fetch, "write_size_kib": write,
-             "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-             "hbm_bytes_per_launch": rd + wr,
-             "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KiB -> bytes"}
-        with open(os.path.join(HERE, "pmc_traffic.json"), "w") as f:
-            json.dump(d, f, indent=1)
-        print(json.dumps(d))
+        shutil.copy(stats, os.path.join(HERE, "%s_%s_kernel_stats.csv" % (tag, w)))
+        kname = dominant(stats)
+        rec = bench_line(os.path.join(d, "trace.log"))
+        counters = {}
+        for pas in ("pmc1", "pmc2", "pmc3"):
+            f = os.path.join(d, pas, "run_counter_collection.csv")
+            if not os.path.exists(f):
+                continue
+            for n in {r["Counter_Name"] for r in csv.DictReader(open(f))}:
+                for k, v in per_kernel(f, n).items():
+                    if k == kname:
+                        counters[n] = v
+        with open(os.path.join(HERE, "%s_%s_counters.json" % (tag, w)), "w") as f:
+            json.dump({"kernel": kname, "per_launch_mean": counters}, f, indent=1)
+        fetch, write = counters.get("FETCH_SIZE"), counters.get("WRITE_SIZE")
+        if rec and fetch is not None and write is not None:
+            rd, wr = 2 * fetch * 1024, write * 1024
+            e = {"kernel": kname, "tag": tag, "fetch_size_kib": fetch, "write_size_kib": write,
+                 "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                 "hbm_bytes_per_launch": rd + wr,
+                 "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KiB -> bytes"}
+            table["entries"][rec["config"]["workload"]] = e
+            print(w, json.dumps(e))
+    with open(tp, "w") as f:
+        json.dump(table, f, indent=1)
 
 
 if __name__ == "__main__":
