@@ -208,6 +208,37 @@ int nipamd_model_prior(const nipamd_model* m, int v, double* out);
 /* Last error message (thread-local), for diagnostics. */
 const char* nipamd_last_error(void);
 
+/* Name of state `state` of variable `var` (the .net `states` field; "0".."card-1"
+ * for models built from a spec).  Copies at most cap-1 bytes into buf; returns
+ * the full length, -1 on bad arguments.  Replaces nip_variable_state_name
+ * (src/nipvariable.c:250-254). */
+int nipamd_model_state_name(const nipamd_model* m, int var, int state, char* buf, int cap);
+
+/*
+ * Time-series data files, the reference's text format:
+ * a line of node symbols, then one line per time step (tokens separated by
+ * ',' and/or white space), series separated by empty lines; unknown tokens
+ * ("null", "N/A", "<null>", ...) are missing (-1).  Columns whose symbol is
+ * not a model variable are ignored.
+ *   nipamd_read_timeseries  replaces read_timeseries (src/nip.c:512-667) with
+ *                           nip_open_data_file / nip_next_line_tokens
+ *                           (src/nipparsers.c:48-522)
+ *   nipamd_write_uncertainseries replaces write_uncertainseries
+ *                           (src/nip.c:815-893): state names, then "%f" rows.
+ */
+typedef struct nipamd_series nipamd_series;
+int nipamd_read_timeseries(const nipamd_model* m, const char* path, nipamd_series** out);
+int nipamd_series_count(const nipamd_series* s);
+int nipamd_series_num_observed(const nipamd_series* s);
+int nipamd_series_observed(const nipamd_series* s, int* vars);   /* model variable per column */
+int nipamd_series_length(const nipamd_series* s, int i);
+const int32_t* nipamd_series_data(const nipamd_series* s, int i); /* [length][n_observed] */
+void nipamd_series_free(nipamd_series* s);
+/* post: the series' posteriors back to back, rows of `stride` doubles, the
+ * variable's card() values at `offset` in each row */
+int nipamd_write_uncertainseries(const nipamd_model* m, const char* path, int var, int n_series,
+                                 const int* lengths, const double* post, int stride, int offset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,8 +19,9 @@ import numpy as np
 from . import build as _build
 
 __all__ = ["NipError", "Model", "parse_model", "lib", "forward_backward_inference",
-           "forward_backward_inference_host", "e_step", "estep_partial", "estep_finalize",
-           "em_learn", "LIB_PATH"]
+           "forward_backward_inference_host", "forward_inference", "forward_inference_host",
+           "e_step", "estep_partial", "estep_finalize", "em_learn", "read_timeseries",
+           "write_uncertainseries", "LIB_PATH"]
 
 LIB_PATH = os.environ.get("NIPAMD_LIB", _build.LIB)
 
@@ -47,6 +48,9 @@ EXPORTS = [
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
     "nipamd_estep_finalize", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
+    "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
+    "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
+    "nipamd_series_data", "nipamd_series_free", "nipamd_write_uncertainseries",
 ]
 
 
@@ -95,6 +99,18 @@ def lib():
         L.nipamd_model_prior.argtypes = [vp, C.c_int, dp]
         L.nipamd_last_error.restype = C.c_char_p
         L.nipamd_graph_cliques.argtypes = [C.c_int, ip, C.c_int, ip, C.c_int, ip, ip, C.c_int]
+        L.nipamd_model_state_name.argtypes = [vp, C.c_int, C.c_int, C.c_char_p, C.c_int]
+        L.nipamd_read_timeseries.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
+        L.nipamd_series_count.argtypes = [vp]
+        L.nipamd_series_num_observed.argtypes = [vp]
+        L.nipamd_series_observed.argtypes = [vp, ip]
+        L.nipamd_series_length.argtypes = [vp, C.c_int]
+        L.nipamd_series_data.argtypes = [vp, C.c_int]
+        L.nipamd_series_data.restype = C.POINTER(C.c_int32)
+        L.nipamd_series_free.argtypes = [vp]
+        L.nipamd_series_free.restype = None
+        L.nipamd_write_uncertainseries.argtypes = [vp, C.c_char_p, C.c_int, C.c_int, ip, dp, C.c_int,
+                                                   C.c_int]
         _lib = L
     return _lib
 
@@ -169,6 +185,16 @@ class Model:
     def variable(self, symbol: str) -> int:
         """model_variable() (src/nip.c:1584): index of a symbol, or -1."""
         return lib().nipamd_model_var_index(self._h, symbol.encode())
+
+    def state_names(self, v: int):
+        """The variable's state names (nip_variable_state_name)."""
+        out = []
+        for st in range(self.card(v)):
+            n = lib().nipamd_model_state_name(self._h, v, st, None, 0)
+            buf = C.create_string_buffer(n + 1)
+            lib().nipamd_model_state_name(self._h, v, st, buf, n + 1)
+            out.append(buf.value.decode())
+        return out
 
     def card(self, v: int) -> int:
         return lib().nipamd_model_var_card(self._h, int(v))
@@ -295,6 +321,44 @@ def forward_backward_inference_host(model: Model, obs, obs_vars, query):
 def forward_inference_host(model: Model, obs, obs_vars, query):
     """forward_inference from host numpy buffers (PCIe-inclusive, synchronous)."""
     return _run_host(lib().nipamd_filter_host, model, obs, obs_vars, query)
+
+
+def read_timeseries(model: Model, path):
+    """read_timeseries() (src/nip.c:512-667) of the reference's data-file format.
+
+    Returns (series, obs_vars): a list of int32 arrays [T_i, n_obs] (state
+    index, -1 missing) and the model variable of each column (file order).
+    """
+    h = C.c_void_p()
+    _check(lib().nipamd_read_timeseries(model._h, os.fsencode(path), C.byref(h)))
+    try:
+        L = lib()
+        n, k = L.nipamd_series_count(h), L.nipamd_series_num_observed(h)
+        ov = (C.c_int * max(k, 1))()
+        _check(L.nipamd_series_observed(h, ov))
+        out = []
+        for i in range(n):
+            T = L.nipamd_series_length(h, i)
+            if k == 0:
+                out.append(np.zeros((T, 0), np.int32))
+                continue
+            p = L.nipamd_series_data(h, i)
+            out.append(np.ctypeslib.as_array(p, shape=(T * k,)).reshape(T, k).copy())
+        return out, [ov[i] for i in range(k)]
+    finally:
+        lib().nipamd_series_free(h)
+
+
+def write_uncertainseries(model: Model, path, var: int, posts):
+    """write_uncertainseries() (src/nip.c:815-893): `posts` is a list of
+    arrays [T_i, card(var)] (or wider rows with the variable first)."""
+    posts = [np.ascontiguousarray(p, np.float64) for p in posts]
+    stride = posts[0].shape[1]
+    flat = np.ascontiguousarray(np.concatenate(posts, axis=0))
+    lengths = np.array([p.shape[0] for p in posts], np.int32)
+    _check(lib().nipamd_write_uncertainseries(
+        model._h, os.fsencode(path), var, len(posts), lengths.ctypes.data_as(C.POINTER(C.c_int)),
+        flat.ctypes.data_as(C.POINTER(C.c_double)), stride, 0))
 
 
 def _obs3(obs, obs_vars):

@@ -34,7 +34,24 @@ def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
+    if out == LIB:
+        build_tools(verbose)
     return out
+
+
+TOOLS = ["nipamd_inference"]
+
+
+def build_tools(verbose: bool = False):
+    """The CLI counterparts of the reference's util/ programs (nip_amd/tools),
+    plain C++ over the C-ABI, next to the library (rpath $ORIGIN)."""
+    for t in TOOLS:
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall",
+               "-I" + os.path.join(ROOT, "include"), os.path.join(PKG, "tools", t + ".cpp"),
+               "-L" + LIB_DIR, "-lnip_amd", "-Wl,-rpath,$ORIGIN", "-o", os.path.join(LIB_DIR, t)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
 
 
 if __name__ == "__main__":

@@ -305,6 +305,11 @@ int compile_model(const NetSpec& spec, Model& m, std::string& err) {
     m.vars[i].symbol = i < (int)spec.symbols.size() ? spec.symbols[i] : ("V" + std::to_string(i));
     m.vars[i].card = spec.card[i];
     if (spec.card[i] <= 0) { err = "non-positive cardinality"; return NIP_ERROR_INVALID_ARGUMENT; }
+    if (i < (int)spec.states.size() && (int)spec.states[i].size() == spec.card[i]) {
+      m.vars[i].states = spec.states[i];
+    } else {
+      for (int s = 0; s < spec.card[i]; s++) m.vars[i].states.push_back(std::to_string(s));
+    }
   }
   auto& V = m.vars;
 
@@ -683,6 +688,11 @@ void build_chain_plan(Model& m) {
       for (int y = 0; y < N; y++) P.A[x * 16 + y] = P.A64[x * 64 + y];
     }
   }
+  P.self.var = vc;
+  P.self.M = N;
+  P.self.E.assign((size_t)N * 64, 0.0);
+  P.self.s.assign(64, 0.0);
+  for (int y = 0; y < N; y++) { P.self.E[(size_t)y * 64 + y] = 1.0; P.self.s[y] = 1.0; }
   P.hmm = hidden.empty() && P.emits.size() == 1 && V.size() == 3 && N <= 16;
   P.valid = true;
 }

@@ -20,11 +20,6 @@
 #include "model.h"
 #include "nip_amd.h"
 
-struct nipamd_model {
-  nipamd::Model m;
-  unsigned version = 1;          // bumped whenever the tables change
-};
-
 namespace {
 
 thread_local std::string g_err;
@@ -155,11 +150,11 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
       for (size_t k = 0; k < P.emits.size(); k++) if ((int)k != r.primary) v *= P.emits[k].s[y];
       b[y] = v;
     }
-    const int M = r.primary >= 0 ? P.emits[r.primary].M : 0;
+    const int M = r.primary >= 0 ? P.emit(r.primary).M : 0;
     std::vector<double> E((size_t)(M + 2) * 16, 0.0);
     for (int y = 0; y < N; y++) {
-      for (int m = 0; m < M; m++) E[(size_t)m * 16 + y] = P.emits[r.primary].E[(size_t)m * 64 + y] * b[y];
-      E[(size_t)M * 16 + y] = (r.primary >= 0 ? P.emits[r.primary].s[y] : 1.0) * b[y];
+      for (int m = 0; m < M; m++) E[(size_t)m * 16 + y] = P.emit(r.primary).E[(size_t)m * 64 + y] * b[y];
+      E[(size_t)M * 16 + y] = (r.primary >= 0 ? P.emit(r.primary).s[y] : 1.0) * b[y];
     }
     std::vector<double> ts(16, 0.0);
     for (int x = 0; x < N; x++) {
@@ -174,7 +169,7 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
   // wide: one unscaled table per observed child, the unobserved ones in ebase
   std::vector<double> W;
   for (int i = 0; i < r.ncol; i++) {
-    const auto& em = P.emits[r.emit[i]];
+    const auto& em = P.emit(r.emit[i]);
     t.tabw_off.push_back(W.size());
     const size_t base = W.size();
     W.resize(base + (size_t)(em.M + 2) * 64, 0.0);
@@ -200,14 +195,14 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
     std::vector<double> MT;
     const int nc = r.ncol > 0 ? r.ncol : 1;
     for (int i = 0; i < nc; i++) {
-      const int M = r.ncol > 0 ? P.emits[r.emit[i]].M : 0;
+      const int M = r.ncol > 0 ? P.emit(r.emit[i]).M : 0;
       t.mtab_off[i] = (int)MT.size();
       const size_t base = MT.size();
       MT.resize(base + (size_t)(M + 2) * NP, 0.0);
       for (int y = 0; y < N; y++) {
         const double f = i == 0 ? eb[y] : 1.0;
         if (r.ncol > 0) {
-          const auto& em = P.emits[r.emit[i]];
+          const auto& em = P.emit(r.emit[i]);
           for (int m = 0; m < M; m++) MT[base + (size_t)m * NP + y] = em.E[(size_t)m * 64 + y] * f;
           MT[base + (size_t)M * NP + y] = em.s[y] * f;
         } else {
@@ -292,7 +287,11 @@ int route_request(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_
   for (int i = 0; i < n_obs; i++) {
     int k = -1;
     for (size_t e = 0; e < P.emits.size(); e++) if (P.emits[e].var == obs_vars[i]) k = (int)e;
-    if (k < 0) { why = "evidence on a variable that is not a leaf child of the interface variable"; return 0; }
+    if (obs_vars[i] == P.v_cur) k = (int)P.emits.size();          // the interface variable itself
+    if (k < 0) {
+      why = "evidence on a variable that is neither the interface variable nor a leaf child of it";
+      return 0;
+    }
     for (int j = 0; j < r.ncol; j++) if (r.emit[j] == k) { why = "observed variable listed twice"; return 0; }
     if (r.ncol == 4) { why = "more than four observed children"; return 0; }
     r.col[r.ncol] = i; r.emit[r.ncol] = k; r.ncol++;
@@ -306,6 +305,10 @@ int route_request(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_
 }
 
 }  // namespace
+
+namespace nipamd {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace nipamd
 
 extern "C" {
 
@@ -479,7 +482,7 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     w.ncol = r.ncol;
     for (int i = 0; i < 4; i++) {
       w.col[i] = i < r.ncol ? r.col[i] : 0;
-      w.M[i] = i < r.ncol ? P.emits[r.emit[i]].M : 0;
+      w.M[i] = i < r.ncol ? P.emit(r.emit[i]).M : 0;
       w.tab_off[i] = rt->mtab_off[i];
     }
     w.tab_rows = rt->mtab_rows; w.tab = rt->mtab;
@@ -510,7 +513,7 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     w.ncol = r.ncol;
     for (int i = 0; i < r.ncol; i++) {
       w.col[i] = r.col[i];
-      w.M[i] = P.emits[r.emit[i]].M;
+      w.M[i] = P.emit(r.emit[i]).M;
       w.tab[i] = rt->tabw + rt->tabw_off[i];
     }
     w.ebase = rt->ebase;
@@ -661,6 +664,8 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   const auto& P = mm->m.chain;
   if (!P.hmm)
     return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice (prev, cur, one child)");
+  if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0))
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan: evidence on the observed child only");
   const int col = r.pcol;
   const int Mo = P.emits[0].M;
   if (nipamd::chain_lds_bytes(Mo, T, true) > 96 * 1024)

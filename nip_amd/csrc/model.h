@@ -17,6 +17,7 @@ enum : int { IF_NONE = 0, IF_INCOMING = 1, IF_OUTGOING = 2, IF_OLD_OUTGOING = 4 
 struct Var {
   std::string symbol;
   int card = 0;
+  std::vector<std::string> states;  // state names (the .net `states` field)
   int next = -1, previous = -1;     // next-slice / previous-slice variable
   std::vector<int> parents;         // v->parents order (reversed file order)
   bool has_prior = false;           // independent variable with a prior vector
@@ -42,6 +43,7 @@ struct Sepset {
 struct NetSpec {
   std::vector<std::string> symbols;
   std::vector<int> card;
+  std::vector<std::vector<std::string>> states;   // may be empty: names "0".."card-1"
   std::vector<int> next;
   struct Pot { int child; std::vector<int> parents; std::vector<double> data; bool has_data; };
   std::vector<Pot> pots;
@@ -69,6 +71,11 @@ struct ChainPlan {
   int c_trans = -1;                 // the in-clique
   std::vector<int> hidden;          // H
   std::vector<ChainEmit> emits;
+  // evidence on cur itself (read_timeseries marks every variable, so data
+  // files can observe the interface variable): an indicator "child" with
+  // E = identity and s = 1, addressed as emit index emits.size()
+  ChainEmit self;
+  const ChainEmit& emit(int k) const { return k == (int)emits.size() ? self : emits[k]; }
   std::vector<double> A64;          // [64][64]
   std::vector<double> pi64;         // [64] prior of prev
   std::vector<double> s_all64;      // [64] product of every child's s
@@ -107,3 +114,9 @@ int m_step(Model& m, const double* params);
 int parse_net_file(const std::string& text, NetSpec& spec, std::string& err);
 
 }  // namespace nipamd
+
+// The opaque handle of the C-ABI (include/nip_amd.h).
+struct nipamd_model {
+  nipamd::Model m;
+  unsigned version = 1;          // bumped whenever the tables change
+};

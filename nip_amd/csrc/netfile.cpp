@@ -110,6 +110,7 @@ int parse_net_file(const std::string& text, NetSpec& spec, std::string& err) {
       if (states.empty()) { err = "net parser: the states field is missing (node " + sym + ")"; return NIP_ERROR_IO; }
       spec.symbols.push_back(sym);
       spec.card.push_back((int)states.size());
+      spec.states.push_back(states);
       next_sym.push_back(nx);
     } else if (toks[i].first == 'w' && w == "potential") {
       i++;
