@@ -201,6 +201,25 @@ int nipamd_estep_finalize(nipamd_model* m, const double* d_partial,
  * and re-initialise the model's tables and priors from them. */
 int nipamd_m_step(nipamd_model* m, const double* params);
 
+/*
+ * em_learn(ts, n_ts, threshold, learning_curve) (src/nip.c:2076-2243) for
+ * series of any lengths on one GPU.  obs: the series back to back
+ * ([sum lengths][n_obs], state index, -1 missing); init: initial parameters
+ * in the em_learn layout, or NULL to draw rand()/RAND_MAX like the reference
+ * (seed with srand first); max_iterations: 0 = the reference's stopping rule
+ * only.  The learning curve (average log-likelihood per time step per
+ * iteration) goes to curve[0..curve_cap).  Returns NIP_NO_ERROR or
+ * NIP_ERROR_BAD_LUCK (or an argument / device error); the model keeps the
+ * parameters of the last m_step.
+ */
+int nipamd_em_learn(nipamd_model* m, int n_series, const int* lengths, const int32_t* obs,
+                    int n_obs, const int* obs_vars, double threshold, const double* init,
+                    int max_iterations, double* curve, int curve_cap, int* curve_len);
+
+/* write_model (src/nip.c:298-484): the model as a Hugin .net file in the
+ * reference's layout (learned CPTs from the family cliques, "%f" values). */
+int nipamd_write_model(const nipamd_model* m, const char* path);
+
 /* Current clique original table / prior of an independent variable. */
 int nipamd_model_original(const nipamd_model* m, int clique, double* out, int cap);
 int nipamd_model_prior(const nipamd_model* m, int v, double* out);
@@ -213,6 +232,9 @@ const char* nipamd_last_error(void);
  * the full length, -1 on bad arguments.  Replaces nip_variable_state_name
  * (src/nipvariable.c:250-254). */
 int nipamd_model_state_name(const nipamd_model* m, int var, int state, char* buf, int cap);
+/* Symbol of variable `var` (nip_variable_symbol, src/nipvariable.c); same
+ * buffer convention. */
+int nipamd_model_var_symbol(const nipamd_model* m, int var, char* buf, int cap);
 
 /*
  * Time-series data files, the reference's text format:

@@ -21,7 +21,7 @@ from . import build as _build
 __all__ = ["NipError", "Model", "parse_model", "lib", "forward_backward_inference",
            "forward_backward_inference_host", "forward_inference", "forward_inference_host",
            "e_step", "estep_partial", "estep_finalize", "em_learn", "read_timeseries",
-           "write_uncertainseries", "LIB_PATH"]
+           "write_uncertainseries", "write_model", "em_learn_series", "LIB_PATH"]
 
 LIB_PATH = os.environ.get("NIPAMD_LIB", _build.LIB)
 
@@ -51,6 +51,7 @@ EXPORTS = [
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
     "nipamd_series_data", "nipamd_series_free", "nipamd_write_uncertainseries",
+    "nipamd_em_learn", "nipamd_write_model", "nipamd_model_var_symbol",
 ]
 
 
@@ -111,6 +112,10 @@ def lib():
         L.nipamd_series_free.restype = None
         L.nipamd_write_uncertainseries.argtypes = [vp, C.c_char_p, C.c_int, C.c_int, ip, dp, C.c_int,
                                                    C.c_int]
+        L.nipamd_em_learn.argtypes = [vp, C.c_int, ip, vp, C.c_int, ip, C.c_double, dp, C.c_int, dp,
+                                      C.c_int, ip]
+        L.nipamd_write_model.argtypes = [vp, C.c_char_p]
+        L.nipamd_model_var_symbol.argtypes = [vp, C.c_int, C.c_char_p, C.c_int]
         _lib = L
     return _lib
 
@@ -347,6 +352,35 @@ def read_timeseries(model: Model, path):
         return out, [ov[i] for i in range(k)]
     finally:
         lib().nipamd_series_free(h)
+
+
+def write_model(model: Model, path):
+    """write_model() (src/nip.c:298-484): the model as a Hugin .net file."""
+    _check(lib().nipamd_write_model(model._h, os.fsencode(path)))
+
+
+def em_learn_series(model: Model, series, obs_vars, threshold, init=None, max_iterations=0):
+    """em_learn() for series of any lengths on one GPU (nipamd_em_learn).
+
+    series: list of int32 arrays [T_i, n_obs].  init: initial parameters in the
+    em_learn layout, or None for rand()/RAND_MAX draws like the reference (C
+    rand(); seed it with libc's srand).  Returns (rc, learning_curve)."""
+    series = [np.ascontiguousarray(np.asarray(s, np.int32).reshape(len(s), -1)) for s in series]
+    k = len(obs_vars)
+    flat = np.ascontiguousarray(np.concatenate(series, axis=0)) if k else np.zeros(1, np.int32)
+    lengths = np.array([len(s) for s in series], np.int32)
+    cap = 100000
+    curve = np.zeros(cap)
+    n = C.c_int(0)
+    ini = None if init is None else np.ascontiguousarray(init, np.float64)
+    rc = lib().nipamd_em_learn(model._h, len(series), lengths.ctypes.data_as(C.POINTER(C.c_int)),
+                               flat.ctypes.data_as(C.c_void_p), k, _ints(obs_vars), threshold,
+                               None if ini is None else ini.ctypes.data_as(C.POINTER(C.c_double)),
+                               max_iterations, curve.ctypes.data_as(C.POINTER(C.c_double)), cap,
+                               C.byref(n))
+    if rc not in (0, 8):
+        _check(rc)
+    return rc, list(curve[:n.value])
 
 
 def write_uncertainseries(model: Model, path, var: int, posts):

@@ -39,7 +39,7 @@ def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
     return out
 
 
-TOOLS = ["nipamd_inference"]
+TOOLS = ["nipamd_inference", "nipamd_train"]
 
 
 def build_tools(verbose: bool = False):

@@ -305,12 +305,19 @@ int compile_model(const NetSpec& spec, Model& m, std::string& err) {
     m.vars[i].symbol = i < (int)spec.symbols.size() ? spec.symbols[i] : ("V" + std::to_string(i));
     m.vars[i].card = spec.card[i];
     if (spec.card[i] <= 0) { err = "non-positive cardinality"; return NIP_ERROR_INVALID_ARGUMENT; }
+    if (i < (int)spec.labels.size()) m.vars[i].label = spec.labels[i];
+    if (i < (int)spec.positions.size()) {
+      m.vars[i].pos_x = spec.positions[i].first;
+      m.vars[i].pos_y = spec.positions[i].second;
+    }
     if (i < (int)spec.states.size() && (int)spec.states[i].size() == spec.card[i]) {
       m.vars[i].states = spec.states[i];
     } else {
       for (int s = 0; s < spec.card[i]; s++) m.vars[i].states.push_back(std::to_string(s));
     }
   }
+  m.node_size_x = spec.node_size_x;
+  m.node_size_y = spec.node_size_y;
   auto& V = m.vars;
 
   // --- potentialDeclaration actions (huginnet.y:582-780) ---

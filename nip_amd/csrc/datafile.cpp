@@ -37,10 +37,6 @@ struct nipamd_series {
   std::vector<int32_t> data;           // [sum lengths][n_obs]
 };
 
-namespace nipamd {
-int set_error(int code, const std::string& msg);
-}
-
 namespace {
 
 constexpr int kMaxLine = 10000;
@@ -186,6 +182,16 @@ int nipamd_write_uncertainseries(const nipamd_model* mm, const char* path, int v
   }
   if (std::fclose(f)) return nipamd::set_error(NIP_ERROR_IO, std::string("cannot close ") + path);
   return NIP_NO_ERROR;
+}
+
+int nipamd_model_var_symbol(const nipamd_model* mm, int var, char* buf, int cap) {
+  if (!mm || var < 0 || var >= (int)mm->m.vars.size()) return -1;
+  const std::string& n = mm->m.vars[var].symbol;
+  if (buf && cap > 0) {
+    std::strncpy(buf, n.c_str(), (size_t)cap - 1);
+    buf[cap - 1] = '\0';
+  }
+  return (int)n.size();
 }
 
 int nipamd_model_state_name(const nipamd_model* mm, int var, int state, char* buf, int cap) {

@@ -18,6 +18,8 @@ struct Var {
   std::string symbol;
   int card = 0;
   std::vector<std::string> states;  // state names (the .net `states` field)
+  std::string label = " ";          // v->name
+  int pos_x = 100, pos_y = 100;
   int next = -1, previous = -1;     // next-slice / previous-slice variable
   std::vector<int> parents;         // v->parents order (reversed file order)
   bool has_prior = false;           // independent variable with a prior vector
@@ -44,6 +46,9 @@ struct NetSpec {
   std::vector<std::string> symbols;
   std::vector<int> card;
   std::vector<std::vector<std::string>> states;   // may be empty: names "0".."card-1"
+  std::vector<std::string> labels;                // `label` (" " if absent, huginnet.y:328-329)
+  std::vector<std::pair<int, int>> positions;     // `position` (100 100 if absent, huginnet.y:49-50)
+  int node_size_x = 80, node_size_y = 60;         // net-level `node_size` (huginnet.y:51-52)
   std::vector<int> next;
   struct Pot { int child; std::vector<int> parents; std::vector<double> data; bool has_data; };
   std::vector<Pot> pots;
@@ -87,6 +92,7 @@ struct ChainPlan {
 };
 struct Model {
   std::vector<Var> vars;
+  int node_size_x = 80, node_size_y = 60;
   std::vector<Clique> cliques;
   std::vector<Sepset> sepsets;
   int in_clique = -1, out_clique = -1;
@@ -112,6 +118,10 @@ int m_step(Model& m, const double* params);
 
 // netfile.cpp
 int parse_net_file(const std::string& text, NetSpec& spec, std::string& err);
+// engine.cpp: record the message behind a C-ABI error code (nipamd_last_error)
+int set_error(int code, const std::string& msg);
+// netwrite.cpp: write_model (src/nip.c:298-484)
+int write_net_file(const Model& m, const std::string& path, std::string& err);
 
 }  // namespace nipamd
 

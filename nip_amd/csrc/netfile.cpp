@@ -3,7 +3,8 @@
 // Covers the subset of the Hugin net language that src/huginnet.y accepts
 // (grammar at huginnet.y:202-834, lexer at :845-1047): an optional `net { }`
 // block (contents ignored), `node`/`discrete node` declarations with `states`,
-// `NIP_next` (and ignored label/position/other fields), and `potential`
+// `NIP_next`, `label`, `position` (other fields ignored), the net block's
+// `node_size`, and `potential`
 // declarations `(child)`, `(child | parents...)` with an optional `data` list.
 // `%` starts a comment outside quotes.  Declaration order is preserved because
 // it fixes the variable IDs (nipvariable.c:60,72).
@@ -82,7 +83,15 @@ int parse_net_file(const std::string& text, NetSpec& spec, std::string& err) {
       i++;
       if (w == "class" && i < toks.size()) i++;  // class name
       if (w == "class") { if (!expect('{')) return NIP_ERROR_IO; continue; }
+      // net { ... node_size = (x y); ... }  (huginnet.y:572-574)
+      const size_t b0 = i;
       skip_block();
+      for (size_t q = b0; q + 5 < i; q++)
+        if (toks[q].first == 'w' && toks[q].second == "node_size" && toks[q + 1].first == '=' &&
+            toks[q + 2].first == '(') {
+          spec.node_size_x = std::abs((int)std::strtod(toks[q + 3].second.c_str(), nullptr));
+          spec.node_size_y = std::abs((int)std::strtod(toks[q + 4].second.c_str(), nullptr));
+        }
     } else if (toks[i].first == 'w' && (w == "node" || w == "discrete")) {
       if (w == "discrete") i++;
       i++;
@@ -90,7 +99,8 @@ int parse_net_file(const std::string& text, NetSpec& spec, std::string& err) {
       std::string sym = toks[i++].second;
       if (!expect('{')) return NIP_ERROR_IO;
       std::vector<std::string> states;
-      std::string nx;
+      std::string nx, label = " ";
+      int px = 100, py = 100;
       while (i < toks.size() && toks[i].first != '}') {
         std::string key = toks[i++].second;
         if (!expect('=')) return NIP_ERROR_IO;
@@ -105,12 +115,19 @@ int parse_net_file(const std::string& text, NetSpec& spec, std::string& err) {
         if (!expect(';')) return NIP_ERROR_IO;
         if (key == "states") states = vals;
         else if (key == "NIP_next" && !vals.empty()) nx = vals[0];
+        else if (key == "label" && !vals.empty()) label = vals[0];
+        else if (key == "position" && vals.size() == 2) {
+          px = std::abs((int)std::strtod(vals[0].c_str(), nullptr));
+          py = std::abs((int)std::strtod(vals[1].c_str(), nullptr));
+        }
       }
       if (!expect('}')) return NIP_ERROR_IO;
       if (states.empty()) { err = "net parser: the states field is missing (node " + sym + ")"; return NIP_ERROR_IO; }
       spec.symbols.push_back(sym);
       spec.card.push_back((int)states.size());
       spec.states.push_back(states);
+      spec.labels.push_back(label);
+      spec.positions.emplace_back(px, py);
       next_sym.push_back(nx);
     } else if (toks[i].first == 'w' && w == "potential") {
       i++;
