@@ -57,13 +57,14 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 
 #ifndef NIPAMD_MFMA_ABLATE
 #define NIPAMD_MFMA_ABLATE 0       // timing-only builds: 11 no posterior stores, 12 no phase-B loads,
-                                   // 14 no phase-B ll, 15 filter step sums every 4th step only
-#endif
-#ifndef NIPAMD_MFMA_PF
-#define NIPAMD_MFMA_PF 1           // partner prefetch distance in chunks (1 or 2)
+                                   // 14 no phase-B ll, 17 phase-B partners only load,
+                                   // 19 phase-B partners idle
 #endif
 #ifndef NIPAMD_MFMA_DMA
 #define NIPAMD_MFMA_DMA 1          // phase-B prefetch by LDS-DMA when the LDS budget allows
+#endif
+#ifndef NIPAMD_MFMA_RESCALE
+#define NIPAMD_MFMA_RESCALE 4      // phase-A filter rescale interval in steps (1, 2, 4 or 8)
 #endif
 #ifndef NIPAMD_MFMA_NT
 #define NIPAMD_MFMA_NT 0           // 1: non-temporal posterior stores
@@ -72,12 +73,16 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 constexpr int kMSeq = 16;          // sequences per block
 constexpr int kMThreads = 256;     // waves: 0 fwd filter, 1 bwd filter, 2 fwd partner, 3 bwd partner
 constexpr int kMChunk = 8;         // steps per chunk = ring slot
+constexpr int kRescale = NIPAMD_MFMA_RESCALE;
+static_assert(kRescale == 1 || kRescale == 2 || kRescale == 4 || kRescale == 8, "rescale interval");
 constexpr int kMG = kScratchGuard;
 constexpr int kStepD = kMSeq * 16;                 // doubles per step (2 KB)
 constexpr int kSlotD = kMChunk * kStepD;           // doubles per ring slot (16 KB)
 constexpr int kOutD = 2 * 2 * kSlotD;              // rings [dir][slot] (64 KB)
 constexpr int kZD = 2 * kMChunk * kMSeq;           // forward z2 ring [slot][step][chain] (2 KB)
 constexpr int kSStep = kMSeq * 16;                 // doubles per step of a block's scratch
+constexpr int kOBRow = 130;                        // DMA buffer doubles per chain: 1 KB + 16 B, so that
+                                                   // chain c starts 4c banks over (conflict-free reads)
 
 __host__ __device__ inline long block_scratch(int T) { return (long)(T + 2 * kMG) * kSStep; }
 
@@ -204,8 +209,7 @@ __device__ __forceinline__ void barrier_lds(WaitAcc* w = nullptr) {
 
 // LDS-DMA prefetch of the other direction's vectors (phase B).  Sixteen
 // global_load_lds_dwordx4, one per chain c: lane L reads q + 128 B * c and the
-// 1 KB lands lane-linearly at dst + 1 KB * c, where the drain reads it back
-// with the same lane mapping (conflict-free).  No VGPR is written, so the
+// 1 KB lands lane-linearly at dst + kOBRow * 8 B * c.  No VGPR is written, so the
 // compiler has nothing to reorder; the completions are counted by hand with
 // s_waitcnt vmcnt (the DMA is invisible to the compiler's own waits).
 template <int C>
@@ -216,7 +220,7 @@ __device__ __forceinline__ void dma1(const double* q, unsigned lds_base) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(q + C * 16), "s"(lds_base + C * 1024u)
+               : "v"(q + C * 16), "s"(lds_base + C * (kOBRow * 8u))
                : "memory");
 }
 template <int... C>
@@ -252,7 +256,7 @@ struct Chain {
     const v4d keep = FWD ? p : u;
     *reinterpret_cast<double2*>(L + c.wo0) = make_double2(keep.x, keep.y);
     *reinterpret_cast<double2*>(L + c.wo1) = make_double2(keep.z, keep.w);
-    if (NIPAMD_MFMA_ABLATE != 15 || SUM) {
+    if (SUM) {
       const double z2 = chain_sum(p);
       if (FWD && c.zw) *Z = z2;
       sc = -__builtin_amdgcn_frexp_exp(z2);   // frexp exponent of 0 is 0
@@ -263,7 +267,17 @@ struct Chain {
   }
 
   // a phase of n steps from t0 in nch chunks (uniform over the block); all
-  // eight codes and evidence vectors of a chunk are read from LDS up front
+  // eight codes and evidence vectors of a chunk are read from LDS up front.
+  // With fs (phase B, filter stores): chunk ci first takes the posteriors of
+  // chunk ci - 2 out of its ring slot and stores them, two chains per step.
+  // a phase of n steps from t0 in nch chunks (uniform over the block); all
+  // eight codes and evidence vectors of a chunk are read from LDS up front.
+  // SPARSE: full chunks rescale (and publish z2) every kRescale-th step only;
+  // the forward partner sums alpha_t itself (phase A, where the filter bounds
+  // the time and the partner idles).  Between rescales the mass shrinks by
+  // the product of kRescale steps' evidence: exact as long as that product
+  // stays above 2^-1022 (each step's evidence mass above 2^-255 at 4).
+  template <bool SPARSE>
   __device__ __forceinline__ void run(const WaveCtx& c, int n, int nch, int t0, int lane, WaitAcc* w) {
     constexpr int dir = FWD ? 1 : -1;
     for (int ci = 0; ci < nch; ci++) {
@@ -279,7 +293,7 @@ struct Chain {
       if (base + kMChunk <= n) {
 #pragma unroll
         for (int k = 0; k < kMChunk; k++) {
-          if ((k & 3) == 3) step<true>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+          if (!SPARSE || (k & (kRescale - 1)) == kRescale - 1) step<true>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
           else step<false>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
         }
       } else {
@@ -319,14 +333,14 @@ __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c
   }
   WaitAcc wa, wb;
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
-  if (FWD) ch.run(c, H, nchA, 0, lane, &wa);
-  else ch.run(c, T - 1 - H, nchA, T - 2, lane, &wa);
+  if (FWD) ch.template run<true>(c, H, nchA, 0, lane, &wa);
+  else ch.template run<true>(c, T - 1 - H, nchA, T - 2, lane, &wa);
   if (stamps && lane == 0) stamps[blockIdx.x * 4 + 1] = __builtin_readcyclecounter();
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   if (stamps && lane == 0) stamps[blockIdx.x * 4 + 2] = __builtin_readcyclecounter();
   // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
-  if (FWD) ch.run(c, T - H, nchB, H, lane, &wb);
-  else ch.run(c, H, nchB, H - 1, lane, &wb);
+  if (FWD) ch.template run<false>(c, T - H, nchB, H, lane, &wb);
+  else ch.template run<false>(c, H, nchB, H - 1, lane, &wb);
   if (NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
     unsigned long long* st = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 4;
     st[blockIdx.x * 8 + (FWD ? 0 : 1)] = wa.cyc;
@@ -340,93 +354,144 @@ __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c
 // published by the filter, and m1_t = sum(u_t o s) = 2^sc_t * y_{t-1},
 // y_t = alpha_t . w (w = A s, the chain plan's `ts`), sc_t = -exp2(z2_{t-1}),
 // y_{-1} = prior . w.  Products of mantissas with exponents carried apart.
-// Lane: chain q*8 + (L >> 3) for q = 0, 1, piece s = L & 7.
+// Lane L owns chain L & 15 and accumulates steps k = L >> 4 and k + 4 of
+// every chunk, so y is an in-lane dot product; the four partial products of
+// a chain are combined once at the end (write).
 struct LL {
-  double m2[2], m1[2], zmin[2];
-  int e2[2], e1[2];
-  double w0, w1;            // w at this lane's two states
+  double m2, m1, zmin;
+  int e2, e1;
+  double w[16];
 
-  __device__ __forceinline__ void init(const ChainArgs& a, int s) {
-    w0 = a.ts[2 * s]; w1 = a.ts[2 * s + 1];
-    const double ym = sum8(a.pi[2 * s] * w0 + a.pi[2 * s + 1] * w1);   // y_{-1}
+  __device__ __forceinline__ void init(const ChainArgs& a, int lane) {
+    double ym = 0.0;
 #pragma unroll
-    for (int q = 0; q < 2; q++) { m2[q] = 1.0; m1[q] = ym; zmin[q] = 1.0; e2[q] = 0; e1[q] = 0; }
+    for (int i = 0; i < 16; i++) { w[i] = a.ts[i]; ym = __builtin_fma(a.pi[i], w[i], ym); }   // y_{-1}
+    m2 = 1.0; m1 = (lane >> 4) == 0 ? ym : 1.0; zmin = 1.0; e2 = 0; e1 = 0;
   }
-  // step t of chain slot q: y = alpha_t . w (sum8'd), z2 from the filter; last = (t == T-1)
-  __device__ __forceinline__ void step(int q, double y, double z2, bool last, bool renorm) {
-    zmin[q] = __builtin_fmin(zmin[q], z2);
-    m2[q] *= z2;
-    if (!last) { m1[q] *= y; e1[q] -= __builtin_amdgcn_frexp_exp(z2); }   // 2^sc_{t+1}
-    if (renorm) {
-      const int k2 = __builtin_amdgcn_frexp_exp(m2[q]); m2[q] = __builtin_ldexp(m2[q], -k2); e2[q] += k2;
-      const int k1 = __builtin_amdgcn_frexp_exp(m1[q]); m1[q] = __builtin_ldexp(m1[q], -k1); e1[q] += k1;
+  __device__ __forceinline__ double dot(const double (&v)[16]) const {
+    double y0 = v[0] * w[0], y1 = v[1] * w[1], y2 = v[2] * w[2], y3 = v[3] * w[3];
+#pragma unroll
+    for (int i = 4; i < 16; i += 4) {
+      y0 = __builtin_fma(v[i], w[i], y0); y1 = __builtin_fma(v[i + 1], w[i + 1], y1);
+      y2 = __builtin_fma(v[i + 2], w[i + 2], y2); y3 = __builtin_fma(v[i + 3], w[i + 3], y3);
     }
+    return (y0 + y1) + (y2 + y3);
+  }
+  // one step: y = alpha_t . w, z2 = sum(alpha_t); zf = the filter's z2 on
+  // the steps where it rescales (rs), whose exponent is sc_{t+1}; `valid`
+  // masks steps past the phase, last = (t == T-1).  Branch-free.
+  __device__ __forceinline__ void step(double y, double z2, double zf, bool rs, bool valid, bool last) {
+    // factors enter as mantissa and exponent: between two rescales the
+    // filter's vectors (hence z2 and y) may be far below 2^-500
+    const double z = valid ? z2 : 1.0, yy = (valid && !last) ? y : 1.0;
+    zmin = __builtin_fmin(zmin, z);
+    m2 *= __builtin_amdgcn_frexp_mant(z); e2 += __builtin_amdgcn_frexp_exp(z);
+    m1 *= __builtin_amdgcn_frexp_mant(yy); e1 += __builtin_amdgcn_frexp_exp(yy);
+    e1 -= (valid && !last && rs) ? __builtin_amdgcn_frexp_exp(zf) : 0;   // 2^sc_{t+1}
+  }
+  __device__ __forceinline__ static double sum16(const double (&v)[16]) {
+    double s0 = v[0] + v[1], s1 = v[2] + v[3], s2 = v[4] + v[5], s3 = v[6] + v[7];
+    s0 += v[8] + v[9]; s1 += v[10] + v[11]; s2 += v[12] + v[13]; s3 += v[14] + v[15];
+    return (s0 + s1) + (s2 + s3);
+  }
+  __device__ __forceinline__ void renorm() {
+    const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+    const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
   }
   __device__ __forceinline__ void write(const ChainArgs& a, long b0, int lane) {
-    if ((lane & 7) != 0) return;
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const long b = b0 + q * 8 + (lane >> 3);
-      if (b >= a.B) continue;
-      double ll = log(m2[q]) - log(m1[q]) + (double)(e2[q] - e1[q]) * 0.69314718055994530942;
-      const bool dead = zmin[q] == 0.0;
-      if (dead) ll = -DBL_MAX;
-      if (a.ll) a.ll[b] = ll;
-      if (a.status) a.status[b] = dead ? 1u : 0u;
-    }
+    renorm();
+    // combine the chain's four lanes (l, l ^ 32, l ^ 16); every operation is
+    // symmetric, so both lanes of a pair hold identical bits
+    auto pair32 = [](double x, auto f) {
+      const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+      const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+      const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+      return f(__hiloint2double((int)rh[0], (int)rl[0]), __hiloint2double((int)rh[1], (int)rl[1]));
+    };
+    auto pair16 = [](double x, auto f) {
+      const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+      const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+      const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+      return f(__hiloint2double((int)rh[0], (int)rl[0]), __hiloint2double((int)rh[1], (int)rl[1]));
+    };
+    auto mul = [](double x, double y) { return x * y; };
+    auto mn = [](double x, double y) { return __builtin_fmin(x, y); };
+    auto add = [](double x, double y) { return x + y; };
+    double E2 = (double)e2, E1 = (double)e1;     // small integers: exact in a double
+    m2 = pair16(pair32(m2, mul), mul);
+    m1 = pair16(pair32(m1, mul), mul);
+    zmin = pair16(pair32(zmin, mn), mn);
+    E2 = pair16(pair32(E2, add), add);
+    E1 = pair16(pair32(E1, add), add);
+    if (lane >= kMSeq) return;
+    const long b = b0 + lane;
+    if (b >= a.B) return;
+    double ll = log(m2) - log(m1) + (E2 - E1) * 0.69314718055994530942;
+    const bool dead = zmin == 0.0;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 1u : 0u;
   }
 };
 
-// Partner wave of one direction.  Phase A: each step's 2 KB of the block's
-// scratch as two contiguous 1 KB instructions (lane L: chain q*8 + (L >> 3),
-// piece L & 7).  Phase B: for chain q, lane L takes step (L >> 3) of the
-// chunk in ADDRESS order and piece s = L & 7 (states 2s, 2s+1): the ring
-// value times the other direction's vector (scratch, one chunk prefetched),
-// normalised over the 8 lanes of its step, and -- when N == 16 with 16-byte
-// rows -- one contiguous 1 KB posterior run per store instruction.
+// Partner wave of one direction.
+// Phase A: each step's 2 KB of the block's scratch as two contiguous 1 KB
+// instructions (lane L: chain q*8 + (L >> 3), piece L & 7); the forward
+// partner also keeps the ll.
+// Phase B: lane L owns chain c = L & 15 at slot steps k = L >> 4 and k + 4:
+// it reads the whole 16-state ring vector and the other direction's vector
+// (scratch, by LDS-DMA one chunk ahead), forms normalise(alpha o beta) in
+// lane and writes it back over the ring vector; a store pass then sends
+// each chain's 8 steps as one contiguous 1 KB run per instruction (lane
+// L: step L >> 3 in address order, piece L & 7).  Without the 16-state
+// layout (PVEC false) or the LDS-DMA budget, the older 8-lane form is used.
 template <bool FWD, bool PVEC, bool DMA>
-__device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* out, const double* zr,
+__device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, const double* zr,
                                              double* Sblk, double* ob_lds, int lane, long b0, int nchA, int nchB) {
   const int T = a.T, H = a.H;
   const int s = lane & 7, hi = lane >> 3;
+  const int c = lane & 15, kq = lane >> 4;
   constexpr bool pvec = PVEC;        // posterior rows of 16 contiguous, 16-byte aligned doubles
   const int nA = FWD ? H : T - 1 - H, nB = FWD ? T - H : H;
   const int tA = FWD ? 0 : T - 2, tB = FWD ? H : H - 1;
   constexpr int dir = FWD ? 1 : -1;
   const bool st0 = 2 * s < a.N, st1 = 2 * s + 1 < a.N;
-  // phase-B geometry of this lane: slot step k, time offset hi in address order
+  // phase-B geometry of the store lanes: slot step kB, time offset hi in address order
   const int kB = FWD ? hi : kMChunk - 1 - hi;
   auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
 
   LL ll;
-  if (FWD) ll.init(a, s);
-  // forward ll over the chunk's valid steps (chain q*8 + hi, piece s)
-  auto ll_chunk = [&](int ci, int n, int t0) {
+  if (FWD) ll.init(a, lane);
+  // chain c's ring vector at slot step k (16 states, in lane)
+  auto ring_vec = [&](const double* slot, int k, double (&v)[16]) {
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+      const double2 x = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(c, p));
+      v[2 * p] = x.x; v[2 * p + 1] = x.y;
+    }
+  };
+  // forward ll of chunk ci, steps kq and kq + 4: in phase A the filter
+  // rescaled every kRescale-th step of full chunks and at every step of a
+  // partial one (Chain::run<true>), in phase B (dense) at every step; z2 is
+  // summed here
+  auto ll_chunk = [&](int ci, int n, int t0, bool dense) {
     const double* slot = out + (ci & 1) * kSlotD;
     const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
-    const bool full = ci * kMChunk + kMChunk <= n;
-    double y[2 * kMChunk];
-#pragma unroll
-    for (int k = 0; k < kMChunk; k++)
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(q * 8 + hi, s));
-        y[2 * k + q] = v.x * ll.w0 + v.y * ll.w1;
-      }
-    sum8_n(y);
-#pragma unroll
-    for (int k = 0; k < kMChunk; k++) {
-      const int i = ci * kMChunk + k;
-      if (i >= n) break;
-      const bool last = t0 + i == T - 1;
-#pragma unroll
-      for (int q = 0; q < 2; q++)
-        ll.step(q, y[2 * k + q], zs[k * kMSeq + q * 8 + hi], last, !full || (k & 3) == 3);
-    }
+    double v0[16], v1[16];
+    ring_vec(slot, kq, v0);
+    ring_vec(slot, kq + 4, v1);
+    const double za = zs[kq * kMSeq + c], zb = zs[(kq + 4) * kMSeq + c];
+    const int i = ci * kMChunk + kq;
+    const bool all = dense || ci * kMChunk + kMChunk > n;
+    const bool rs0 = all || (kq & (kRescale - 1)) == kRescale - 1;
+    const bool rs1 = all || ((kq + 4) & (kRescale - 1)) == kRescale - 1;
+    ll.step(ll.dot(v0), LL::sum16(v0), za, rs0, i < n, t0 + i == T - 1);
+    ll.step(ll.dot(v1), LL::sum16(v1), zb, rs1, i + 4 < n, t0 + i + 4 == T - 1);
+    ll.renorm();
   };
   auto drainA = [&](int ci) {
     const double* slot = out + (ci & 1) * kSlotD;
-    if (FWD) ll_chunk(ci, nA, tA);
+    if (FWD) ll_chunk(ci, nA, tA, false);
 #pragma unroll
     for (int k = 0; k < kMChunk; k++) {
       const int i = ci * kMChunk + k;
@@ -449,131 +514,162 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* o
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 
-  // other direction's vectors of chunk ci, all 16 chains, this lane's piece
-  v2d oa[kMSeq], ob[kMSeq];
-#if NIPAMD_MFMA_PF == 2
-  v2d oc[kMSeq];
-#endif
-  auto load_other = [&](v2d (&o)[kMSeq], int ci) {
-    const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
-#pragma unroll
-    for (int c = 0; c < kMSeq; c++)
-      o[c] = NIPAMD_MFMA_ABLATE == 12 ? v2d{1.0 + c, 2.0} : *reinterpret_cast<const v2d*>(q + c * 16);
-  };
-  // DMA: buffer k of this partner's two 16 KB LDS buffers
-  const unsigned ob_base = (unsigned)(uintptr_t)ob_lds;
-  auto dma_other = [&](int k, int ci) {
-    const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
-    dma16(q, __builtin_amdgcn_readfirstlane(ob_base + (unsigned)k * (kMSeq * 1024u)),
-          std::make_integer_sequence<int, kMSeq>{});
-  };
-  auto read_other = [&](v2d (&o)[kMSeq], int k) {
-    const double* src = ob_lds + k * (kMSeq * 128) + 2 * lane;
-#pragma unroll
-    for (int c = 0; c < kMSeq; c++) o[c] = *reinterpret_cast<const v2d*>(src + c * 128);
-  };
   // spare scratch rows past the last block: target of masked lanes' stores
   double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
-  auto drainB = [&](int ci, const v2d (&o)[kMSeq]) {
-    if (FWD && NIPAMD_MFMA_ABLATE != 14) ll_chunk(ci, nB, tB);
-    if (!PVEC && !a.post) return;
-    const double* slot = out + (ci & 1) * kSlotD;
-    const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;   // valid steps
-    const bool ok = kB < nk;
-    const int t = tlow(ci) + hi;
-    if constexpr (pvec) {
-      // branch-free, eight chains at a time with their dependency chains interleaved
+  unsigned long long pw = 0, pl = 0, pd = 0;     // NIPAMD_WAIT_TIMES: DMA wait / drain / store cycles
+
+  if constexpr (PVEC && DMA) {
+    // LDS-DMA prefetch of the other direction's vectors: buffer k, chain C at
+    // C * kOBRow doubles, rows = the chunk's 8 steps in address order
+    const unsigned ob_base = (unsigned)(uintptr_t)ob_lds;
+    auto dma_other = [&](int k, int ci) {
+      const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
+      dma16(q, __builtin_amdgcn_readfirstlane(ob_base + (unsigned)k * (kMSeq * kOBRow * 8u)),
+            std::make_integer_sequence<int, kMSeq>{});
+    };
+    // chain c, slot steps kq and kq + 4: posterior in lane, written over the ring vector
+    auto drainV = [&](int ci, int buf) {
+      double* slot = out + (ci & 1) * kSlotD;
+      const double* ob = ob_lds + buf * (kMSeq * kOBRow) + c * kOBRow;
+      const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
 #pragma unroll
-      for (int q0 = 0; q0 < kMSeq; q0 += 8) {
-        double px[8], py[8], z[8], r[8];
+      for (int h = 0; h < 2; h++) {
+        const int k = kq + 4 * h;
+        const int row = FWD ? k : kMChunk - 1 - k;     // DMA row (address order) of slot step k
+        double v[16], o[16];
+        ring_vec(slot, k, v);
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q0 + i, s));
-          px[i] = v.x * o[q0 + i].x; py[i] = v.y * o[q0 + i].y;
-          z[i] = px[i] + py[i];
+        for (int p = 0; p < 8; p++) {
+          const double2 x = *reinterpret_cast<const double2*>(ob + row * 16 + 2 * p);
+          o[2 * p] = x.x; o[2 * p + 1] = x.y;
         }
-        sum8_n(z);
-        recip_n(z, r);                                   // an all-zero row stays zero
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const long bb = b0 + q0 + i;
-#if NIPAMD_MFMA_ABLATE == 13     // timing-only: block-major posterior layout (wrong layout)
-          double* p = (ok && bb < a.B)
-                          ? a.post + ((size_t)(b0 / kMSeq) * a.T + t) * kStepD + (q0 + i) * 16 + 2 * s
-                          : sink;
-#else
-          double* p = (ok && bb < a.B)
-                          ? a.post + (size_t)bb * a.post_bstride + (long)t * 16 + a.post_off + 2 * s
-                          : sink;
-#endif
-#if NIPAMD_MFMA_ABLATE == 11
-          if (px[i] == 12345.0)
-#endif
-#if NIPAMD_MFMA_NT
-          {
-            typedef double v2d __attribute__((ext_vector_type(2)));
-            __builtin_nontemporal_store(v2d{px[i] * r[i], py[i] * r[i]}, reinterpret_cast<v2d*>(p));
-          }
-#else
-          *reinterpret_cast<double2*>(p) = make_double2(px[i] * r[i], py[i] * r[i]);
-#endif
+        if (FWD && NIPAMD_MFMA_ABLATE != 14) {
+          const int i = ci * kMChunk + k;
+          const double zf = zs[k * kMSeq + c];           // phase B: the filter rescales every step
+          ll.step(ll.dot(v), zf, zf, true, i < nB, tB + i == T - 1);
         }
+        double pr[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) pr[i] = v[i] * o[i];
+        double z0 = pr[0] + pr[1], z1 = pr[2] + pr[3], z2 = pr[4] + pr[5], z3 = pr[6] + pr[7];
+        z0 += pr[8] + pr[9]; z1 += pr[10] + pr[11]; z2 += pr[12] + pr[13]; z3 += pr[14] + pr[15];
+        const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
+#pragma unroll
+        for (int p = 0; p < 8; p++)
+          *reinterpret_cast<double2*>(slot + k * kStepD + piece_off(c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
       }
-    } else {
+      if (FWD) ll.renorm();
+    };
+    // chain q's 8 steps as one contiguous 1 KB run per store instruction
+    auto store_pass = [&](int ci) {
+      const double* slot = out + (ci & 1) * kSlotD;
+      const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
+      const bool ok = kB < nk;
+      double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s;
 #pragma unroll
       for (int q = 0; q < kMSeq; q++) {
         const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
-        const double px = v.x * o[q].x, py = v.y * o[q].y;
-        const double r = recip(sum8(px + py));
-        const long bb = b0 + q;
-        if (!ok || bb >= a.B) continue;
-        double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
-        if (st0) p[0] = px * r;
-        if (st1) p[1] = py * r;
-      }
-    }
-  };
-  // chunk ci is drained right after the barrier that ends it, while the
-  // filter computes chunk ci + 1; its inputs were loaded one chunk earlier
-#if NIPAMD_MFMA_PF == 2
-  if (nchB > 0) load_other(oa, 0);
-  if (nchB > 1) load_other(ob, 1);
-  for (int ci = 0; ci < nchB; ci += 3) {
-    if (ci + 2 < nchB) load_other(oc, ci + 2);
-    barrier_lds();
-    drainB(ci, oa);
-    if (ci + 1 >= nchB) break;
-    if (ci + 3 < nchB) load_other(oa, ci + 3);
-    barrier_lds();
-    drainB(ci + 1, ob);
-    if (ci + 2 >= nchB) break;
-    if (ci + 4 < nchB) load_other(ob, ci + 4);
-    barrier_lds();
-    drainB(ci + 2, oc);
-  }
+        double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
+#if NIPAMD_MFMA_ABLATE == 11
+        if (v.x == 12345.0)
+#endif
+#if NIPAMD_MFMA_NT
+        __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
 #else
-  // prefetches are unconditional (an over-run reloads the last chunk) so the
-  // loop body is straight-line code and the compiler's vmcnt waits stay exact
-  if constexpr (DMA) {
+        *reinterpret_cast<double2*>(p) = v;
+#endif
+      }
+    };
     // The phase barrier drained every memory operation.  Before the first
     // drain, chunk 1's sixteen DMAs follow chunk 0's (vmcnt 16); before every
-    // later drain, its DMAs are followed by the previous drain's sixteen
-    // posterior stores and the next chunk's sixteen DMAs (vmcnt 32).  The
-    // counter retires in order; anything extra issued in between only makes a
-    // wait stricter.
+    // later drain, its DMAs are followed by the previous chunk's sixteen
+    // posterior stores and the next chunk's sixteen DMAs (vmcnt 32): the
+    // counter retires loads, stores and DMAs together in issue order.
     const int last = nchB > 0 ? nchB - 1 : 0;
-    dma_other(0, 0);
+    if (NIPAMD_MFMA_ABLATE != 19) dma_other(0, 0);
     for (int ci = 0; ci < nchB; ci++) {
-      dma_other((ci + 1) & 1, ci + 1 < last ? ci + 1 : last);   // over-run reloads the last chunk
+      if (NIPAMD_MFMA_ABLATE != 19)
+        dma_other((ci + 1) & 1, ci + 1 < last ? ci + 1 : last);   // over-run reloads the last chunk
       barrier_lds(&wb);
-      if (ci == 0) wait_vm<16>();
+      const unsigned long long c0 = NIPAMD_WAIT_TIMES ? __builtin_readcyclecounter() : 0;
+      if (NIPAMD_MFMA_ABLATE == 19) {}
+      else if (ci == 0) wait_vm<16>();
       else wait_vm<32>();
-      read_other(oa, ci & 1);
-      drainB(ci, oa);
+      unsigned long long c1 = 0;
+      if (NIPAMD_WAIT_TIMES) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        c1 = __builtin_readcyclecounter();
+        pw += c1 - c0;
+      }
+      if (NIPAMD_MFMA_ABLATE != 17 && NIPAMD_MFMA_ABLATE != 19) {
+        drainV(ci, ci & 1);
+        if (NIPAMD_WAIT_TIMES) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const unsigned long long c2 = __builtin_readcyclecounter();
+          pl += c2 - c1; c1 = c2;
+        }
+        store_pass(ci);
+        if (NIPAMD_WAIT_TIMES) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          pd += __builtin_readcyclecounter() - c1;
+        }
+      }
     }
     wait_vm<0>();                    // no DMA left in flight
   } else {
-    // prefetches are unconditional (an over-run reloads the last chunk)
+    // other direction's vectors of chunk ci, all 16 chains, this lane's piece
+    v2d oa[kMSeq], ob[kMSeq];
+    auto load_other = [&](v2d (&o)[kMSeq], int ci) {
+      const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
+#pragma unroll
+      for (int cc = 0; cc < kMSeq; cc++) o[cc] = *reinterpret_cast<const v2d*>(q + cc * 16);
+    };
+    auto drainB = [&](int ci, const v2d (&o)[kMSeq]) {
+      if (FWD) ll_chunk(ci, nB, tB, true);
+      if (!PVEC && !a.post) return;
+      const double* slot = out + (ci & 1) * kSlotD;
+      const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;   // valid steps
+      const bool ok = kB < nk;
+      const int t = tlow(ci) + hi;
+      if constexpr (pvec) {
+        // branch-free, eight chains at a time with their dependency chains interleaved
+#pragma unroll
+        for (int q0 = 0; q0 < kMSeq; q0 += 8) {
+          double px[8], py[8], z[8], r[8];
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q0 + i, s));
+            px[i] = v.x * o[q0 + i].x; py[i] = v.y * o[q0 + i].y;
+            z[i] = px[i] + py[i];
+          }
+          sum8_n(z);
+          recip_n(z, r);                                 // an all-zero row stays zero
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const long bb = b0 + q0 + i;
+            double* p = (ok && bb < a.B)
+                            ? a.post + (size_t)bb * a.post_bstride + (long)t * 16 + a.post_off + 2 * s
+                            : sink;
+            *reinterpret_cast<double2*>(p) = make_double2(px[i] * r[i], py[i] * r[i]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kMSeq; q++) {
+          const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
+          const double px = v.x * o[q].x, py = v.y * o[q].y;
+          const double r = recip(sum8(px + py));
+          const long bb = b0 + q;
+          if (!ok || bb >= a.B) continue;
+          double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
+          if (st0) p[0] = px * r;
+          if (st1) p[1] = py * r;
+        }
+      }
+    };
+    // chunk ci is drained right after the barrier that ends it, while the
+    // filter computes chunk ci + 1; its inputs were loaded one chunk earlier.
+    // Prefetches are unconditional (an over-run reloads the last chunk).
     const int last = nchB > 0 ? nchB - 1 : 0;
     load_other(oa, 0);
     for (int ci = 0; ci < nchB; ci += 2) {
@@ -586,16 +682,19 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, const double* o
       drainB(ci + 1, ob);
     }
   }
-#endif
   if (FWD) ll.write(a, b0, lane);
   if (NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
     unsigned long long* st = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 4;
     st[blockIdx.x * 8 + 2 + (FWD ? 0 : 1)] = wa.cyc;
     st[blockIdx.x * 8 + 6 + (FWD ? 0 : 1)] = wb.cyc;
+    unsigned long long* pp = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 16;
+    pp[blockIdx.x * 8 + (FWD ? 0 : 4) + 0] = pw;
+    pp[blockIdx.x * 8 + (FWD ? 0 : 4) + 1] = pl;
+    pp[blockIdx.x * 8 + (FWD ? 0 : 4) + 2] = pd;
   }
 }
 
-constexpr int kOBD = 2 * 2 * kMSeq * 128;          // DMA buffers [2 partners][2][16 chains][1 KB] (64 KB)
+constexpr int kOBD = 2 * 2 * kMSeq * kOBRow;       // DMA buffers [2 partners][2][16 chains][1 KB + 16 B pad]
 
 template <bool DMA>
 __global__ __launch_bounds__(kMThreads, 1)
@@ -610,6 +709,12 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * kMSeq;
+  unsigned long long* rts = a.counts ? reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 12
+                                     : nullptr;     // diagnostics: wall-clock stamps
+  if (rts && tid == 0) {
+    rts[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+    rts[blockIdx.x * 4 + 1] = __builtin_readcyclecounter();
+  }
   const int T = a.T;
   const int Tr = chain_codes_row(T);
 
@@ -656,10 +761,10 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   const bool fwd = (wave & 1) == 0;
   double* ring = out + (fwd ? 0 : 2 * kSlotD);
   double* Sblk = a.S + (size_t)blockIdx.x * block_scratch(T) + kMG * kSStep;   // t = 0
+  const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
+                    ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
   if (wave >= 2) {
-    const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
-                      ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
-                      ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
     double* ob = obuf + (fwd ? 0 : kOBD / 2);
     if (pvec) {
       if (fwd) partner_wave<true, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
@@ -667,6 +772,11 @@ void chain_fb_mfma_kernel(ChainArgs a) {
     } else {
       if (fwd) partner_wave<true, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
       else partner_wave<false, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+    }
+    if (rts && fwd && lane == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      rts[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+      rts[blockIdx.x * 4 + 3] = __builtin_readcyclecounter();
     }
     return;
   }
@@ -712,7 +822,7 @@ int launch_mfma(const ChainArgs& a, size_t lds, hipStream_t stream) {
 int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream) {
   const size_t base = (chain_mfma_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
   const size_t with_dma = base + (size_t)kOBD * sizeof(double);
-  if (NIPAMD_MFMA_DMA && NIPAMD_MFMA_PF == 1 && NIPAMD_MFMA_ABLATE != 12 && with_dma <= 160 * 1024)
+  if (NIPAMD_MFMA_DMA && NIPAMD_MFMA_ABLATE != 12 && with_dma <= 160 * 1024)
     return launch_mfma<true>(a, with_dma, stream);
   return launch_mfma<false>(a, base, stream);
 }

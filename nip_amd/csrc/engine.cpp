@@ -8,6 +8,7 @@
 // NIPAMD_ERROR_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -562,15 +563,15 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     unsigned long long* dst = nullptr;
     const int nblk = (int)((B + 15) / 16);
     if (mf && times) {
-      HIP_OK(hipMalloc(&dst, (size_t)nblk * 12 * sizeof(unsigned long long)));
-      HIP_OK(hipMemsetAsync(dst, 0, (size_t)nblk * 12 * sizeof(unsigned long long), (hipStream_t)stream));
+      HIP_OK(hipMalloc(&dst, (size_t)nblk * 24 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(dst, 0, (size_t)nblk * 24 * sizeof(unsigned long long), (hipStream_t)stream));
       a.counts = reinterpret_cast<double*>(dst);
     }
     const int rc = mf ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
                       : nipamd::chain_fb_launch(a, (hipStream_t)stream);
     a.counts = nullptr;
     if (dst) {
-      std::vector<unsigned long long> h((size_t)nblk * 12);
+      std::vector<unsigned long long> h((size_t)nblk * 24);
       HIP_OK(hipStreamSynchronize((hipStream_t)stream));
       HIP_OK(hipMemcpy(h.data(), dst, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
       (void)hipFree(dst);
@@ -589,6 +590,28 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
         std::fprintf(stderr, "[nipamd] barrier wait cycles A/B: fwd filter %.0f/%.0f  bwd filter %.0f/%.0f  "
                      "fwd partner %.0f/%.0f  bwd partner %.0f/%.0f\n", w[0] / nblk, w[4] / nblk, w[1] / nblk,
                      w[5] / nblk, w[2] / nblk, w[6] / nblk, w[3] / nblk, w[7] / nblk);
+      double pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < nblk; k++)
+        for (int i = 0; i < 8; i++) pp[i] += (double)h[(size_t)nblk * 16 + k * 8 + i];
+      if (pp[0] + pp[4] > 0)
+        std::fprintf(stderr, "[nipamd] phase-B partner cycles (DMA wait / ll / drain): fwd %.0f/%.0f/%.0f  "
+                     "bwd %.0f/%.0f/%.0f\n", pp[0] / nblk, pp[1] / nblk, pp[2] / nblk, pp[4] / nblk, pp[5] / nblk,
+                     pp[6] / nblk);
+      // wall-clock view (s_memrealtime, 100 MHz): block entry and partner end
+      const unsigned long long* rt = h.data() + (size_t)nblk * 12;
+      unsigned long long t0 = ~0ull, e0 = 0, e1 = ~0ull, s1 = 0;
+      double mhz = 0, me = 0;
+      for (int k = 0; k < nblk; k++) {
+        t0 = std::min(t0, rt[k * 4 + 0]); s1 = std::max(s1, rt[k * 4 + 0]);
+        e0 = std::max(e0, rt[k * 4 + 2]); e1 = std::min(e1, rt[k * 4 + 2]);
+        me += (double)(rt[k * 4 + 2] - rt[k * 4 + 0]);
+        if (rt[k * 4 + 2] > rt[k * 4 + 0])
+          mhz += 100.0 * (double)(rt[k * 4 + 3] - rt[k * 4 + 1]) / (double)(rt[k * 4 + 2] - rt[k * 4 + 0]);
+      }
+      std::fprintf(stderr, "[nipamd] wall us: last entry %.2f  first end %.2f  last end %.2f  mean block %.2f  "
+                   "clock %.0f MHz; entry->stamp0 cycles %.0f\n", (s1 - t0) / 100.0, (e1 - t0) / 100.0,
+                   (e0 - t0) / 100.0, me / nblk / 100.0, mhz / nblk,
+                   [&] { double x = 0; for (int k = 0; k < nblk; k++) x += (double)(h[k * 4] - rt[k * 4 + 1]); return x / nblk; }());
     }
     if (rc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));

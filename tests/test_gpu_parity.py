@@ -73,6 +73,36 @@ def test_model_net_zero_mass():
     check(m, obs, [m.variable("M1")], [m.variable("P1")])
 
 
+def test_long_sequences_register_prefetch():
+    """T = 2000: the observation codes leave no LDS room for the phase-B
+    LDS-DMA buffers, so the matrix-core kernel prefetches into registers."""
+    nodes, pots = synth.hmm_spec(16, 16, seed=11)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = synth.observations(18, 2000, 16, seed=9)
+    check(m, obs, [m.variable("M1")], [m.variable("P1")])
+
+
+def near_identity(n, eps):
+    d = np.full((n, n), eps)
+    np.fill_diagonal(d, 1.0)
+    return (d / d.sum(axis=1, keepdims=True)).ravel()
+
+
+def test_peaked_model_rescaling():
+    """Near-identity transition (1e-50 off the diagonal) and emission (1e-60):
+    random data makes every step's evidence mass about 1e-50, so the filters'
+    sparse rescaling (every 4th step in phase A) runs at 1e-200 between
+    rescales.  Results must still match the reference's per-step normalisation."""
+    N = 16
+    nodes = [("P0", N, "P1"), ("P1", N, None), ("M1", N, None)]
+    pots = [("M1", ["P1"], near_identity(N, 1e-60)),
+            ("P1", ["P0"], near_identity(N, 1e-50)),
+            ("P0", [], np.full(N, 1.0 / N))]
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = synth.observations(19, 77, N, seed=4)
+    check(m, obs, [m.variable("M1")], [m.variable("P1")])
+
+
 def test_large_batch_properties():
     """Config-2 scale: posteriors normalised, ll finite and <= 0, spot parity."""
     nodes, pots = synth.hmm_spec(16, 16)
