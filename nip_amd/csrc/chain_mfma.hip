@@ -266,12 +266,39 @@ struct Chain {
     X = p;
   }
 
-  // a phase of n steps from t0 in nch chunks (uniform over the block); all
-  // eight codes and evidence vectors of a chunk are read from LDS up front.
-  // With fs (phase B, filter stores): chunk ci first takes the posteriors of
-  // chunk ci - 2 out of its ring slot and stores them, two chains per step.
-  // a phase of n steps from t0 in nch chunks (uniform over the block); all
-  // eight codes and evidence vectors of a chunk are read from LDS up front.
+  // the eight codes and evidence vectors of the chunk starting at step `base`
+  __device__ __forceinline__ void load_chunk(const WaveCtx& c, int t0, int base, v4d (&e)[kMChunk]) {
+    constexpr int dir = FWD ? 1 : -1;
+    int code[kMChunk];
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++) code[k] = c.codes[t0 + dir * (base + k)];   // guards cover over-run
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + code[k] * 16);
+  }
+
+  template <bool SPARSE>
+  __device__ __forceinline__ void chunk(const WaveCtx& c, int n, int ci, int t0, int lane, WaitAcc* w,
+                                        const v4d (&e)[kMChunk], v4d (&en)[kMChunk]) {
+    double* slot = c.out + (ci & 1) * kSlotD;
+    double* zs = FWD ? c.zr + (ci & 1) * kMChunk * kMSeq + (lane & 15) : nullptr;
+    const int base = ci * kMChunk;
+    load_chunk(c, t0, base + kMChunk, en);       // the next chunk's inputs, one chunk ahead
+    if (base + kMChunk <= n) {
+#pragma unroll
+      for (int k = 0; k < kMChunk; k++) {
+        if (!SPARSE || (k & (kRescale - 1)) == kRescale - 1) step<true>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+        else step<false>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kMChunk; k++)
+        if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+    }
+    barrier_lds(w);
+  }
+
+  // a phase of n steps from t0 in nch chunks (uniform over the block); a
+  // chunk's codes and evidence vectors are read from LDS one chunk ahead.
   // SPARSE: full chunks rescale (and publish z2) every kRescale-th step only;
   // the forward partner sums alpha_t itself (phase A, where the filter bounds
   // the time and the partner idles).  Between rescales the mass shrinks by
@@ -279,29 +306,12 @@ struct Chain {
   // stays above 2^-1022 (each step's evidence mass above 2^-255 at 4).
   template <bool SPARSE>
   __device__ __forceinline__ void run(const WaveCtx& c, int n, int nch, int t0, int lane, WaitAcc* w) {
-    constexpr int dir = FWD ? 1 : -1;
-    for (int ci = 0; ci < nch; ci++) {
-      double* slot = c.out + (ci & 1) * kSlotD;
-      double* zs = FWD ? c.zr + (ci & 1) * kMChunk * kMSeq + (lane & 15) : nullptr;
-      const int base = ci * kMChunk;
-      int code[kMChunk];
-#pragma unroll
-      for (int k = 0; k < kMChunk; k++) code[k] = c.codes[t0 + dir * (base + k)];   // guards cover over-run
-      v4d e[kMChunk];
-#pragma unroll
-      for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + code[k] * 16);
-      if (base + kMChunk <= n) {
-#pragma unroll
-        for (int k = 0; k < kMChunk; k++) {
-          if (!SPARSE || (k & (kRescale - 1)) == kRescale - 1) step<true>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
-          else step<false>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kMChunk; k++)
-          if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
-      }
-      barrier_lds(w);
+    v4d ea[kMChunk], eb[kMChunk];
+    if (nch > 0) load_chunk(c, t0, 0, ea);
+    for (int ci = 0; ci < nch; ci += 2) {
+      chunk<SPARSE>(c, n, ci, t0, lane, w, ea, eb);
+      if (ci + 1 >= nch) break;
+      chunk<SPARSE>(c, n, ci + 1, t0, lane, w, eb, ea);
     }
   }
 };
