@@ -111,6 +111,42 @@ size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T);
 // beyond one sink row (S needs >= 64 doubles)
 int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, bool filter_only, hipStream_t stream);
 
+// marginals of the chain's other variables from the interface variable's
+// (derive.hip): the previous-slice copy, a hidden parent, a leaf child
+enum : int { kDerivePrev = 0, kDeriveChild = 1, kDeriveHidden = 2 };
+struct DeriveArgs {
+  int kind;
+  int filter;            // 1: forward_inference marginals (cur = filtered)
+  long B;
+  int T, N;
+  const double* cur;     // the interface variable's marginals [B][T] rows
+  long cur_bstride;
+  int cur_tstride;
+  const double* alpha;   // its filtered marginals (the forward messages); = cur when filtering
+  long al_bstride;
+  int al_tstride;
+  double* out;
+  long out_bstride;
+  int out_tstride;
+  int out_off;
+  const double* A;       // [64][64]
+  const double* pi;      // [64]
+  const int* obs;        // the request's evidence (e_t of filtering)
+  long obs_bstride;
+  int obs_tstride;
+  int ncol;
+  int col[4];
+  int M[4];
+  const double* tab[4];  // [(M+2)][64] per observed column
+  const double* ebase;   // [64]
+  int child_col;         // kDeriveChild: the child's column in obs, or -1
+  int child_M;
+  const double* child_E; // [(M+1)][64]: E, then the row sums
+  int hid_card;          // kDeriveHidden
+  const double* G;       // [card][64][64]
+};
+int derive_launch(const DeriveArgs& a, hipStream_t stream);
+
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block

@@ -704,4 +704,31 @@ void build_chain_plan(Model& m) {
   P.valid = true;
 }
 
+void hidden_table(const Model& m, int j, std::vector<double>& G) {
+  const ChainPlan& P = m.chain;
+  const auto& V = m.vars;
+  const int N = P.N, vp = P.v_prev, vc = P.v_cur, cin = P.c_trans;
+  const int cj = V[P.hidden[j]].card;
+  G.assign((size_t)cj * 64 * 64, 0.0);
+  long hsize = 1;
+  for (int h : P.hidden) hsize *= V[h].card;
+  std::vector<int> val(V.size(), 0), hv(P.hidden.size(), 0);
+  for (long hi = 0; hi < hsize; hi++) {              // the order of build_chain_plan's A64 loop
+    long r = hi;
+    double w = 1.0;
+    for (size_t k = 0; k < P.hidden.size(); k++) {
+      const int c = V[P.hidden[k]].card;
+      hv[k] = (int)(r % c); r /= c;
+      val[P.hidden[k]] = hv[k];
+      w *= V[P.hidden[k]].prior[hv[k]];
+    }
+    double* g = G.data() + (size_t)hv[j] * 64 * 64;
+    for (int x = 0; x < N; x++)
+      for (int y = 0; y < N; y++) {
+        val[vp] = x; val[vc] = y;
+        g[x * 64 + y] += m.cliques[cin].original[clique_index(m, cin, val)] * w;
+      }
+  }
+}
+
 }  // namespace nipamd

@@ -69,6 +69,10 @@ struct DevState {
   double* R = nullptr;     // E-step partial [chain_estep_slab(M)] of nipamd_estep
   double* W = nullptr;     // E-step work: slabs + tree levels + chunk results + partial
   size_t W_bytes = 0;
+  double* Q = nullptr;     // derived marginals: interface marginals / forward messages
+  size_t Q_bytes = 0;
+  std::vector<double*> childE;   // per leaf child [(M+1)][64]: E, then the row sums
+  std::vector<double*> G;        // per hidden parent [card][64][64], built on first use
 };
 
 DevState* dev_of(nipamd_model* mm) {
@@ -85,12 +89,16 @@ void free_tables(DevState* d) {
     (void)hipFree(r.mtab); (void)hipFree(r.wv);
   }
   d->reqs.clear();
+  for (double* p : d->childE) (void)hipFree(p);
+  for (double* p : d->G) (void)hipFree(p);
+  d->childE.clear();
+  d->G.clear();
 }
 
 void dev_release(DevState* d) {
   if (!d) return;
   free_tables(d);
-  (void)hipFree(d->S); (void)hipFree(d->W); (void)hipFree(d->R);
+  (void)hipFree(d->S); (void)hipFree(d->W); (void)hipFree(d->R); (void)hipFree(d->Q);
   *d = DevState();
 }
 
@@ -117,8 +125,25 @@ int ensure_tables(nipamd_model* mm) {
   if (int rc = upload(&d->A64, P.A64)) return rc;
   if (int rc = upload(&d->pi64, P.pi64)) return rc;
   if (int rc = upload(&d->sall64, P.s_all64)) return rc;
+  for (const auto& E : P.emits) {
+    std::vector<double> t(E.E);
+    t.insert(t.end(), E.s.begin(), E.s.end());
+    double* p = nullptr;
+    if (int rc = upload(&p, t)) return rc;
+    d->childE.push_back(p);
+  }
+  d->G.assign(P.hidden.size(), nullptr);
   d->version = mm->version;
   return 0;
+}
+
+// G table of hidden parent j on the device (derived marginals)
+int ensure_hidden(nipamd_model* mm, int j) {
+  DevState* d = dev_of(mm);
+  if (d->G[j]) return 0;
+  std::vector<double> g;
+  nipamd::hidden_table(mm->m, j, g);
+  return upload(&d->G[j], g);
 }
 
 // A request's routing through the chain plan: which emission child each
@@ -237,6 +262,17 @@ int ensure_scratch(nipamd_model* mm, size_t bytes) {
   return 0;
 }
 
+int ensure_q(nipamd_model* mm, size_t bytes) {
+  DevState* d = dev_of(mm);
+  if (d->Q_bytes >= bytes) return 0;
+  (void)hipFree(d->Q);
+  d->Q = nullptr;
+  d->Q_bytes = 0;
+  HIP_OK(hipMalloc(&d->Q, bytes));
+  d->Q_bytes = bytes;
+  return 0;
+}
+
 int ensure_work(nipamd_model* mm, size_t bytes) {
   DevState* d = dev_of(mm);
   if (d->W_bytes >= bytes) return 0;
@@ -275,6 +311,17 @@ bool use_mfma() {
   return v;
 }
 
+// Role of a query variable in the chain plan: 0 the interface variable, 1 its
+// previous-slice copy, 2 + k leaf child k, 1000 + j hidden parent j; -1 none.
+// Every variable of a valid plan has one (build_chain_plan accounts for all).
+int query_kind(const nipamd::ChainPlan& P, int v) {
+  if (v == P.v_cur) return 0;
+  if (v == P.v_prev) return 1;
+  for (size_t k = 0; k < P.emits.size(); k++) if (P.emits[k].var == v) return 2 + (int)k;
+  for (size_t j = 0; j < P.hidden.size(); j++) if (P.hidden[j] == v) return 1000 + (int)j;
+  return -1;
+}
+
 // Which GPU plan (if any) covers this request.
 int route_request(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
                   const int* query, Route& r, std::string& why) {
@@ -298,7 +345,7 @@ int route_request(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_
     r.col[r.ncol] = i; r.emit[r.ncol] = k; r.ncol++;
   }
   for (int i = 0; i < n_query; i++)
-    if (query[i] != P.v_cur) { why = "query variable other than the current-slice interface variable"; return 0; }
+    if (query_kind(P, query[i]) < 0) { why = "query variable outside the chain plan"; return 0; }
   r.narrow = P.N <= 16 && r.ncol <= 1;
   if (r.ncol == 1) { r.primary = r.emit[0]; r.pcol = r.col[0]; }
   else if (!P.emits.empty()) { r.primary = 0; r.pcol = -1; }
@@ -448,24 +495,14 @@ int nipamd_m_step(nipamd_model* mm, const double* params) {
   return rc;
 }
 
-// forward_backward_inference (filt = false) / forward_inference (filt = true)
-static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
-                   int B, int T, int n_query, const int* query, double* d_post,
-                   double* d_ll, uint32_t* d_status, void* stream, bool filt) {
-  if (!mm || B < 0 || T < 1 || (n_obs > 0 && (!d_obs || !obs_vars)) || (n_query > 0 && (!query || !d_post)))
-    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
-  if (B == 0) return 0;
-  Route r;
-  std::string why;
-  if (!route_request(mm, n_obs, obs_vars, n_query, query, r, why))
-    return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+// One launch of the kernel family that serves route r: the interface
+// variable's marginals (smoothed, or filtered) into dst rows (dbs / dts /
+// doff), or only ll / status when dst is null.
+static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, const int32_t* d_obs, int n_obs,
+                      int B, int T, double* dst, long dbs, int dts, int doff,
+                      double* d_ll, uint32_t* d_status, void* stream, bool filt) {
   const auto& P = mm->m.chain;
-  if (int rc = ensure_tables(mm)) return rc;
-  ReqTables* rt = nullptr;
-  if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
   DevState* d = dev_of(mm);
-  int stride = 0;
-  for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
   const long ocols = n_obs > 0 ? n_obs : 1;
   static const bool force_wide = [] {
     const char* e = std::getenv("NIPAMD_FB_KERNEL");
@@ -489,16 +526,11 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     w.tab_rows = rt->mtab_rows; w.tab = rt->mtab;
     w.B = B; w.T = T; w.H = filt ? T : T / 2; w.N = P.N;
     w.A = d->A64; w.pi = d->pi64; w.w = rt->wv; w.S = d->S;
-    w.post = n_query > 0 ? d_post : nullptr;
-    w.post_bstride = (long)T * stride; w.post_tstride = stride;
+    w.post = dst;
+    w.post_bstride = dbs; w.post_tstride = dts; w.post_off = doff;
     w.ll = d_ll; w.status = d_status;
-    const int nq = n_query > 0 ? n_query : 1;
-    for (int q = 0; q < nq; q++) {
-      w.post_off = q * P.N;
-      if (q > 0) { w.ll = nullptr; w.status = nullptr; }
-      if (nipamd::chain_mfma_wide_launch(w, NT, filt, (hipStream_t)stream))
-        return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    }
+    if (nipamd::chain_mfma_wide_launch(w, NT, filt, (hipStream_t)stream))
+      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return 0;
   }
   if (!r.narrow) {
@@ -520,16 +552,11 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     w.ebase = rt->ebase;
     w.B = B; w.T = T; w.H = filt ? 0 : T / 2; w.N = P.N;
     w.A = d->A64; w.pi = d->pi64; w.s = d->sall64; w.S = d->S;
-    w.post = n_query > 0 ? d_post : nullptr;
-    w.post_bstride = (long)T * stride; w.post_tstride = stride;
+    w.post = dst;
+    w.post_bstride = dbs; w.post_tstride = dts; w.post_off = doff;
     w.ll = d_ll; w.status = d_status;
-    const int nq = n_query > 0 ? n_query : 1;
-    for (int q = 0; q < nq; q++) {
-      w.post_off = q * P.N;
-      if (q > 0) { w.ll = nullptr; w.status = nullptr; }
-      if (nipamd::chain_wide_launch(w, (hipStream_t)stream))
-        return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    }
+    if (nipamd::chain_wide_launch(w, (hipStream_t)stream))
+      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return 0;
   }
   const int M0 = rt->M0;
@@ -543,19 +570,13 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
   a.obs_col = r.pcol;
   a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = M0;
   a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
-  a.post = d_post;
-  a.post_bstride = (long)T * stride;
-  a.post_tstride = stride;
-  a.post_off = 0;
+  a.post = dst;
+  a.post_bstride = dbs;
+  a.post_tstride = dts;
+  a.post_off = doff;
   a.ll = d_ll;
   a.status = d_status;
-  if (n_query == 0) { a.post = nullptr; }
-  // query variables all equal the chain variable: one launch per copy keeps
-  // the kernel simple (the common case is exactly one)
-  const int nq = n_query > 0 ? n_query : 1;
-  for (int q = 0; q < nq; q++) {
-    a.post_off = q * P.N;
-    if (q > 0) { a.ll = nullptr; a.status = nullptr; }
+  {
     const bool mf = use_mfma() && nipamd::chain_mfma_lds_bytes(M0, T) <= 160 * 1024;
     // diagnostics: NIPAMD_PHASE_TIMES=1 records per-block phase timestamps
     // (start / end of phase A / start of phase B / end) and prints a summary
@@ -614,6 +635,109 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
                    [&] { double x = 0; for (int k = 0; k < nblk; k++) x += (double)(h[k * 4] - rt[k * 4 + 1]); return x / nblk; }());
     }
     if (rc)
+      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  }
+  return 0;
+}
+
+
+// forward_backward_inference (filt = false) / forward_inference (filt = true).
+// The interface variable's marginals come from the chain kernels; every
+// other queried variable's are derived from them (derive.hip), with the
+// forward messages of a filter pass when a hidden parent is smoothed.
+static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                   int B, int T, int n_query, const int* query, double* d_post,
+                   double* d_ll, uint32_t* d_status, void* stream, bool filt) {
+  if (!mm || B < 0 || T < 1 || (n_obs > 0 && (!d_obs || !obs_vars)) || (n_query > 0 && (!query || !d_post)))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  for (int i = 0; i < n_query; i++)
+    if (query[i] < 0 || query[i] >= (int)mm->m.vars.size()) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad query variable");
+  if (B == 0) return 0;
+  Route r;
+  std::string why;
+  if (!route_request(mm, n_obs, obs_vars, n_query, query, r, why))
+    return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+  const auto& P = mm->m.chain;
+  if (int rc = ensure_tables(mm)) return rc;
+  ReqTables* rt = nullptr;
+  if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
+  std::vector<int> kind(n_query), off(n_query);
+  int stride = 0, first_cur = -1;
+  bool derived = false, fwd_msgs = false;
+  for (int i = 0; i < n_query; i++) {
+    kind[i] = query_kind(P, query[i]);
+    off[i] = stride;
+    stride += mm->m.vars[query[i]].card;
+    if (kind[i] == 0) { if (first_cur < 0) first_cur = i; }
+    else { derived = true; fwd_msgs |= kind[i] >= 1000 && !filt; }
+  }
+  const long pbs = (long)T * stride;
+  const int N = P.N;
+  const size_t per = (size_t)B * T * N;
+  // where the interface marginals live: the first query slot naming the
+  // interface variable, or (derived queries only) the work buffer Q
+  double* cur = nullptr;
+  long cbs = 0;
+  int cts = 0;
+  double* fwd = nullptr;
+  if (derived) {
+    const size_t need = (first_cur < 0 ? per : 0) + (fwd_msgs ? per : 0);
+    if (need) if (int rc = ensure_q(mm, need * sizeof(double))) return rc;
+    double* q = dev_of(mm)->Q;
+    if (first_cur < 0) { cur = q; cbs = (long)T * N; cts = N; q += per; }
+    else { cur = d_post + off[first_cur]; cbs = pbs; cts = stride; }
+    if (fwd_msgs) fwd = q;
+  }
+  bool first = true;
+  for (int i = 0; i < n_query; i++) {
+    if (kind[i] != 0) continue;
+    if (int rc = launch_cur(mm, r, rt, d_obs, n_obs, B, T, d_post, pbs, stride, off[i],
+                            first ? d_ll : nullptr, first ? d_status : nullptr, stream, filt)) return rc;
+    first = false;
+  }
+  if (first)       // no query slot names the interface variable
+    if (int rc = launch_cur(mm, r, rt, d_obs, n_obs, B, T, cur, cbs, cts, 0, d_ll, d_status, stream, filt)) return rc;
+  if (fwd_msgs)    // the forward messages: a filter pass
+    if (int rc = launch_cur(mm, r, rt, d_obs, n_obs, B, T, fwd, (long)T * N, N, 0, nullptr, nullptr, stream, true))
+      return rc;
+  if (!derived) return 0;
+  DevState* d = dev_of(mm);
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  for (int i = 0; i < n_query; i++) {
+    if (kind[i] == 0) continue;
+    nipamd::DeriveArgs g{};
+    g.filter = filt ? 1 : 0;
+    g.B = B; g.T = T; g.N = N;
+    g.cur = cur; g.cur_bstride = cbs; g.cur_tstride = cts;
+    if (fwd) { g.alpha = fwd; g.al_bstride = (long)T * N; g.al_tstride = N; }
+    else { g.alpha = cur; g.al_bstride = cbs; g.al_tstride = cts; }
+    g.out = d_post; g.out_bstride = pbs; g.out_tstride = stride; g.out_off = off[i];
+    g.A = d->A64; g.pi = d->pi64;
+    g.obs = d_obs; g.obs_bstride = (long)T * ocols; g.obs_tstride = (int)ocols;
+    g.ncol = r.ncol;
+    for (int c = 0; c < r.ncol; c++) {
+      g.col[c] = r.col[c];
+      g.M[c] = P.emit(r.emit[c]).M;
+      g.tab[c] = rt->tabw + rt->tabw_off[c];
+    }
+    g.ebase = rt->ebase;
+    g.child_col = -1;
+    if (kind[i] == 1) {
+      g.kind = nipamd::kDerivePrev;
+    } else if (kind[i] < 1000) {
+      const int k = kind[i] - 2;
+      g.kind = nipamd::kDeriveChild;
+      g.child_M = P.emits[k].M;
+      g.child_E = d->childE[k];
+      for (int c = 0; c < r.ncol; c++) if (r.emit[c] == k) g.child_col = r.col[c];
+    } else {
+      const int j = kind[i] - 1000;
+      if (int rc = ensure_hidden(mm, j)) return rc;
+      g.kind = nipamd::kDeriveHidden;
+      g.hid_card = mm->m.vars[P.hidden[j]].card;
+      g.G = d->G[j];
+    }
+    if (nipamd::derive_launch(g, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   }
   return 0;

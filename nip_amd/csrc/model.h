@@ -114,6 +114,9 @@ int compile_graph_only(int n, const std::vector<int>& card,
 std::string model_desc_json(const Model& m);
 int param_size(const Model& m);
 void build_chain_plan(Model& m);
+// [card(h_j)][64][64]: the in-clique folded under the priors over every
+// hidden parent but h_j, at h_j = d (sum_d G[d] = A64); derived marginals
+void hidden_table(const Model& m, int j, std::vector<double>& G);
 int m_step(Model& m, const double* params);
 
 // netfile.cpp

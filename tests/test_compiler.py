@@ -85,7 +85,8 @@ def test_chain_plan_recognition():
     # transition, observed leaf children A1, B1 (SURVEY 8(d) config 3 shape)
     assert d.gpu_supported([d.variable("A1"), d.variable("B1")], [d.variable("C1")])
     assert d.gpu_supported([d.variable("B1")], [d.variable("C1")])
-    assert not d.gpu_supported([d.variable("A1")], [d.variable("D1")])      # query off the chain
+    # every variable of the slice can be queried (derived marginals: prev, hidden parent, children)
+    assert d.gpu_supported([d.variable("A1")], [d.variable(v) for v in ("D1", "C0", "B1", "A1")])
     assert not d.gpu_supported([d.variable("D1")], [d.variable("C1")])      # evidence on a folded parent
     # a slice with two interface variables is not an interface chain
     nodes = [("a0", 2, "a1"), ("b0", 2, "b1"), ("a1", 2, None), ("b1", 2, None), ("o", 2, None)]
