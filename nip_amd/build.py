@@ -39,7 +39,7 @@ def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
     return out
 
 
-TOOLS = ["nipamd_inference", "nipamd_train"]
+TOOLS = ["nipamd_inference", "nipamd_train", "nipamd_map"]
 
 
 def build_tools(verbose: bool = False):

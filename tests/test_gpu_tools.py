@@ -109,3 +109,64 @@ def test_inference_demo1(tmp_path):
     rng = np.random.default_rng(1)
     series = [[[rng.choice(a + ["null"]), "x", rng.choice(b)] for _ in range(T)] for T in (5, 9, 5)]
     check(os.path.join(GOLD, "demo1.net"), ["A1", "junk", "B1"], series, "C1", tmp_path)
+
+
+MAP_TOOL = os.path.join(build.LIB_DIR, "nipamd_map")
+
+
+def check_map(net, header, series, tmp_path):
+    """nipamd_map's output file against nipmap.c restated over the oracle's
+    smoothed marginals of every hidden variable (first strictly greater state
+    from 0, nipmap.c:154-160); a state within 1e-9 of the maximum is a tie
+    either implementation may pick."""
+    m = nip_amd.Model.from_net(net)
+    data, out = str(tmp_path / "data.txt"), str(tmp_path / "map.txt")
+    write_data(data, header, series)
+    r = subprocess.run([MAP_TOOL, net, data, out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    syms = [d["symbol"] for d in m.desc()["vars"]]
+    names = [m.state_names(i) for i in range(m.num_vars)]
+    rs, ov = ref.read_timeseries(data, syms, names)
+    hidden = [v for v in range(m.num_vars) if v not in ov]
+    text = open(out).read()
+    lines = text.split("\n")
+    assert lines[0] == " ".join(syms[v] for v in hidden)
+    orc = PortOracle(m.desc())
+    i = 1
+    for s in rs:
+        post, _ = orc.fb(np.array(s, np.int32).reshape(len(s), len(ov)), ov, hidden)
+        for t in range(len(s)):
+            assert lines[i].endswith(" ")
+            got = lines[i][:-1].split(" ")
+            i += 1
+            off = 0
+            for h, v in enumerate(hidden):
+                row = post[t, off:off + m.card(v)]
+                off += m.card(v)
+                best, mx = 0, 0.0
+                for j, x in enumerate(row):
+                    if x > mx:
+                        best, mx = j, x
+                if got[h] != names[v][best]:
+                    j = names[v].index(got[h])
+                    assert abs(row[j] - row[best]) <= 1e-9, (t, syms[v], got[h], names[v][best], row)
+        assert lines[i] == ""
+        i += 1
+    assert text.endswith("\n\n")
+
+
+def test_map_model_net(tmp_path):
+    """examples/model.net with M1 observed: MAP of P0 (the previous slice) and P1."""
+    rng = np.random.default_rng(12)
+    series = [[[rng.choice(["0", "1", "2", "null"], p=[0.4, 0.3, 0.2, 0.1])] for _ in range(T)]
+              for T in (24, 3, 24, 1, 9)]
+    check_map(os.path.join(GOLD, "model.net"), ["M1"], series, tmp_path)
+
+
+def test_map_demo1_hidden_parent(tmp_path):
+    """demo1.net with A1, B1 observed: MAP of C0, C1 and the hidden parent D1."""
+    m = nip_amd.Model.from_net(os.path.join(GOLD, "demo1.net"))
+    a, b = m.state_names(m.variable("A1")), m.state_names(m.variable("B1"))
+    rng = np.random.default_rng(2)
+    series = [[[rng.choice(a + ["null"]), rng.choice(b)] for _ in range(T)] for T in (6, 6, 11)]
+    check_map(os.path.join(GOLD, "demo1.net"), ["A1", "B1"], series, tmp_path)
