@@ -67,7 +67,7 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #define NIPAMD_MFMA_RESCALE 4      // phase-A filter rescale interval in steps (1, 2, 4 or 8)
 #endif
 #ifndef NIPAMD_MFMA_NT
-#define NIPAMD_MFMA_NT 0           // 1: non-temporal posterior stores
+#define NIPAMD_MFMA_NT 0           // posterior stores: 1 non-temporal, 2 sc1 buffer stores, 3 plain buffer stores
 #endif
 
 constexpr int kMSeq = 16;          // sequences per block
@@ -575,18 +575,36 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
       const double* slot = out + (ci & 1) * kSlotD;
       const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
       const bool ok = kB < nk;
+#if NIPAMD_MFMA_NT >= 2
+      // buffer stores into this block's rows: a masked lane's offset lies past
+      // num_records and the store is dropped; aux 16 = sc1 (write-through)
+      const long nq = a.B - b0 < kMSeq ? a.B - b0 : kMSeq;
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.post + (size_t)b0 * a.post_bstride, (short)0,
+                                                          (int)(nq * a.post_bstride * 8), 0x00020000);
+      const int vbase = (int)(((long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s) * 8);
+#else
       double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s;
+#endif
 #pragma unroll
       for (int q = 0; q < kMSeq; q++) {
         const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
-        double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
 #if NIPAMD_MFMA_ABLATE == 11
         if (v.x == 12345.0)
 #endif
+#if NIPAMD_MFMA_NT >= 2
+        {
+          typedef unsigned v4u __attribute__((ext_vector_type(4)));
+          const int vo = ok ? vbase + (int)(q * a.post_bstride * 8) : (int)0x80000000;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, vo, 0,
+                                                 NIPAMD_MFMA_NT == 2 ? 16 : 0);
+        }
+#else
+        double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
 #if NIPAMD_MFMA_NT
         __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
 #else
         *reinterpret_cast<double2*>(p) = v;
+#endif
 #endif
       }
     };
