@@ -235,6 +235,15 @@ int nipamd_model_state_name(const nipamd_model* m, int var, int state, char* buf
 /* Symbol of variable `var` (nip_variable_symbol, src/nipvariable.c); same
  * buffer convention. */
 int nipamd_model_var_symbol(const nipamd_model* m, int var, char* buf, int cap);
+/* The .net `label` of a variable (v->name, src/nipvariable.h:54); same buffer
+ * convention. */
+int nipamd_model_var_label(const nipamd_model* m, int var, char* buf, int cap);
+/* The rest of a variable record (src/nipvariable.h:51-78) for the nip.h
+ * compat layer: info[9] = {cardinality, next, previous (variable index or
+ * -1), interface_status (NIP_INTERFACE_* bits), pos_x, pos_y, num_of_parents,
+ * model node_size_x, node_size_y}; parents[0..cap) in v->parents order.
+ * Returns num_of_parents, -1 on bad arguments. */
+int nipamd_model_var_info(const nipamd_model* m, int var, int* info, int* parents, int cap);
 
 /*
  * Time-series data files, the reference's text format:
@@ -260,6 +269,31 @@ void nipamd_series_free(nipamd_series* s);
  * variable's card() values at `offset` in each row */
 int nipamd_write_uncertainseries(const nipamd_model* m, const char* path, int var, int n_series,
                                  const int* lengths, const double* post, int stride, int offset);
+
+/*
+ * generate_data (src/nip.c:2325-2478) for B series of
+ * length T on the GPU, for models with an interface-chain plan.  The draws
+ * are the ones the reference makes after random_seed(&seed) (srand) when it
+ * calls generate_data B times in a row (util/nipsample.c:100-110): series b
+ * uses rand() draws [b T nv, (b+1) T nv) of that one stream.
+ *   d_data  int32 [B][T][nv] device, column i = variable order[i]
+ *   order   nipamd_generate_order: the sampling order of nip.c:2343-2375
+ *           (independent variables, then children of drawn parents) =
+ *           time_series->observed of the reference's result; returns nv
+ * nipamd_generate is asynchronous on `stream` once the tables are resident
+ * (the first call per model builds them); _host copies out and synchronises.
+ */
+int nipamd_generate_order(const nipamd_model* m, int* order);
+int nipamd_generate(nipamd_model* m, long seed, int B, int T, int32_t* d_data, void* stream);
+int nipamd_generate_host(nipamd_model* m, long seed, int B, int T, int32_t* data);
+/* Same with the rand() values given ([B][T][nv], what rand() returned, in
+ * draw order): the compat generate_data draws them from the caller's own
+ * rand() stream, whatever state it is in. */
+int nipamd_generate_host_draws(nipamd_model* m, int B, int T, const int32_t* draws, int32_t* data);
+/* The 31-word glibc rand() state window of each of B series that use
+ * draws_per_series draws each after srand(seed): win[b][m] = r[313 + b d + m]
+ * (the next draw is (r[n-31] + r[n-3]) >> 1).  Exposed for tests. */
+int nipamd_rand_windows(long seed, int B, long draws_per_series, uint32_t* win);
 
 #ifdef __cplusplus
 }

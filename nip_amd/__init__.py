@@ -52,6 +52,9 @@ EXPORTS = [
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
     "nipamd_series_data", "nipamd_series_free", "nipamd_write_uncertainseries",
     "nipamd_em_learn", "nipamd_write_model", "nipamd_model_var_symbol",
+    "nipamd_model_var_label", "nipamd_model_var_info",
+    "nipamd_generate_order", "nipamd_generate", "nipamd_generate_host", "nipamd_rand_windows",
+    "nipamd_generate_host_draws",
 ]
 
 
@@ -326,6 +329,41 @@ def forward_backward_inference_host(model: Model, obs, obs_vars, query):
 def forward_inference_host(model: Model, obs, obs_vars, query):
     """forward_inference from host numpy buffers (PCIe-inclusive, synchronous)."""
     return _run_host(lib().nipamd_filter_host, model, obs, obs_vars, query)
+
+
+def generate_order(model: Model):
+    """The sampling order of generate_data (src/nip.c:2343-2375): the model
+    variable of each data column."""
+    L = lib()
+    n = L.nipamd_generate_order(model._h, None)
+    order = (C.c_int * max(n, 1))()
+    L.nipamd_generate_order(model._h, order)
+    return list(order)[:n]
+
+
+def generate_data(model: Model, seed: int, B: int, T: int, out=None, stream=None):
+    """generate_data (src/nip.c:2325-2478) B times from srand(seed), on the
+    GPU: (order, int32 tensor [B][T][nv]); column i holds variable order[i]
+    (the reference's ts->observed)."""
+    import torch
+    order = generate_order(model)
+    if out is None:
+        out = torch.empty((B, T, len(order)), dtype=torch.int32, device="cuda")
+    assert out.dtype == torch.int32 and out.is_cuda and out.is_contiguous()
+    assert tuple(out.shape) == (B, T, len(order))
+    L = lib()
+    L.nipamd_generate.argtypes = [C.c_void_p, C.c_long, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    _check(L.nipamd_generate(model._h, seed, B, T, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return order, out
+
+
+def rand_windows(seed: int, B: int, draws_per_series: int):
+    """glibc rand() state window [B][31] of each series (nipamd_rand_windows)."""
+    out = np.zeros((B, 31), np.uint32)
+    L = lib()
+    L.nipamd_rand_windows.argtypes = [C.c_long, C.c_int, C.c_long, C.c_void_p]
+    _check(L.nipamd_rand_windows(seed, B, draws_per_series, out.ctypes.data_as(C.c_void_p)))
+    return out
 
 
 def read_timeseries(model: Model, path):

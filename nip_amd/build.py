@@ -52,6 +52,37 @@ def build_tools(verbose: bool = False):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
+    build_compat(verbose)
+
+
+COMPAT_LIB = os.path.join(LIB_DIR, "libnip.so")
+# the reference's own command-line programs, compiled unmodified against the
+# compat headers and linked with libnip.so (drop-in check, oracle/_ref is
+# git-ignored; only built where /root/reference exists)
+REF_UTIL = os.environ.get("NIPAMD_REF_UTIL", "/root/reference/util")
+REF_PROGRAMS = ["nipinference", "nipmap", "niptrain", "nipsample"]
+REF_BIN_DIR = os.path.join(ROOT, "oracle", "_ref", "compat")
+
+
+def build_compat(verbose: bool = False):
+    """libnip.so: the reference's nip.h API over the engine (nip_amd/compat)."""
+    inc = ["-I" + os.path.join(ROOT, "include", "compat"), "-I" + os.path.join(ROOT, "include")]
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-fPIC", "-shared", *inc,
+           os.path.join(PKG, "compat", "compat.cpp"), "-L" + LIB_DIR, "-lnip_amd",
+           "-Wl,-rpath,$ORIGIN", "-o", COMPAT_LIB]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    if not os.path.isdir(REF_UTIL):
+        return
+    os.makedirs(REF_BIN_DIR, exist_ok=True)
+    for p in REF_PROGRAMS:
+        cmd = [os.environ.get("CC", "gcc"), "-O2", "-w", *inc, os.path.join(REF_UTIL, p + ".c"),
+               "-L" + LIB_DIR, "-lnip", "-lnip_amd", "-lm", "-Wl,-rpath," + LIB_DIR,
+               "-Wl,-rpath,$ORIGIN/../../../nip_amd/_lib", "-o", os.path.join(REF_BIN_DIR, p)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
 
 
 if __name__ == "__main__":

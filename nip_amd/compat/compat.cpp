@@ -1,0 +1,801 @@
+// libnip.so -- the reference's time-series API (src/nip.h) over the nip_amd
+// GPU engine (the drop-in boundary with the reference's struct
+// layouts).  Declared in include/compat/nip.h.
+//
+// Each nip_model owns an engine handle (nipamd_model) in a side table keyed
+// by the nip_model pointer, so the public struct keeps the reference's layout
+// (nip.h:71-104).  The variable records (nipvariable.h:51-78) are filled from
+// the engine's compiled model.  Inference and learning go to the engine:
+//   forward_inference           -> nipamd_filter_host   (nip.c:1103-1315)
+//   forward_backward_inference  -> nipamd_fb_host       (nip.c:1320-1581)
+//   em_learn                    -> nipamd_em_learn      (nip.c:2076-2243)
+// with the evidence of MARKED observed variables only (insert_ts_step with
+// NIP_MARK_ON, nip.c:982-1003, 1240, 1455, 1816).  There is no CPU path: a
+// request the engine has no GPU plan for fails (NULL / error code) after
+// nip_report_error.
+#include <array>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <unistd.h>
+#include <vector>
+
+#include "nip.h"
+
+namespace {
+
+struct Compat {
+  nip_model_struct pub{};
+  nipamd_model* eng = nullptr;
+  std::vector<nip_variable_struct> vars;
+  std::vector<std::string> symbols, labels;
+  std::vector<std::vector<std::string>> states;
+  std::vector<std::vector<char*>> state_ptrs;
+  std::vector<std::vector<double>> likelihood, prior;
+  std::vector<std::vector<nip_variable>> parents;
+  std::vector<nip_variable> all, next, previous, outgoing, prev_outgoing, incoming, children,
+      independent;
+};
+
+std::unordered_map<const nip_model_struct*, Compat*> g_models;
+
+Compat* lookup(nip_model m) {
+  auto it = g_models.find(m);
+  return it == g_models.end() ? nullptr : it->second;
+}
+
+// model variable index of v (ids are 1.. in declaration order), -1 if v is not
+// one of c's variables
+int index_of(const Compat* c, nip_variable v) {
+  if (!v || v->id < NIP_VAR_MIN_ID || v->id > c->vars.size()) return -1;
+  const int i = (int)v->id - 1;
+  return &c->vars[i] == v ? i : -1;
+}
+
+#define REPORT(e) nip_report_error((char*)__FILE__, __LINE__, (e), 1)
+
+void engine_error(int e) {
+  std::fprintf(stderr, "nip_amd: %s\n", nipamd_last_error());
+  REPORT(e);
+}
+
+void refresh_priors(Compat* c) {
+  for (size_t i = 0; i < c->vars.size(); i++) {
+    if (!c->vars[i].prior) continue;
+    if (nipamd_model_prior(c->eng, (int)i, nullptr) == (int)c->prior[i].size())
+      nipamd_model_prior(c->eng, (int)i, c->prior[i].data());
+  }
+}
+
+// the marked observed columns of a series: (column, model variable)
+void marked_columns(const time_series ts, const Compat* c, std::vector<int>& col,
+                    std::vector<int>& var) {
+  col.clear();
+  var.clear();
+  for (int i = 0; i < ts->num_of_observed; i++) {
+    nip_variable v = ts->observed[i];
+    if (!(NIP_MARK(v) & NIP_MARK_ON)) continue;
+    col.push_back(i);
+    var.push_back(index_of(c, v));
+  }
+}
+
+uncertain_series new_ucs(nip_variable vars[], int nvars, int T) {
+  auto* u = (uncertain_series)std::calloc(1, sizeof(uncertain_series_struct));
+  if (!u) return nullptr;
+  u->num_of_vars = nvars;
+  u->length = T;
+  u->variables = (nip_variable*)std::calloc(nvars > 0 ? nvars : 1, sizeof(nip_variable));
+  u->data = (double***)std::calloc(T > 0 ? T : 1, sizeof(double**));
+  bool ok = u->variables && u->data;
+  if (ok && nvars > 0) std::memcpy(u->variables, vars, (size_t)nvars * sizeof(nip_variable));
+  for (int t = 0; ok && t < T; t++) {
+    u->data[t] = (double**)std::calloc(nvars > 0 ? nvars : 1, sizeof(double*));
+    ok = u->data[t] != nullptr;
+    for (int i = 0; ok && i < nvars; i++)
+      ok = (u->data[t][i] = (double*)std::calloc(NIP_CARDINALITY(vars[i]), sizeof(double))) != nullptr;
+  }
+  if (!ok) {
+    free_uncertainseries(u);
+    return nullptr;
+  }
+  return u;
+}
+
+// n series through the engine, batched by (length, marked columns)
+int run_inference(time_series* ts, int n, nip_variable vars[], int nvars, bool filter,
+                  uncertain_series* out, double* ll) {
+  if (!ts || n < 1 || !out || (nvars > 0 && !vars)) return NIP_ERROR_INVALID_ARGUMENT;
+  for (int s = 0; s < n; s++) out[s] = nullptr;
+  Compat* c = ts[0] ? lookup(ts[0]->model) : nullptr;
+  if (!c) return NIP_ERROR_INVALID_ARGUMENT;
+  std::vector<int> q(nvars), off(nvars);
+  int stride = 0;
+  for (int i = 0; i < nvars; i++) {
+    if ((q[i] = index_of(c, vars[i])) < 0) return NIP_ERROR_INVALID_ARGUMENT;
+    off[i] = stride;
+    stride += NIP_CARDINALITY(vars[i]);
+  }
+  std::map<std::pair<int, std::vector<int>>, std::vector<int>> groups;
+  std::vector<std::vector<int>> cols(n), ovars(n);
+  for (int s = 0; s < n; s++) {
+    if (!ts[s] || ts[s]->model != ts[0]->model || ts[s]->length < 0) return NIP_ERROR_INVALID_ARGUMENT;
+    marked_columns(ts[s], c, cols[s], ovars[s]);
+    groups[{ts[s]->length, ovars[s]}].push_back(s);
+  }
+  int rc = NIP_NO_ERROR;
+  for (const auto& [key, ids] : groups) {
+    const int T = key.first, B = (int)ids.size();
+    const std::vector<int>& ov = key.second;
+    const int k = (int)ov.size();
+    std::vector<double> post((size_t)B * T * (stride > 0 ? stride : 1)), l(B, 0.0);
+    if (T > 0) {
+      std::vector<int32_t> obs((size_t)B * T * (k > 0 ? k : 1), -1);
+      for (int b = 0; b < B; b++) {
+        const time_series x = ts[ids[b]];
+        for (int t = 0; t < T; t++)
+          for (int i = 0; i < k; i++) obs[((size_t)b * T + t) * k + i] = x->data[t][cols[ids[b]][i]];
+      }
+      std::vector<uint32_t> st(B);
+      rc = (filter ? nipamd_filter_host : nipamd_fb_host)(c->eng, obs.data(), k, ov.data(), B, T,
+                                                          nvars, q.data(), post.data(), l.data(),
+                                                          st.data());
+      if (rc != NIP_NO_ERROR) break;
+    }
+    for (int b = 0; b < B; b++) {
+      uncertain_series u = new_ucs(vars, nvars, T);
+      if (!u) {
+        rc = NIP_ERROR_OUTOFMEMORY;
+        break;
+      }
+      const double* p = post.data() + (size_t)b * T * stride;
+      for (int t = 0; t < T; t++)
+        for (int i = 0; i < nvars; i++)
+          std::memcpy(u->data[t][i], p + (size_t)t * stride + off[i],
+                      (size_t)NIP_CARDINALITY(vars[i]) * sizeof(double));
+      out[ids[b]] = u;
+      if (ll) ll[ids[b]] = l[b];
+    }
+    if (rc != NIP_NO_ERROR) break;
+  }
+  if (rc != NIP_NO_ERROR)
+    for (int s = 0; s < n; s++) {
+      free_uncertainseries(out[s]);
+      out[s] = nullptr;
+    }
+  return rc;
+}
+
+std::string desc_json(nipamd_model* e) {
+  const int len = nipamd_model_desc_json(e, nullptr, 0);
+  std::string d((size_t)len + 1, '\0');
+  nipamd_model_desc_json(e, d.data(), len + 1);
+  d.resize(len);
+  return d;
+}
+
+// the integer list starting at the first '[' at or after p
+std::vector<int> ints_at(const std::string& d, size_t p) {
+  std::vector<int> out;
+  p = d.find('[', p) + 1;
+  while (p < d.size() && d[p] != ']') {
+    char* end;
+    out.push_back((int)std::strtol(d.c_str() + p, &end, 10));
+    p = end - d.c_str();
+    if (d[p] == ',') p++;
+  }
+  return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+/* ---- niperrorhandler (src/niperrorhandler.c:27-69) ---- */
+
+static int g_error_counter = 0;
+static int g_error_code = 0;
+
+int nip_report_error(char* srcFile, int line, int error, int verbose) {
+  g_error_code = error;
+  g_error_counter++;
+  if (verbose) {
+    std::fprintf(stderr, "In %s (%d): ", srcFile, line);
+    switch (error) {
+      case 0: std::fprintf(stderr, "O.K.\n"); break;
+      case EFAULT: std::fprintf(stderr, "Nullpointer given.\n"); break;
+      case EDOM: std::fprintf(stderr, "Argument outside the defined domain.\n"); break;
+      case EINVAL: std::fprintf(stderr, "Invalid argument given.\n"); break;
+      case ENOMEM: std::fprintf(stderr, "Failed to allocate memory.\n"); break;
+      case EIO: std::fprintf(stderr, "I/O failure.\n"); break;
+      case ENOENT: std::fprintf(stderr, "Requested file not found.\n"); break;
+      default: std::fprintf(stderr, "Something went wrong.\n");
+    }
+  }
+  return error;
+}
+
+void nip_reset_error_handler(void) { g_error_code = g_error_counter = 0; }
+int nip_check_error_type(void) { return g_error_code; }
+int nip_check_error_counter(void) { return g_error_counter; }
+
+/* ---- double lists (src/niplists.c) ---- */
+
+nip_double_list nip_new_double_list(void) {
+  auto* l = (nip_double_list)std::malloc(sizeof(nip_double_list_struct));
+  if (l) {
+    l->length = 0;
+    l->first = l->last = nullptr;
+  }
+  return l;
+}
+
+int nip_append_double(nip_double_list l, double d) {
+  if (!l) return REPORT(NIP_ERROR_NULLPOINTER);
+  auto* k = (nip_double_link)std::malloc(sizeof(nip_double_link_struct));
+  if (!k) return REPORT(NIP_ERROR_OUTOFMEMORY);
+  k->data = d;
+  k->fwd = nullptr;
+  k->bwd = l->last;
+  if (l->last) l->last->fwd = k; else l->first = k;
+  l->last = k;
+  l->length++;
+  return NIP_NO_ERROR;
+}
+
+int nip_prepend_double(nip_double_list l, double d) {
+  if (!l) return REPORT(NIP_ERROR_NULLPOINTER);
+  auto* k = (nip_double_link)std::malloc(sizeof(nip_double_link_struct));
+  if (!k) return REPORT(NIP_ERROR_OUTOFMEMORY);
+  k->data = d;
+  k->bwd = nullptr;
+  k->fwd = l->first;
+  if (l->first) l->first->bwd = k; else l->last = k;
+  l->first = k;
+  l->length++;
+  return NIP_NO_ERROR;
+}
+
+double* nip_double_list_to_array(nip_double_list l) {
+  if (!l || l->length < 1) return nullptr;
+  auto* a = (double*)std::calloc(l->length, sizeof(double));
+  int i = 0;
+  for (nip_double_link k = l->first; a && k; k = k->fwd) a[i++] = k->data;
+  return a;
+}
+
+void nip_empty_double_list(nip_double_list l) {
+  if (!l) return;
+  for (nip_double_link k = l->first; k;) {
+    nip_double_link n = k->fwd;
+    std::free(k);
+    k = n;
+  }
+  l->first = l->last = nullptr;
+  l->length = 0;
+}
+
+/* ---- variables (src/nipvariable.c:201-315) ---- */
+
+void nip_mark_variable(nip_variable v) { if (v) v->mark = NIP_MARK_ON; }
+void nip_unmark_variable(nip_variable v) { if (v) v->mark = NIP_MARK_OFF; }
+int nip_variable_marked(nip_variable v) { return v ? v->mark != NIP_MARK_OFF : 0; }
+char* nip_variable_symbol(nip_variable v) { return v ? v->symbol : nullptr; }
+
+int nip_variable_state_index(nip_variable v, char* state) {
+  if (!v->state_names) return -1;
+  for (int i = 0; i < v->cardinality; i++)
+    if (std::strcmp(state, v->state_names[i]) == 0) return i;
+  return -1;
+}
+
+char* nip_variable_state_name(nip_variable v, int index) {
+  return v->state_names ? v->state_names[index] : nullptr;
+}
+
+int nip_equal_variables(nip_variable v1, nip_variable v2) { return v1 && v2 ? v1->id == v2->id : 0; }
+
+int nip_number_of_parents(nip_variable v) {
+  if (!v) {
+    nip_report_error((char*)__FILE__, __LINE__, EFAULT, 1);
+    return -1;
+  }
+  return v->num_of_parents;
+}
+
+/* ---- models (src/nip.c:122-508, 1584-1597) ---- */
+
+nip_model parse_model(char* file) {
+  nipamd_model* e = nullptr;
+  if (!file || nipamd_model_from_net(file, &e) != NIP_NO_ERROR) {
+    std::fprintf(stderr, "nip_amd: %s\n", nipamd_last_error());
+    REPORT(NIP_ERROR_GENERAL);
+    return nullptr;
+  }
+  auto* c = new Compat;
+  c->eng = e;
+  const int n = nipamd_model_num_vars(e);
+  c->vars.resize(n);
+  c->symbols.resize(n);
+  c->labels.resize(n);
+  c->states.resize(n);
+  c->state_ptrs.resize(n);
+  c->likelihood.resize(n);
+  c->prior.resize(n);
+  c->parents.resize(n);
+  std::vector<std::array<int, 9>> info(n);
+  std::vector<std::vector<int>> par(n);
+  char buf[4096];
+  for (int i = 0; i < n; i++) {
+    nipamd_model_var_symbol(e, i, buf, sizeof buf);
+    c->symbols[i] = buf;
+    nipamd_model_var_label(e, i, buf, sizeof buf);
+    c->labels[i] = buf;
+    const int np = nipamd_model_var_info(e, i, info[i].data(), nullptr, 0);
+    par[i].resize(np);
+    nipamd_model_var_info(e, i, info[i].data(), par[i].data(), np);
+    const int card = info[i][0];
+    for (int s = 0; s < card; s++) {
+      nipamd_model_state_name(e, i, s, buf, sizeof buf);
+      c->states[i].push_back(buf);
+    }
+    c->likelihood[i].assign(card, 1.0);
+    if (np == 0) {
+      c->prior[i].assign(card, 0.0);  // nip.c:175-180: a missing prior reads as zeros
+      nipamd_model_prior(e, i, c->prior[i].data());
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    nip_variable_struct& v = c->vars[i];
+    v.id = (unsigned long)i + NIP_VAR_MIN_ID;
+    v.symbol = c->symbols[i].data();
+    v.name = c->labels[i].data();
+    v.cardinality = info[i][0];
+    for (auto& s : c->states[i]) c->state_ptrs[i].push_back(s.data());
+    v.state_names = c->state_ptrs[i].data();
+    v.likelihood = c->likelihood[i].data();
+    v.prior = c->prior[i].empty() ? nullptr : c->prior[i].data();
+    v.prior_entered = 0;
+    v.next = info[i][1] >= 0 ? &c->vars[info[i][1]] : nullptr;
+    v.previous = info[i][2] >= 0 ? &c->vars[info[i][2]] : nullptr;
+    for (int p : par[i]) c->parents[i].push_back(&c->vars[p]);
+    v.num_of_parents = (int)par[i].size();
+    v.parents = c->parents[i].empty() ? nullptr : c->parents[i].data();
+    v.family_clique = nullptr;
+    v.family_mapping = nullptr;
+    v.interface_status = info[i][3];
+    v.mark = NIP_MARK_OFF;
+    v.pos_x = info[i][4];
+    v.pos_y = info[i][5];
+    c->all.push_back(&v);
+  }
+  // the special-purpose arrays of nip.c:216-247
+  for (int i = 0; i < n; i++) {
+    nip_variable v = &c->vars[i];
+    if (v->next) {
+      c->next.push_back(v);
+      c->previous.push_back(v->next);
+    }
+    if (v->interface_status & NIP_INTERFACE_INCOMING) c->incoming.push_back(v);
+    if (v->interface_status & NIP_INTERFACE_OLD_OUTGOING) {
+      c->prev_outgoing.push_back(v);
+      c->outgoing.push_back(v->next);
+    }
+    (v->parents ? c->children : c->independent).push_back(v);
+  }
+  nip_model_struct& m = c->pub;
+  const std::string d = desc_json(e);
+  const size_t cs = d.find("\"cliques\":["), ss = d.find("],\"sepsets\"");
+  m.num_of_cliques = 0;
+  for (size_t p = d.find("{\"vars\":", cs); p != std::string::npos && p < ss; p = d.find("{\"vars\":", p + 1))
+    m.num_of_cliques++;
+  m.cliques = nullptr;
+  m.num_of_vars = n;
+  m.variables = c->all.data();
+  m.num_of_nexts = (int)c->next.size();
+  m.next = c->next.data();
+  m.previous = c->previous.data();
+  m.outgoing_interface_size = (int)c->outgoing.size();
+  m.outgoing_interface = c->outgoing.data();
+  m.previous_outgoing_interface = c->prev_outgoing.data();
+  m.incoming_interface_size = (int)c->incoming.size();
+  m.incoming_interface = c->incoming.data();
+  m.in_clique = m.out_clique = nullptr;
+  m.num_of_children = (int)c->children.size();
+  m.children = c->children.data();
+  m.independent = c->independent.data();
+  m.node_size_x = n > 0 ? info[0][7] : 80;
+  m.node_size_y = n > 0 ? info[0][8] : 60;
+  g_models[&c->pub] = c;
+  return &c->pub;
+}
+
+void free_model(nip_model model) {
+  Compat* c = lookup(model);
+  if (!c) return;
+  g_models.erase(model);
+  nipamd_model_free(c->eng);
+  delete c;
+}
+
+int write_model(nip_model model, char* filename) {
+  Compat* c = lookup(model);
+  if (!c || !filename) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  const int e = nipamd_write_model(c->eng, filename);
+  if (e != NIP_NO_ERROR) engine_error(e);
+  return e;
+}
+
+nip_variable model_variable(nip_model model, char* symbol) {
+  if (!model) {
+    REPORT(NIP_ERROR_NULLPOINTER);
+    return nullptr;
+  }
+  for (int i = 0; i < model->num_of_vars; i++)
+    if (std::strcmp(symbol, model->variables[i]->symbol) == 0) return model->variables[i];
+  return nullptr;
+}
+
+// nip.c:2523-2553 prints every clique, then its sepsets in link order; the
+// potentials are device-resident in the engine and are not printed here
+void print_cliques(nip_model model) {
+  Compat* c = lookup(model);
+  if (!c) {
+    REPORT(NIP_ERROR_NULLPOINTER);
+    return;
+  }
+  const std::string d = desc_json(c->eng);
+  const size_t cs = d.find("\"cliques\":["), ss = d.find("],\"sepsets\":["), se = d.find("],\"in_clique\"");
+  std::vector<std::vector<int>> sep;
+  for (size_t p = d.find("{\"a\":", ss); p != std::string::npos && p < se; p = d.find("{\"a\":", p + 1))
+    sep.push_back(ints_at(d, d.find("\"vars\":", p)));
+  std::printf("Cliques of the model:\n");
+  for (size_t p = d.find("{\"vars\":", cs); p != std::string::npos && p < ss; p = d.find("{\"vars\":", p + 1)) {
+    std::printf("clique ");
+    for (int v : ints_at(d, p)) std::printf("%s ", c->symbols[v].c_str());
+    std::printf("\n");
+    for (int s : ints_at(d, d.find("\"links\":", p))) {
+      std::printf("sepset ");
+      for (int v : sep[s]) std::printf("%s ", c->symbols[v].c_str());
+      std::printf("\n");
+    }
+    std::printf("\n");
+  }
+}
+
+/* ---- time series (src/nip.c:512-931) ---- */
+
+int read_timeseries(nip_model model, char* datafile, time_series** results) {
+  Compat* c = lookup(model);
+  if (!c || !datafile || !results) {
+    REPORT(NIP_ERROR_INVALID_ARGUMENT);
+    return 0;
+  }
+  nipamd_series* s = nullptr;
+  if (nipamd_read_timeseries(c->eng, datafile, &s) != NIP_NO_ERROR) {
+    std::fprintf(stderr, "nip_amd: %s\n", nipamd_last_error());
+    REPORT(NIP_ERROR_IO);
+    return 0;
+  }
+  const int N = nipamd_series_count(s), k = nipamd_series_num_observed(s), n = model->num_of_vars;
+  std::vector<int> ov(k > 0 ? k : 1);
+  nipamd_series_observed(s, ov.data());
+  *results = (time_series*)std::calloc(N > 0 ? N : 1, sizeof(time_series));
+  bool ok = *results != nullptr;
+  for (int i = 0; ok && i < N; i++) {
+    auto* ts = (time_series)std::calloc(1, sizeof(time_series_struct));
+    if (!(ok = ts != nullptr)) break;
+    (*results)[i] = ts;
+    ts->model = model;
+    ts->length = nipamd_series_length(s, i);
+    ts->num_of_observed = k;
+    ts->num_of_hidden = n - k;
+    ts->hidden = (nip_variable*)std::calloc(n - k > 0 ? n - k : 1, sizeof(nip_variable));
+    ts->observed = k > 0 ? (nip_variable*)std::calloc(k, sizeof(nip_variable)) : nullptr;
+    if (!(ok = ts->hidden && (k == 0 || ts->observed))) break;
+    int h = 0;
+    for (int v = 0; v < n; v++) {  // nip.c:578-589: model order
+      bool seen = false;
+      for (int j = 0; j < k; j++) seen |= ov[j] == v;
+      if (!seen) ts->hidden[h++] = model->variables[v];
+    }
+    for (int j = 0; j < k; j++) ts->observed[j] = model->variables[ov[j]];
+    if (k > 0) {
+      ts->data = (int**)std::calloc(ts->length > 0 ? ts->length : 1, sizeof(int*));
+      if (!(ok = ts->data != nullptr)) break;
+      const int32_t* d = nipamd_series_data(s, i);
+      for (int t = 0; ok && t < ts->length; t++) {
+        if (!(ok = (ts->data[t] = (int*)std::calloc(k, sizeof(int))) != nullptr)) break;
+        for (int j = 0; j < k; j++) ts->data[t][j] = d[(size_t)t * k + j];
+      }
+    }
+  }
+  nipamd_series_free(s);
+  if (!ok) {
+    REPORT(NIP_ERROR_OUTOFMEMORY);
+    if (*results)
+      for (int i = 0; i < N; i++) free_timeseries((*results)[i]);
+    std::free(*results);
+    *results = nullptr;
+    return 0;
+  }
+  return N;
+}
+
+int write_timeseries(time_series* ts_set, int n_series, char* filename) {
+  if (!(n_series > 0 && ts_set && filename)) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  nip_model model = ts_set[0]->model;
+  for (int n = 1; n < n_series; n++)
+    if (ts_set[n]->model != model) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  // union of the observed variables in first-seen order (nip_variable_union)
+  std::vector<nip_variable> obs;
+  for (int n = 0; n < n_series; n++)
+    for (int i = 0; i < ts_set[n]->num_of_observed; i++) {
+      bool seen = false;
+      for (nip_variable v : obs) seen |= nip_equal_variables(v, ts_set[n]->observed[i]) != 0;
+      if (!seen) obs.push_back(ts_set[n]->observed[i]);
+    }
+  if (obs.empty()) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  FILE* f = std::fopen(filename, "w");
+  if (!f) return REPORT(NIP_ERROR_IO);
+  for (size_t i = 0; i < obs.size(); i++) {
+    if (i) std::fprintf(f, "%c", NIP_FIELD_SEPARATOR);
+    std::fprintf(f, "%s", nip_variable_symbol(obs[i]));
+  }
+  std::fputs("\n", f);
+  std::vector<int> rec(obs.size()), map;
+  for (int n = 0; n < n_series; n++) {
+    const time_series ts = ts_set[n];
+    map.assign(ts->num_of_observed, 0);
+    for (int i = 0; i < ts->num_of_observed; i++)
+      for (size_t j = 0; j < obs.size(); j++)
+        if (nip_equal_variables(obs[j], ts->observed[i])) map[i] = (int)j;
+    for (int t = 0; t < ts->length; t++) {
+      std::fill(rec.begin(), rec.end(), -1);
+      for (int i = 0; i < ts->num_of_observed; i++) rec[map[i]] = ts->data[t][i];
+      for (size_t i = 0; i < obs.size(); i++) {
+        if (i) std::fprintf(f, "%c", NIP_FIELD_SEPARATOR);
+        if (rec[i] >= 0) std::fprintf(f, "%s", nip_variable_state_name(obs[i], rec[i]));
+        else std::fputs("null", f);
+      }
+      std::fputs("\n", f);
+    }
+    std::fputs("\n", f);
+  }
+  if (std::fclose(f)) return REPORT(NIP_ERROR_IO);
+  return NIP_NO_ERROR;
+}
+
+void free_timeseries(time_series ts) {
+  if (!ts) return;
+  if (ts->data) {
+    for (int t = 0; t < ts->length; t++) std::free(ts->data[t]);
+    std::free(ts->data);
+  }
+  std::free(ts->hidden);
+  std::free(ts->observed);
+  std::free(ts);
+}
+
+int timeseries_length(time_series ts) { return ts ? ts->length : 0; }
+
+char* get_observation(time_series ts, nip_variable v, int time) {
+  int j = -1;
+  for (int i = 0; i < ts->model->num_of_vars - ts->num_of_hidden; i++)
+    if (nip_equal_variables(v, ts->observed[i])) j = i;
+  if (j < 0 || time < 0 || ts->length <= time) return nullptr;
+  return v->state_names[ts->data[time][j]];
+}
+
+int set_observation(time_series ts, nip_variable v, int time, char* observation) {
+  int j = -1;
+  for (int i = 0; i < ts->model->num_of_vars - ts->num_of_hidden; i++)
+    if (nip_equal_variables(v, ts->observed[i])) j = i;
+  const int i = nip_variable_state_index(v, observation);
+  if (j < 0 || i < 0) return NIP_ERROR_INVALID_ARGUMENT;
+  ts->data[time][j] = i;
+  return 0;
+}
+
+int write_uncertainseries(uncertain_series* ucs_set, int n_series, nip_variable v, char* filename) {
+  const int n = v ? NIP_CARDINALITY(v) : 0;
+  if (!(n > 0 && ucs_set && filename && n_series > 0)) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  std::vector<int> vi(n_series, -1);
+  for (int s = 0; s < n_series; s++) {
+    for (int i = 0; i < ucs_set[s]->num_of_vars; i++)
+      if (nip_equal_variables(v, ucs_set[s]->variables[i])) {
+        vi[s] = i;
+        break;
+      }
+    if (vi[s] < 0) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  }
+  FILE* f = std::fopen(filename, "w");
+  if (!f) return REPORT(NIP_ERROR_IO);
+  for (int i = 0; i < n; i++) {
+    if (i) std::fprintf(f, "%c", NIP_FIELD_SEPARATOR);
+    std::fprintf(f, "%s", nip_variable_state_name(v, i));
+  }
+  std::fputs("\n", f);
+  for (int s = 0; s < n_series; s++) {
+    const uncertain_series u = ucs_set[s];
+    for (int t = 0; t < u->length; t++) {
+      for (int i = 0; i < n; i++) {
+        if (i) std::fprintf(f, "%c", NIP_FIELD_SEPARATOR);
+        std::fprintf(f, "%f", u->data[t][vi[s]][i]);
+      }
+      std::fputs("\n", f);
+    }
+    std::fputs("\n", f);
+  }
+  if (std::fclose(f)) return REPORT(NIP_ERROR_IO);
+  return NIP_NO_ERROR;
+}
+
+void free_uncertainseries(uncertain_series ucs) {
+  if (!ucs) return;
+  if (ucs->data) {
+    for (int t = 0; t < ucs->length; t++) {
+      if (!ucs->data[t]) continue;
+      for (int i = 0; i < ucs->num_of_vars; i++) std::free(ucs->data[t][i]);
+      std::free(ucs->data[t]);
+    }
+    std::free(ucs->data);
+  }
+  std::free(ucs->variables);
+  std::free(ucs);
+}
+
+int uncertainseries_length(uncertain_series ucs) { return ucs ? ucs->length : 0; }
+
+/* ---- inference and learning on the engine ---- */
+
+uncertain_series forward_inference(time_series ts, nip_variable vars[], int nvars,
+                                   double* loglikelihood) {
+  uncertain_series u = nullptr;
+  const int e = run_inference(&ts, 1, vars, nvars, true, &u, loglikelihood);
+  if (e != NIP_NO_ERROR) engine_error(e);
+  return u;
+}
+
+uncertain_series forward_backward_inference(time_series ts, nip_variable vars[], int nvars,
+                                            double* loglikelihood) {
+  uncertain_series u = nullptr;
+  const int e = run_inference(&ts, 1, vars, nvars, false, &u, loglikelihood);
+  if (e != NIP_NO_ERROR) engine_error(e);
+  return u;
+}
+
+int forward_backward_inference_batch(time_series* ts, int n_ts, nip_variable vars[], int nvars,
+                                     uncertain_series* ucs_out, double* ll_out) {
+  const int e = run_inference(ts, n_ts, vars, nvars, false, ucs_out, ll_out);
+  if (e != NIP_NO_ERROR) engine_error(e);
+  return e;
+}
+
+int em_learn(time_series* ts, int n_ts, double threshold, nip_double_list learning_curve) {
+  if (!ts || n_ts < 1 || !ts[0] || !ts[0]->model) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  Compat* c = lookup(ts[0]->model);
+  if (!c) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  if (learning_curve && NIP_LIST_LENGTH(learning_curve) > 0) nip_empty_double_list(learning_curve);
+  std::vector<int> col, var, ov;
+  marked_columns(ts[0], c, col, ov);
+  std::vector<int> lengths(n_ts);
+  size_t total = 0;
+  for (int s = 0; s < n_ts; s++) {
+    if (!ts[s] || ts[s]->model != ts[0]->model) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+    marked_columns(ts[s], c, col, var);
+    if (var != ov) {
+      std::fprintf(stderr, "nip_amd: em_learn needs the same observed variables in every series\n");
+      return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+    }
+    total += (size_t)(lengths[s] = ts[s]->length);
+  }
+  const int k = (int)ov.size();
+  std::vector<int32_t> obs(total * (k > 0 ? k : 1) + 1, -1);
+  size_t r = 0;
+  for (int s = 0; s < n_ts; s++) {
+    marked_columns(ts[s], c, col, var);
+    for (int t = 0; t < ts[s]->length; t++, r++)
+      for (int i = 0; i < k; i++) obs[r * k + i] = ts[s]->data[t][col[i]];
+  }
+  std::vector<double> curve(1 << 16);
+  int curve_len = 0;
+  const int e = nipamd_em_learn(c->eng, n_ts, lengths.data(), obs.data(), k, ov.data(), threshold,
+                                nullptr, 0, curve.data(), (int)curve.size(), &curve_len);
+  refresh_priors(c);
+  if (e != NIP_NO_ERROR && e != NIP_ERROR_BAD_LUCK) {
+    engine_error(e);
+    return e;
+  }
+  // on BAD_LUCK the curve so far stays (nip.c:2192-2198)
+  for (int i = 0; learning_curve && i < curve_len && i < (int)curve.size(); i++) {
+    const int a = nip_append_double(learning_curve, curve[i]);
+    if (a != NIP_NO_ERROR) return a;
+  }
+  return e;
+}
+
+/* generate_data (src/nip.c:2325-2478) on the engine: the rand() draws come
+ * from the caller's own stream, one per variable per step in sampling order,
+ * exactly as the reference consumes them; the sampling is the GPU's.  The
+ * result's observed variables are the sampling order (nip.c:2384-2389) and
+ * every variable ends up marked (nip.c:2343-2375). */
+time_series generate_data(nip_model model, int length) {
+  Compat* c = lookup(model);
+  if (!c || length < 0) {
+    REPORT(NIP_ERROR_INVALID_ARGUMENT);
+    return nullptr;
+  }
+  const int nv = nipamd_generate_order(c->eng, nullptr);
+  std::vector<int> order(nv > 0 ? nv : 1);
+  nipamd_generate_order(c->eng, order.data());
+  std::vector<int32_t> draws((size_t)length * nv + 1), out((size_t)length * nv + 1);
+  for (size_t i = 0; i + 1 < draws.size(); i++) draws[i] = std::rand();
+  const int e = nipamd_generate_host_draws(c->eng, 1, length, draws.data(), out.data());
+  if (e != NIP_NO_ERROR) {
+    engine_error(e);
+    return nullptr;
+  }
+  for (int i = 0; i < model->num_of_vars; i++) nip_mark_variable(model->variables[i]);
+  auto* ts = (time_series)std::calloc(1, sizeof(time_series_struct));
+  if (!ts) {
+    REPORT(NIP_ERROR_OUTOFMEMORY);
+    return nullptr;
+  }
+  ts->model = model;
+  ts->hidden = nullptr;
+  ts->num_of_hidden = model->num_of_vars - nv;
+  ts->num_of_observed = nv;
+  ts->length = length;
+  ts->observed = (nip_variable*)std::calloc(nv > 0 ? nv : 1, sizeof(nip_variable));
+  ts->data = (int**)std::calloc(length > 0 ? length : 1, sizeof(int*));
+  bool ok = ts->observed && ts->data;
+  for (int i = 0; ok && i < nv; i++) ts->observed[i] = model->variables[order[i]];
+  for (int t = 0; ok && t < length; t++) {
+    ok = (ts->data[t] = (int*)std::calloc(nv > 0 ? nv : 1, sizeof(int))) != nullptr;
+    for (int i = 0; ok && i < nv; i++) ts->data[t][i] = out[(size_t)t * nv + i];
+  }
+  if (!ok) {
+    REPORT(NIP_ERROR_OUTOFMEMORY);
+    free_timeseries(ts);
+    return nullptr;
+  }
+  return ts;
+}
+
+/* ---- random numbers (src/nip.c:2482-2520) ---- */
+
+long random_seed(long* seedpointer) {
+  long seed;
+  if (!seedpointer) {
+    const time_t now = std::time(nullptr);
+    const struct tm* tp = std::localtime(&now);
+    seed = tp->tm_sec + 60 * tp->tm_min + 3600 * tp->tm_hour;
+    seed ^= (getpid() + (getpid() << 15));
+  } else {
+    seed = *seedpointer;
+  }
+  std::srand((unsigned)seed);
+  return seed;
+}
+
+int lottery(double* distribution, int size) {
+  int i = 0;
+  double sum = 0;
+  const double r = std::rand() / (double)RAND_MAX;
+  do {
+    if (i >= size) {
+      REPORT(NIP_ERROR_INVALID_ARGUMENT);
+      return size - 1;
+    }
+    sum += distribution[i++];
+  } while (sum < r);
+  return i - 1;
+}
+
+}  // extern "C"

@@ -147,6 +147,33 @@ struct DeriveArgs {
 };
 int derive_launch(const DeriveArgs& a, hipStream_t stream);
 
+// generate_data (generate.hip): one sampling step per variable, in sampling
+// order.  In the first slice the conditional row of step i starts at
+// tab[off0 + idx], idx = sum_c value(ctx[c]) * stride[c] (in elements) with
+// value(j) = this slice's draw of step j (j >= 0) or the previous slice's
+// draw of the interface variable (j = -1); later slices use off1 / ctx1 /
+// stride1.
+constexpr int kGenMaxCtx = 6;
+constexpr int kGenMaxVars = 64;
+struct GenStep {
+  int card = 0;
+  int nctx = 0, nctx1 = 0;
+  long off0 = 0, off1 = 0;
+  int ctx[kGenMaxCtx] = {}, ctx1[kGenMaxCtx] = {};
+  long stride[kGenMaxCtx] = {}, stride1[kGenMaxCtx] = {};
+};
+struct GenArgs {
+  int B = 0, T = 0, nv = 0;
+  int x1_step = 0;                  // the step drawing the interface variable
+  const GenStep* steps = nullptr;   // [nv] device
+  const double* tab = nullptr;      // device tables
+  long zero_off = 0;                // an all-zero row (>= every card)
+  const uint32_t* win = nullptr;    // [B][31] rand() state of each series
+  const int* draws = nullptr;       // or the rand() values themselves, [B][T][nv]
+  int* out = nullptr;               // [B][T][nv] draws, sampling-order columns
+};
+int generate_launch(const GenArgs& a, hipStream_t stream);
+
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block

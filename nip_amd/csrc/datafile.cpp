@@ -206,4 +206,30 @@ int nipamd_model_state_name(const nipamd_model* mm, int var, int state, char* bu
   return (int)n.size();
 }
 
+int nipamd_model_var_label(const nipamd_model* mm, int var, char* buf, int cap) {
+  if (!mm || var < 0 || var >= (int)mm->m.vars.size()) return -1;
+  const std::string& n = mm->m.vars[var].label;
+  if (buf && cap > 0) {
+    std::strncpy(buf, n.c_str(), (size_t)cap - 1);
+    buf[cap - 1] = '\0';
+  }
+  return (int)n.size();
+}
+
+int nipamd_model_var_info(const nipamd_model* mm, int var, int* info, int* parents, int cap) {
+  if (!mm || var < 0 || var >= (int)mm->m.vars.size() || !info) return -1;
+  const auto& v = mm->m.vars[var];
+  info[0] = v.card;
+  info[1] = v.next;
+  info[2] = v.previous;
+  info[3] = v.ifs;
+  info[4] = v.pos_x;
+  info[5] = v.pos_y;
+  info[6] = (int)v.parents.size();
+  info[7] = mm->m.node_size_x;
+  info[8] = mm->m.node_size_y;
+  for (int i = 0; parents && i < (int)v.parents.size() && i < cap; i++) parents[i] = v.parents[i];
+  return (int)v.parents.size();
+}
+
 }  // extern "C"

@@ -413,6 +413,7 @@ int nipamd_model_from_net(const char* path, nipamd_model** out) {
 
 void nipamd_model_free(nipamd_model* mm) {
   if (!mm) return;
+  nipamd::generate_release(mm);
   DevState* d = static_cast<DevState*>(mm->m.dev);
   dev_release(d);
   delete d;

@@ -133,3 +133,8 @@ struct nipamd_model {
   nipamd::Model m;
   unsigned version = 1;          // bumped whenever the tables change
 };
+
+namespace nipamd {
+// generate.cpp: drop a model's cached generate_data tables (nipamd_model_free)
+void generate_release(const nipamd_model* mm);
+}  // namespace nipamd

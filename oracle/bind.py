@@ -330,6 +330,17 @@ class RefHarness:
         n = self.lib().nh_prior(self.h, v, out)
         return out if n else None
 
+    def generate(self, seed, n_series, T):
+        """generate_data (nip.c:2325-2478) n_series times from srand(seed):
+        (order [nv], data [n_series][T][nv] in sampling-order columns)."""
+        nv = len(self._cards)
+        order = np.zeros(nv, np.int32)
+        data = np.zeros((n_series, T, nv), np.int32)
+        L = self.lib()
+        L.nh_generate.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, _i32p, _i32p]
+        L.nh_generate(self.h, seed, n_series, T, order, data.reshape(-1))
+        return order, data
+
 
 def ref_graph_cliques(card, edges, set_parents=True):
     """Cliques of a DAG through the reference's own triangulation."""

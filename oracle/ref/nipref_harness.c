@@ -794,6 +794,77 @@ int nh_prior(int h, int v, double* out){
   return var->cardinality;
 }
 
+/* lottery, src/nip.c:2507-2520 */
+static int h_lottery(const double* d, int size){
+  int i = 0;
+  double sum = 0;
+  double r = rand() / (double)RAND_MAX;
+  do{
+    if(i >= size) return size - 1;
+    sum += d[i++];
+  } while(sum < r);
+  return i - 1;
+}
+
+/*
+ * generate_data, restated from src/nip.c:2325-2478, for n_series series of
+ * length T drawn one after the other from one rand() stream seeded with
+ * srand(seed) (random_seed(&seed), nip.c:2482-2502, then generate_data per
+ * series as a sampling program would).  order[nv]: the sampling order
+ * (independent variables first, then children whose parents are all drawn,
+ * nip.c:2343-2375) = the column order of data[n_series][T][nv].
+ */
+int nh_generate(int h, long seed, int n_series, int T, int* order, int* data){
+  nh_model* m = nh_models[h];
+  int nv = m->num_of_vars, i, j, k, t, s, ok;
+  char* mark = (char*) calloc(nv, 1);
+  double* dist;
+  nip_potential* alpha;
+  int maxc = 1;
+  j = 0;
+  for(i = 0; i < nv; i++)
+    if(m->variables[i]->num_of_parents == 0){ order[j++] = i; mark[i] = 1; }
+  while(j < nv){
+    for(i = 0; i < nv; i++){
+      nip_variable v = m->variables[i];
+      if(mark[i]) continue;
+      ok = 1;
+      for(k = 0; k < v->num_of_parents; k++)
+        if(!mark[nh_var_index(m, v->parents[k])]){ ok = 0; break; }
+      if(ok){ order[j++] = i; mark[i] = 1; }
+    }
+  }
+  free(mark);
+  for(i = 0; i < nv; i++)
+    if(NIP_CARDINALITY(m->variables[i]) > maxc) maxc = NIP_CARDINALITY(m->variables[i]);
+  dist = (double*) calloc(maxc, sizeof(double));
+  alpha = h_alloc_ag(m, 0);
+  srand((unsigned)seed);
+  for(s = 0; s < n_series; s++){
+    int* d = data + (size_t)s * T * nv;
+    h_reset_model(m);
+    h_use_priors(m, 0);
+    for(t = 0; t < T; t++){
+      if(t > 0) h_finish_pass(m, 1, alpha[0], NULL);
+      for(i = 0; i < nv; i++){
+        h_make_consistent(m);
+        h_write_result(m, order[i], dist);
+        k = h_lottery(dist, NIP_CARDINALITY(m->variables[order[i]]));
+        d[(size_t)t * nv + i] = k;
+        nip_enter_index_observation(m->variables, m->num_of_vars, m->cliques,
+                                    m->num_of_cliques, m->variables[order[i]], k);
+      }
+      h_make_consistent(m);
+      h_start_pass(m, 1, alpha[0]);
+      h_reset_model(m);
+      h_use_priors(m, 1);
+    }
+  }
+  h_free_ag(alpha, 0);
+  free(dist);
+  return nv;
+}
+
 /*
  * Cliques of an explicit graph through the reference's own triangulation
  * (nip_moralise_graph, nip_make_graph_undirected, nip_triangulate_graph --

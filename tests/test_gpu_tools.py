@@ -36,8 +36,8 @@ def write_data(path, header, series):
             f.write("\n")
 
 
-def run_tool(net, data, var, out):
-    r = subprocess.run([TOOL, net, data, var, out], capture_output=True, text=True, timeout=120)
+def run_tool(net, data, var, out, tool=TOOL):
+    r = subprocess.run([tool, net, data, var, out], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     m = re.search(r"Average log\. likelihood = (\S+)", r.stdout)
     return float(m.group(1))
@@ -57,11 +57,11 @@ def parse_output(path):
     return header, blocks
 
 
-def check(net, header, series, var, tmp_path):
+def check(net, header, series, var, tmp_path, tool=TOOL):
     m = nip_amd.Model.from_net(net)
     data, out = str(tmp_path / "data.txt"), str(tmp_path / "post.txt")
     write_data(data, header, series)
-    avg = run_tool(net, data, var, out)
+    avg = run_tool(net, data, var, out, tool)
     got_header, blocks = parse_output(out)
     v = m.variable(var)
     assert got_header == m.state_names(v)
@@ -114,7 +114,7 @@ def test_inference_demo1(tmp_path):
 MAP_TOOL = os.path.join(build.LIB_DIR, "nipamd_map")
 
 
-def check_map(net, header, series, tmp_path):
+def check_map(net, header, series, tmp_path, tool=MAP_TOOL):
     """nipamd_map's output file against nipmap.c restated over the oracle's
     smoothed marginals of every hidden variable (first strictly greater state
     from 0, nipmap.c:154-160); a state within 1e-9 of the maximum is a tie
@@ -122,7 +122,7 @@ def check_map(net, header, series, tmp_path):
     m = nip_amd.Model.from_net(net)
     data, out = str(tmp_path / "data.txt"), str(tmp_path / "map.txt")
     write_data(data, header, series)
-    r = subprocess.run([MAP_TOOL, net, data, out], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([tool, net, data, out], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     syms = [d["symbol"] for d in m.desc()["vars"]]
     names = [m.state_names(i) for i in range(m.num_vars)]
