@@ -46,7 +46,28 @@ WORKLOADS = {
     "estep": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024),
     "config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256),
     "config5": ("config5", lambda a: synth.wide_spec(64, 16), ["O1"], "X1", 256, 128),
+    "generate": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 65536, 1024),
 }
+
+
+def cpu_baseline_generate(nodes, pots, T, budget_s: float = 12.0):
+    """The reference's generate_data (oracle/_ref harness: nip.c's sampling
+    loop over the reference's own join-tree code) on this host, one core,
+    series of the bench length until the budget is spent."""
+    from oracle import bind
+    orc = bind.RefHarness(synth.spec_to_replay(nodes, pots), cards=[n[1] for n in nodes])
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        orc.generate(12345 + n, 1, T)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": n * T / el, "unit": "sequence-timesteps/s", "cores": 1, "kind": "reference",
+            "sample": "%d series x T=%d, generate_data (nip.c:2325-2478 loop over the reference's "
+                      "nippotential/nipjointree code compiled from /root/reference sources), gcc -O2, "
+                      "%.1f s" % (n, T, el)}
 
 
 def cpu_baseline(nodes, pots, obs, ov, q, budget_s: float = 12.0, t_sample: int = 0):
@@ -135,7 +156,14 @@ def main():
     obs = torch.from_numpy(obs_np).to(dev)
     ll = torch.empty((B,), dtype=torch.float64, device=dev)
     st = torch.empty((B,), dtype=torch.int32, device=dev)
-    if args.workload != "estep":
+    if args.workload == "generate":
+        sample = torch.empty((B, T, model.num_vars), dtype=torch.int32, device=dev)
+        st.zero_()
+        ll.zero_()
+
+        def step():
+            nip_amd.generate_data(model, 12345 + rank, B, T, sample)
+    elif args.workload != "estep":
         post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
 
         def step():
@@ -193,6 +221,12 @@ def main():
         workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
             N, M, B, T)
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
+    elif args.workload == "generate":
+        kname = "generate_kernel"
+        bpu = 4 * model.num_vars       # the int32 draws written; the tables stay in cache
+        workload = "generate_data: HMM-shaped DBN, %d hidden x %d observed states, B=%d series/GPU x T=%d" % (
+            N, M, B, T)
+        metric = "sequence-timesteps/s generate_data (sampling), 16-state DBN"
     elif args.workload == "config3":
         workload = "config3: demo1.net structure, 5 vars x 32 states, A1 B1 observed, C1 posterior, " \
                    "B=%d seq/GPU x T=%d" % (B, T)
@@ -216,7 +250,9 @@ def main():
                          "traffic": traffic, "kernel": kname,
                          "kernel_ms": kern_ms, "bytes_per_unit": bpu},
         }
-        if world == 1 and not args.no_cpu_baseline and args.workload != "estep":
+        if world == 1 and not args.no_cpu_baseline and args.workload == "generate":
+            rec["cpu_baseline"] = cpu_baseline_generate(nodes, pots, T)
+        elif world == 1 and not args.no_cpu_baseline and args.workload != "estep":
             names = [n[0] for n in nodes]
             rec["cpu_baseline"] = cpu_baseline(
                 nodes, pots, obs_np, [names.index(v) for v in ov_names], names.index(q_name),

@@ -59,6 +59,17 @@ int index_of(const Compat* c, nip_variable v) {
 
 #define REPORT(e) nip_report_error((char*)__FILE__, __LINE__, (e), 1)
 
+// The caller's rand() stream belongs to the caller (random_seed, lottery, the
+// reference's generate_data and em_learn draw from it): while the engine and
+// the HIP runtime run, rand() is switched to a scratch state, so nothing they
+// do (runtime initialisation included) draws from or reseeds the caller's.
+struct RandGuard {
+  char scratch[128];
+  char* saved;
+  RandGuard() { saved = initstate(1, scratch, sizeof scratch); }
+  ~RandGuard() { setstate(saved); }
+};
+
 void engine_error(int e) {
   std::fprintf(stderr, "nip_amd: %s\n", nipamd_last_error());
   REPORT(e);
@@ -142,6 +153,7 @@ int run_inference(time_series* ts, int n, nip_variable vars[], int nvars, bool f
           for (int i = 0; i < k; i++) obs[((size_t)b * T + t) * k + i] = x->data[t][cols[ids[b]][i]];
       }
       std::vector<uint32_t> st(B);
+      RandGuard guard;
       rc = (filter ? nipamd_filter_host : nipamd_fb_host)(c->eng, obs.data(), k, ov.data(), B, T,
                                                           nvars, q.data(), post.data(), l.data(),
                                                           st.data());
@@ -705,8 +717,16 @@ int em_learn(time_series* ts, int n_ts, double threshold, nip_double_list learni
   }
   std::vector<double> curve(1 << 16);
   int curve_len = 0;
-  const int e = nipamd_em_learn(c->eng, n_ts, lengths.data(), obs.data(), k, ov.data(), threshold,
-                                nullptr, 0, curve.data(), (int)curve.size(), &curve_len);
+  // the random start from the caller's stream, rand()/RAND_MAX per parameter
+  // in the em_learn layout (nip_random_potential per variable, nip.c:2135-2138)
+  std::vector<double> init(nipamd_model_param_size(c->eng) + 1);
+  for (size_t i = 0; i + 1 < init.size(); i++) init[i] = std::rand() / (double)RAND_MAX;
+  int e;
+  {
+    RandGuard guard;
+    e = nipamd_em_learn(c->eng, n_ts, lengths.data(), obs.data(), k, ov.data(), threshold,
+                        init.data(), 0, curve.data(), (int)curve.size(), &curve_len);
+  }
   refresh_priors(c);
   if (e != NIP_NO_ERROR && e != NIP_ERROR_BAD_LUCK) {
     engine_error(e);
@@ -736,7 +756,11 @@ time_series generate_data(nip_model model, int length) {
   nipamd_generate_order(c->eng, order.data());
   std::vector<int32_t> draws((size_t)length * nv + 1), out((size_t)length * nv + 1);
   for (size_t i = 0; i + 1 < draws.size(); i++) draws[i] = std::rand();
-  const int e = nipamd_generate_host_draws(c->eng, 1, length, draws.data(), out.data());
+  int e;
+  {
+    RandGuard guard;
+    e = nipamd_generate_host_draws(c->eng, 1, length, draws.data(), out.data());
+  }
   if (e != NIP_NO_ERROR) {
     engine_error(e);
     return nullptr;

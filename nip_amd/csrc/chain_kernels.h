@@ -173,6 +173,8 @@ struct GenArgs {
   int* out = nullptr;               // [B][T][nv] draws, sampling-order columns
 };
 int generate_launch(const GenArgs& a, hipStream_t stream);
+// win [B][31] from qd_base = {x^D mod (x^31 - x^28 - 1) [31], r[313..373] [61]}
+int rand_window_launch(int B, const uint32_t* qd_base, uint32_t* win, hipStream_t stream);
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);

@@ -23,9 +23,11 @@
 //
 // glibc rand() (TYPE_3): srand(seed) fills r[0..30] by 16807 * r mod 2^31-1,
 // r[31..33] = r[0..2], r[n] = r[n-31] + r[n-3] (mod 2^32) after, and the k-th
-// rand() is r[344 + k] >> 1.  Series b starts at draw b * T * nv; its window
-// r[313 + o .. 343 + o] comes from series b-1's by x^(T nv) mod
-// (x^31 - x^28 - 1), the recurrence's characteristic polynomial.
+// rand() is r[344 + k] >> 1.  Series b starts at draw o = b * T * nv; its
+// window r[313 + o .. 343 + o] is x^o mod (x^31 - x^28 - 1) (the
+// recurrence's characteristic polynomial) applied to r[313..373]: the host
+// computes x^(T nv) once, rand_window_kernel raises it to the b-th power per
+// series (nipamd_rand_windows is the host form, for tests).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -396,18 +398,26 @@ int nipamd_generate(nipamd_model* mm, long seed, int B, int T, int32_t* d_data, 
   if (int rc = prepare(mm, g)) return rc;
   if (B == 0 || T == 0) return NIP_NO_ERROR;
   const int nv = (int)g->order.size();
-  std::vector<uint32_t> win((size_t)B * 31);
-  rand_windows(seed, B, (long)T * nv, win.data());
+  // x^(T nv) mod P and the stream's words r[313..373]: the kernel derives
+  // every series' window from them (rand_window_kernel)
+  const std::vector<uint32_t> r = glibc_state((unsigned)seed, 374);
+  const Poly Q = xpow((long)T * nv);
+  std::vector<uint32_t> qd(Q.begin(), Q.end());
+  qd.insert(qd.end(), r.begin() + 313, r.begin() + 374);
   hipStream_t st = (hipStream_t)stream;
-  if (g->win_cap < win.size()) {
+  const size_t need = (size_t)B * 31 + qd.size();
+  if (g->win_cap < need) {
     GEN_HIP(hipStreamSynchronize(st));
     (void)hipFree(g->d_win);
     g->d_win = nullptr;
     g->win_cap = 0;
-    GEN_HIP(hipMalloc(&g->d_win, win.size() * sizeof(uint32_t)));
-    g->win_cap = win.size();
+    GEN_HIP(hipMalloc(&g->d_win, need * sizeof(uint32_t)));
+    g->win_cap = need;
   }
-  GEN_HIP(hipMemcpyAsync(g->d_win, win.data(), win.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  uint32_t* d_qd = g->d_win + (size_t)B * 31;
+  GEN_HIP(hipMemcpyAsync(d_qd, qd.data(), qd.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  GEN_HIP(hipStreamSynchronize(st));     // 368 bytes; the host vector ends here
+  if (rand_window_launch(B, d_qd, g->d_win, st)) return set_error(NIPAMD_ERROR_DEVICE, "generate: window launch failed");
   GenArgs a;
   a.B = B;
   a.T = T;
@@ -419,7 +429,6 @@ int nipamd_generate(nipamd_model* mm, long seed, int B, int T, int32_t* d_data, 
   a.win = g->d_win;
   a.out = d_data;
   if (generate_launch(a, st)) return set_error(NIPAMD_ERROR_DEVICE, "generate: kernel launch failed");
-  GEN_HIP(hipStreamSynchronize(st));   // the host window buffer ends here
   return NIP_NO_ERROR;
 }
 

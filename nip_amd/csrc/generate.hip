@@ -79,7 +79,56 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(GenArgs a) {
   }
 }
 
+// c = a * b mod (x^31 - x^28 - 1), coefficients mod 2^32 (fully unrolled:
+// every index static, the polynomials live in VGPRs)
+__device__ __forceinline__ void polymulmod(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  uint32_t c[61];
+#pragma unroll
+  for (int k = 0; k < 61; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 31; i++)
+#pragma unroll
+    for (int j = 0; j < 31; j++) c[i + j] += a[i] * b[j];
+#pragma unroll
+  for (int d = 60; d >= 31; d--) {
+    c[d - 3] += c[d];
+    c[d - 31] += c[d];
+  }
+#pragma unroll
+  for (int k = 0; k < 31; k++) out[k] = c[k];
+}
+
+// win[b] = the rand() window of series b: x^(b D) mod P = (x^D)^b by square
+// and multiply on the bits of b, applied to the stream's first 61 words
+__global__ __launch_bounds__(256) void rand_window_kernel(int B, const uint32_t* __restrict__ qd,
+                                                          uint32_t* __restrict__ win) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  uint32_t r[31], p[31];
+#pragma unroll
+  for (int k = 0; k < 31; k++) { r[k] = k == 0; p[k] = qd[k]; }
+  for (unsigned e = (unsigned)b; e; e >>= 1) {
+    if (e & 1) polymulmod(r, p, r);
+    if (e > 1) polymulmod(p, p, p);
+  }
+  const uint32_t* base = qd + 31;               // r[313 .. 373]
+#pragma unroll
+  for (int m = 0; m < 31; m++) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 31; j++) s += r[j] * base[m + j];
+    win[(long)b * 31 + m] = s;
+  }
+}
+
 }  // namespace
+
+int rand_window_launch(int B, const uint32_t* qd_base, uint32_t* win, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(rand_window_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, stream, B,
+                     qd_base, win);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int generate_launch(const GenArgs& a, hipStream_t stream) {
   if (a.B <= 0 || a.T <= 0) return 0;

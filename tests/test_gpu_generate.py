@@ -79,6 +79,16 @@ def test_reference_nipsample(tmp_path, net):
     assert open(out).read() == "\n".join(lines) + "\n"
 
 
+def test_generate_many_series():
+    """300 series: every series' rand() window is derived on the GPU
+    (rand_window_kernel: x^(b T nv) by square-and-multiply on b's bits),
+    including the last ones, far into the stream."""
+    nodes, pots = synth.hmm_spec(4, 3, seed=1)
+    _, got = gen(nodes, pots, 31337, 300, 7)
+    want = bind.RefHarness(synth.spec_to_replay(nodes, pots)).generate(31337, 300, 7)[1]
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+
+
 def test_generate_edge_lengths():
     """T = 1 (first slice only), B = 1, and B*T = 0 (nothing drawn)."""
     nodes, pots = synth.demo1_spec(4)
@@ -110,7 +120,11 @@ def test_generate_large_batch_properties():
     counts = np.zeros((16, 16))
     np.add.at(counts, (x, o), 1)
     emp = counts / counts.sum(1, keepdims=True)
-    E = np.array(pots[[p[0] for p in pots].index("M1")][2], np.float64).reshape(16, 16)
+    # the emission clique {P1, M1} as the reference's parser leaves it (its CPT
+    # quirk normalises along the lowest-ID variable, P1), conditioned on P1
+    d = m.desc()
+    c = [k for k, cl in enumerate(d["cliques"]) if cl["vars"] == sorted([m.variable("P1"), m.variable("M1")])][0]
+    E = np.asarray(d["cliques"][c]["original"]).reshape(16, 16).T       # [P1][M1]
     E = E / E.sum(1, keepdims=True)
     n = counts.sum(1, keepdims=True)
     assert (np.abs(emp - E) <= 5 * np.sqrt(E * (1 - E) / n) + 1e-9).all()     # 5 sigma per cell
