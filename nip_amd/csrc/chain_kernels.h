@@ -168,9 +168,12 @@ struct GenArgs {
   const GenStep* steps = nullptr;   // [nv] device
   const double* tab = nullptr;      // device tables
   long zero_off = 0;                // an all-zero row (>= every card)
+  const double* cum = nullptr;      // running row sums of tab (same offsets)
+  long cum_n = 0;                   // their size (doubles)
   const uint32_t* win = nullptr;    // [B][31] rand() state of each series
   const int* draws = nullptr;       // or the rand() values themselves, [B][T][nv]
   int* out = nullptr;               // [B][T][nv] draws, sampling-order columns
+  int stage = 1;                    // slices buffered in LDS per store burst (launch sets it)
 };
 int generate_launch(const GenArgs& a, hipStream_t stream);
 // win [B][31] from qd_base = {x^D mod (x^31 - x^28 - 1) [31], r[313..373] [61]}

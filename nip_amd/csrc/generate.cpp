@@ -105,6 +105,7 @@ struct GenCache {
   std::vector<GenStep> steps;
   int x1_step = 0;
   long zero_off = 0;
+  long cum_off = 0;                   // the running-sum tables follow the tables
   GenStep* d_steps = nullptr;
   double* d_tab = nullptr;
   uint32_t* d_win = nullptr;
@@ -199,9 +200,11 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
     }
   normalise_rows(X1tab.data(), X1tab.size(), N);
   std::vector<double> tab;
-  auto append = [&](const std::vector<double>& t) {
+  std::vector<std::pair<long, int>> segs;     // (offset, row length) of every table
+  auto append = [&](const std::vector<double>& t, int card) {
     const long off = (long)tab.size();
     tab.insert(tab.end(), t.begin(), t.end());
+    segs.push_back({off, card});
     return off;
   };
   auto hweight = [&](long hi) {               // prod p_h over the H of index hi
@@ -242,7 +245,7 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
       normalise_rows(Tq.data(), Tq.size(), cards[q]);
       GenStep& s = g.steps[step_of[ind[q]]];
       s.card = cards[q];
-      s.off0 = append(Tq);
+      s.off0 = append(Tq, cards[q]);
       s.nctx = (int)q;
       long stride = cards[q];
       for (int c = (int)q - 1; c >= 0; c--) {
@@ -258,7 +261,7 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
     std::vector<double> I((size_t)N * N, 0.0);
     for (int x = 0; x < N; x++) I[(size_t)x * N + x] = 1.0;
     GenStep& s0 = g.steps[step_of[vp]];
-    s0.off1 = append(I);
+    s0.off1 = append(I, N);
     s0.nctx1 = 1;
     s0.ctx1[0] = -1;
     s0.stride1[0] = N;
@@ -275,7 +278,7 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
         for (long j = 0; j < block; j++) Tq[i] += W1[i * block + j];
       normalise_rows(Tq.data(), Tq.size(), cq);
       GenStep& s = g.steps[step_of[hid[q]]];
-      s.off1 = append(Tq);
+      s.off1 = append(Tq, cq);
       s.nctx1 = (int)q + 1;
       long stride = cq;
       for (int c = (int)q - 1; c >= 0; c--) {
@@ -291,7 +294,7 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
   {
     GenStep& s = g.steps[step_of[vc]];
     s.card = N;
-    s.off0 = s.off1 = append(X1tab);
+    s.off0 = s.off1 = append(X1tab, N);
     s.nctx = s.nctx1 = 1 + (int)hid.size();
     long stride = N;
     for (int q = (int)hid.size() - 1; q >= 0; q--) {
@@ -310,15 +313,26 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
     normalise_rows(T.data(), T.size(), E.M);
     GenStep& s = g.steps[step_of[E.var]];
     s.card = E.M;
-    s.off0 = s.off1 = append(T);
+    s.off0 = s.off1 = append(T, E.M);
     s.nctx = s.nctx1 = 1;
     s.ctx[0] = s.ctx1[0] = step_of[vc];
     s.stride[0] = s.stride1[0] = E.M;
   }
   int maxc = 1;
   for (const GenStep& s : g.steps) maxc = std::max(maxc, s.card);
-  g.zero_off = (long)tab.size();
-  tab.resize(tab.size() + maxc, 0.0);
+  g.zero_off = append(std::vector<double>(maxc, 0.0), maxc);
+  // running sums of every row, added in lottery()'s order (sum += d[i++],
+  // nip.c:2512-2518) so the kernel compares exactly the reference's sums
+  std::vector<double> cum(tab.size());
+  for (size_t k = 0; k < segs.size(); k++) {
+    const long end = k + 1 < segs.size() ? segs[k + 1].first : (long)tab.size();
+    for (long i = segs[k].first; i < end; i += segs[k].second) {
+      double sum = 0.0;
+      for (int j = 0; j < segs[k].second; j++) cum[i + j] = (sum += tab[i + j]);
+    }
+  }
+  tab.insert(tab.end(), cum.begin(), cum.end());
+  g.cum_off = (long)cum.size();
   g.x1_step = step_of[vc];
   release(g);
   GEN_HIP(hipMalloc(&g.d_steps, sizeof(GenStep) * nv));
@@ -426,6 +440,8 @@ int nipamd_generate(nipamd_model* mm, long seed, int B, int T, int32_t* d_data, 
   a.steps = g->d_steps;
   a.tab = g->d_tab;
   a.zero_off = g->zero_off;
+  a.cum = g->d_tab + g->cum_off;
+  a.cum_n = g->cum_off;
   a.win = g->d_win;
   a.out = d_data;
   if (generate_launch(a, st)) return set_error(NIPAMD_ERROR_DEVICE, "generate: kernel launch failed");
@@ -453,6 +469,8 @@ int nipamd_generate_host_draws(nipamd_model* mm, int B, int T, const int32_t* dr
     a.steps = g->d_steps;
     a.tab = g->d_tab;
     a.zero_off = g->zero_off;
+    a.cum = g->d_tab + g->cum_off;
+  a.cum_n = g->cum_off;
     a.draws = d_draws;
     a.out = d_out;
     if (generate_launch(a, nullptr)) rc = set_error(NIPAMD_ERROR_DEVICE, "generate: kernel launch failed");

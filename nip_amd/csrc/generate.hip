@@ -18,6 +18,8 @@
 // thread then samples from an all-zero row, as lottery() does there.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "chain_kernels.h"
 
 namespace nipamd {
@@ -26,19 +28,34 @@ namespace {
 
 constexpr int kGenBlock = 64;   // one wave per block: spreads B series over the CUs
 
+// LDS_TAB: the running-sum tables (a.cum_n doubles) are copied into LDS first;
+// otherwise every row read goes to L2 / HBM, where the output stream evicts them
+template <bool LDS_TAB>
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(GenArgs a) {
   extern __shared__ uint32_t lds[];
   uint32_t* st = lds;                               // [31][kGenBlock] rand() state
-  int* smp = (int*)(lds + 31 * kGenBlock);          // [nv][kGenBlock] draws of this slice
+  // draws of the last `stage` slices, [stage][nv][kGenBlock]: written out per
+  // thread in one burst of stores every `stage` slices, so a load's vmcnt wait
+  // (loads and stores retire in order) meets outstanding stores that rarely
+  int* stage = (int*)(lds + 31 * kGenBlock);
   const int tid = threadIdx.x;
   const long b = (long)blockIdx.x * kGenBlock + tid;
+  double* cum_lds = (double*)(lds + (31 + a.stage * a.nv) * kGenBlock);
+  if (LDS_TAB) {
+    for (long k = tid; k < a.cum_n; k += kGenBlock) cum_lds[k] = a.cum[k];
+    __syncthreads();
+  }
+  const double* cum = LDS_TAB ? cum_lds : a.cum;
   if (b >= a.B) return;                              // no block-level sync below
   if (!a.draws)
     for (int m = 0; m < 31; m++) st[m * kGenBlock + tid] = a.win[b * 31 + m];
   int pos = 0, prev = 0;
   bool dead = false;
   int* out = a.out + b * (long)a.T * a.nv;
+  int tt = 0;
+  long t0 = 0;
   for (int t = 0; t < a.T; t++) {
+    int* smp = stage + (long)tt * a.nv * kGenBlock;
     for (int i = 0; i < a.nv; i++) {
       const GenStep& s = a.steps[i];
       const int nctx = t ? s.nctx1 : s.nctx;
@@ -49,7 +66,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(GenArgs a) {
         const int j = ctx[c];
         idx += (long)(j >= 0 ? smp[j * kGenBlock + tid] : prev) * stride[c];
       }
-      const double* row = dead ? a.tab + a.zero_off : a.tab + (t ? s.off1 : s.off0) + idx;
+      const long ro = dead ? a.zero_off : (t ? s.off1 : s.off0) + idx;
       // rand(): r[n] = r[n-31] + r[n-3]; slot pos holds r[n-31], slot pos+28 (mod 31) r[n-3]
       int draw;
       if (a.draws) {
@@ -62,20 +79,35 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(GenArgs a) {
         draw = (int)(v >> 1);
       }
       const double r = (double)draw / 2147483647.0;
-      // lottery() (nip.c:2507-2520)
+      // lottery() (nip.c:2507-2520): the first k whose running sum is not
+      // below r.  The sums (cum, added in lottery()'s order on the host) are
+      // non-decreasing, so k = #{cum < r}: independent loads, no chain.
+      const double* crow = cum + ro;
       int k = 0;
-      double sum = 0.0;
-      for (;;) {
-        if (k >= s.card) { k = s.card; break; }
-        sum += row[k++];
-        if (!(sum < r)) break;
+      for (int k0 = 0; k0 < s.card; k0 += 16) {
+        double c[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) c[u] = k0 + u < s.card ? crow[k0 + u] : r;
+#pragma unroll
+        for (int u = 0; u < 16; u++) k += c[u] < r;
       }
-      k -= 1;
-      if (row[k] == 0.0) dead = true;
+      // a zero-probability draw: r == 0 takes state 0 (reached only with
+      // row[0] == 0 then), and running off the row end takes the last state
+      if (k == s.card) {
+        k = s.card - 1;
+        if (a.tab[ro + k] == 0.0) dead = true;
+      } else if (r == 0.0 && crow[0] == 0.0) {
+        dead = true;
+      }
       smp[i * kGenBlock + tid] = k;
-      out[(long)t * a.nv + i] = k;
     }
     prev = smp[a.x1_step * kGenBlock + tid];
+    if (++tt == a.stage || t == a.T - 1) {
+      int* o = out + t0 * a.nv;
+      for (int u = 0; u < tt * a.nv; u++) __builtin_nontemporal_store(stage[u * kGenBlock + tid], o + u);
+      t0 += tt;
+      tt = 0;
+    }
   }
 }
 
@@ -132,9 +164,16 @@ int rand_window_launch(int B, const uint32_t* qd_base, uint32_t* win, hipStream_
 
 int generate_launch(const GenArgs& a, hipStream_t stream) {
   if (a.B <= 0 || a.T <= 0) return 0;
-  const size_t lds = (size_t)(31 + a.nv) * kGenBlock * sizeof(uint32_t);
-  hipLaunchKernelGGL(generate_kernel, dim3((unsigned)((a.B + kGenBlock - 1) / kGenBlock)),
-                     dim3(kGenBlock), lds, stream, a);
+  GenArgs g = a;
+  g.stage = std::max(1, std::min(16, (256 - 31) / std::max(1, a.nv)));   // <= 64 KB LDS per block
+  size_t lds = (size_t)(31 + g.stage * a.nv) * kGenBlock * sizeof(uint32_t);
+  const dim3 grid((unsigned)((a.B + kGenBlock - 1) / kGenBlock));
+  if (lds + a.cum_n * sizeof(double) <= 64 * 1024) {
+    lds += a.cum_n * sizeof(double);
+    hipLaunchKernelGGL(generate_kernel<true>, grid, dim3(kGenBlock), lds, stream, g);
+  } else {
+    hipLaunchKernelGGL(generate_kernel<false>, grid, dim3(kGenBlock), lds, stream, g);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
