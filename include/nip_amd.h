@@ -295,6 +295,20 @@ int nipamd_generate_host_draws(nipamd_model* m, int B, int T, const int32_t* dra
  * (the next draw is (r[n-31] + r[n-3]) >> 1).  Exposed for tests. */
 int nipamd_rand_windows(long seed, int B, long draws_per_series, uint32_t* win);
 
+/*
+ * util/niplikelihood.c batched: for every step of B
+ * series of length T, independently (no message between slices), the
+ * probability mass after the evidence of the UNMARKED columns (m1), after all
+ * columns (m2), and ll = log(m2) - log(m1) = ln p(marked | unmarked)
+ * (niplikelihood.c:111-133).  marked[n_obs]: 1 for the variables of interest.
+ * d_obs int32 [B][T][n_obs]; d_m1, d_m2, d_ll double [B][T].  Synchronous.
+ */
+int nipamd_likelihood(nipamd_model* m, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                      const int* marked, int B, int T, double* d_m1, double* d_m2, double* d_ll,
+                      void* stream);
+int nipamd_likelihood_host(nipamd_model* m, const int32_t* obs, int n_obs, const int* obs_vars,
+                           const int* marked, int B, int T, double* m1, double* m2, double* ll);
+
 #ifdef __cplusplus
 }
 #endif

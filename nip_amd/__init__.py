@@ -54,7 +54,7 @@ EXPORTS = [
     "nipamd_em_learn", "nipamd_write_model", "nipamd_model_var_symbol",
     "nipamd_model_var_label", "nipamd_model_var_info",
     "nipamd_generate_order", "nipamd_generate", "nipamd_generate_host", "nipamd_rand_windows",
-    "nipamd_generate_host_draws",
+    "nipamd_generate_host_draws", "nipamd_likelihood", "nipamd_likelihood_host",
 ]
 
 
@@ -355,6 +355,24 @@ def generate_data(model: Model, seed: int, B: int, T: int, out=None, stream=None
     L.nipamd_generate.argtypes = [C.c_void_p, C.c_long, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
     _check(L.nipamd_generate(model._h, seed, B, T, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
     return order, out
+
+
+def likelihood(model: Model, obs, obs_vars, marked):
+    """util/niplikelihood.c batched on the GPU: (m1, m2, ll) [B][T] -- the
+    mass after the unmarked columns' evidence, after all, and log(m2/m1)
+    per step, each step on its own (niplikelihood.c:111-133)."""
+    obs = np.ascontiguousarray(np.asarray(obs, np.int32))
+    if obs.ndim == 2:
+        obs = obs[:, :, None]
+    B, T, nobs = obs.shape
+    out = [np.zeros((B, T)) for _ in range(3)]
+    L = lib()
+    L.nipamd_likelihood_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                         C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    _check(L.nipamd_likelihood_host(model._h, obs.ctypes.data_as(C.c_void_p), nobs, _ints(obs_vars),
+                                    _ints([1 if m else 0 for m in marked]), B, T,
+                                    *[o.ctypes.data_as(C.c_void_p) for o in out]))
+    return tuple(out)
 
 
 def rand_windows(seed: int, B: int, draws_per_series: int):

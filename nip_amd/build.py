@@ -39,7 +39,7 @@ def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
     return out
 
 
-TOOLS = ["nipamd_inference", "nipamd_train", "nipamd_map"]
+TOOLS = ["nipamd_inference", "nipamd_train", "nipamd_map", "nipamd_likelihood"]
 
 
 def build_tools(verbose: bool = False):

@@ -330,6 +330,18 @@ class RefHarness:
         n = self.lib().nh_prior(self.h, v, out)
         return out if n else None
 
+    def likelihood(self, obs, obs_vars, marked):
+        """util/niplikelihood.c over the reference's code: [ns][T][3] of
+        (m1, m2, log(m2) - log(m1)) per step."""
+        obs = np.ascontiguousarray(np.asarray(obs, np.int32))
+        ns, T, nobs = obs.shape
+        out = np.zeros((ns, T, 3))
+        L = self.lib()
+        L.nh_likelihood.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, _i32p, _i32p, _i32p, _f64p]
+        L.nh_likelihood(self.h, ns, T, nobs, np.asarray(obs_vars, np.int32),
+                        np.asarray([1 if x else 0 for x in marked], np.int32), obs.reshape(-1), out.reshape(-1))
+        return out
+
     def generate(self, seed, n_series, T):
         """generate_data (nip.c:2325-2478) n_series times from srand(seed):
         (order [nv], data [n_series][T][nv] in sampling-order columns)."""

@@ -794,6 +794,42 @@ int nh_prior(int h, int v, double* out){
   return var->cardinality;
 }
 
+/*
+ * util/niplikelihood.c:111-133 restated over the reference's code: per step
+ * of each series on its own, the mass after the unmarked columns' evidence
+ * (m1), after the marked ones' too (m2), ll = log(m2) - log(m1).
+ * obs [ns][T][nobs]; marked [nobs]; out [ns][T][3] = (m1, m2, ll).
+ */
+int nh_likelihood(int h, int ns, int T, int nobs, const int* obs_vars, const int* marked,
+                  const int* obs, double* out){
+  nh_model* m = nh_models[h];
+  int s, t, i;
+  for(s = 0; s < ns; s++){
+    h_reset_model(m);
+    h_use_priors(m, 0);
+    for(t = 0; t < T; t++){
+      const int* row = obs + ((size_t)s * T + t) * nobs;
+      double* o = out + ((size_t)s * T + t) * 3;
+      for(i = 0; i < nobs; i++)
+        if(!marked[i] && row[i] >= 0)
+          nip_enter_index_observation(m->variables, m->num_of_vars, m->cliques,
+                                      m->num_of_cliques, m->variables[obs_vars[i]], row[i]);
+      h_make_consistent(m);
+      o[0] = nip_probability_mass(m->cliques, m->num_of_cliques);
+      for(i = 0; i < nobs; i++)
+        if(marked[i] && row[i] >= 0)
+          nip_enter_index_observation(m->variables, m->num_of_vars, m->cliques,
+                                      m->num_of_cliques, m->variables[obs_vars[i]], row[i]);
+      h_make_consistent(m);
+      o[1] = nip_probability_mass(m->cliques, m->num_of_cliques);
+      o[2] = log(o[1]) - log(o[0]);
+      h_reset_model(m);
+      h_use_priors(m, 1);
+    }
+  }
+  return 0;
+}
+
 /* lottery, src/nip.c:2507-2520 */
 static int h_lottery(const double* d, int size){
   int i = 0;
