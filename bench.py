@@ -6,18 +6,25 @@ src/nip.c:1320, batched) over one batch of B synthetic sequences x T time
 slices resident in HBM -- SURVEY 8(d) config 2: HMM-shaped DBN with 16 hidden
 and 16 observed states, B = 4096 sequences per GPU, T = 1024.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W]
 
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL for the
-barrier / max-over-ranks only: sequences shard with no data-path collective,
-"scaling": "weak").  Rank 0 prints one JSON line.
+N > 1: one process per GPU.  Run directly with --gpus N, bench.py starts
+``python -m torch.distributed.run --nproc-per-node N`` on itself as a child
+process (before anything touches the GPU) and exits with its code; under a
+launcher it checks WORLD_SIZE == N and refuses to run otherwise.  fb-style
+workloads shard sequences with no data-path collective (RCCL only for the
+barrier and the max-over-ranks timing, "scaling": "weak"); the em workload
+ exchanges one packed all-gather per EM iteration.
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
-import ctypes as C
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,7 +54,49 @@ WORKLOADS = {
     "config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256),
     "config5": ("config5", lambda a: synth.wide_spec(64, 16), ["O1"], "X1", 256, 128),
     "generate": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 65536, 1024),
+    "em": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024),
 }
+
+
+def host_info():
+    """CPU model and the cores the baseline may use (the GPU box grants 16
+    per GPU: OMP_NUM_THREADS; os.cpu_count() shows the whole machine)."""
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    return model, cores, os.cpu_count()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_or_check(args, argv):
+    """--gpus N > 1 without a launcher: run N ranks under torch.distributed.run
+    as a child process and exit with its code (nothing here has touched the
+    GPU).  Under a launcher: WORLD_SIZE must equal --gpus."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+               "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+        sys.exit(subprocess.call(cmd))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit("bench: --gpus %d but WORLD_SIZE=%d; refusing to report a different world size"
+                 % (args.gpus, world))
+    return world
 
 
 def cpu_baseline_generate(nodes, pots, T, budget_s: float = 12.0):
@@ -71,34 +120,50 @@ def cpu_baseline_generate(nodes, pots, T, budget_s: float = 12.0):
 
 
 def cpu_baseline(nodes, pots, obs, ov, q, budget_s: float = 12.0, t_sample: int = 0):
-    """Reference CPU path on this host, single core, bounded sample.  ov / q are
-    variable indices in declaration order; t_sample > 0 times only the first
-    t_sample slices of each sequence (config 5's 16.7M-entry clique)."""
+    """Reference-equivalent CPU path on this host over a bounded sample of the
+    bench workload: the C restatement of forward_backward_inference
+    (oracle/nip_oracle.c, bit-identical to the reference's own code on every
+    golden case) with OpenMP over sequences on all granted cores, one
+    sequence per thread.  Where oracle/_ref exists (built in
+    the build container), the reference's own compiled code is also timed
+    on one core and r = port/ref per-core throughput is reported.  ov / q
+    are variable indices in declaration order; t_sample > 0 times only the
+    first t_sample slices of each sequence (config 5's 16.7M-entry clique)."""
     from oracle import bind
-    kind = "reference"
-    try:
-        if not bind.ref_available():
-            raise RuntimeError("oracle/_ref not built")
-        orc = bind.RefHarness(synth.spec_to_replay(nodes, pots), cards=[n[1] for n in nodes])
-    except Exception:
-        kind = "port"
-        import nip_amd
-        orc = bind.PortOracle(nip_amd.Model.from_spec(nodes, pots).desc())
+    import nip_amd
+    cpu, cores, ncpu = host_info()
     T = t_sample or obs.shape[1]
+    orc = bind.PortOracle(nip_amd.Model.from_spec(nodes, pots).desc())
+    # size the sample: one sequence on one thread first
     t0 = time.perf_counter()
-    n = 0
-    while True:
-        orc.fb(obs[n][:T], ov, [q])
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= obs.shape[0]:
-            break
-    return {"value": n * T / el, "unit": "sequence-timesteps/s", "cores": 1, "kind": kind,
-            "sample": "%d sequences x T=%d of the bench workload, forward_backward_inference with "
-                      "ll, %s, gcc -O2, %.1f s" % (
-                          n, T, "reference nippotential/nipjointree/nipgraph compiled from "
-                          "/root/reference sources + restated nip.c loop" if kind == "reference"
-                          else "standalone C restatement (oracle/nip_oracle.c)", el)}
+    orc.fb(obs[0][:T], ov, [q])
+    one = max(time.perf_counter() - t0, 1e-6)
+    n = int(max(cores, min(obs.shape[0], budget_s / one * cores)))
+    n = max(cores, (n // cores) * cores)
+    sample = np.ascontiguousarray(obs[:n, :T])
+    t0 = time.perf_counter()
+    orc.fb_batch(sample, ov, [q], nthreads=cores)
+    el = time.perf_counter() - t0
+    rec = {"value": n * T / el, "unit": "sequence-timesteps/s", "cores": cores, "kind": "port",
+           "cpu_model": cpu, "host_cpus": ncpu,
+           "sample": "%d sequences x T=%d of the bench workload, forward_backward_inference with ll, "
+                     "C restatement (oracle/nip_oracle.c, gcc -O2) with OpenMP over %d threads, "
+                     "%.1f s" % (n, T, cores, el)}
+    try:
+        if bind.ref_available():
+            ref = bind.RefHarness(synth.spec_to_replay(nodes, pots), cards=[x[1] for x in nodes])
+            k, t0 = 0, time.perf_counter()
+            while True:
+                ref.fb(obs[k][:T], ov, [q])
+                k += 1
+                if time.perf_counter() - t0 >= budget_s / 4 or k >= obs.shape[0]:
+                    break
+            ref_rate = k * T / (time.perf_counter() - t0)
+            rec["reference_1core"] = ref_rate
+            rec["r_port_over_ref_per_core"] = (rec["value"] / cores) / ref_rate
+    except Exception as e:  # the reference build is optional on the GPU box
+        rec["reference_1core_error"] = str(e)[:200]
+    return rec
 
 
 def load_traffic(workload: str):
@@ -127,16 +192,18 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb",
                     help="fb: the headline metric (config 2 smoothing); estep: one batched "
                          "e_step (config 4 per-GPU shard: counts + ll, no posterior write); "
+                         "em: config 4, one step = one em_learn iteration (m_step, e_step of "
+                         "the shard, the packed all-gather over RCCL, finalize); "
                          "config3: demo1 @ 32 states smoothing; config5: wide-clique smoothing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
     args = ap.parse_args()
+    world = launch_or_check(args, sys.argv[1:])
 
     import torch
     import torch.distributed as dist
     import nip_amd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -163,6 +230,20 @@ def main():
 
         def step():
             nip_amd.generate_data(model, 12345 + rank, B, T, sample)
+    elif args.workload == "em":
+        from nip_amd import em as nem
+        group = dist.group.WORLD if world > 1 else None
+        em_state = {"params": synth.uniform01(2024, model.param_size()) + 0.05, "ll": [],
+                    "exchange_ms": []}
+
+        def step():
+            tm = {}
+            p, l, bad = nem.iteration(model, em_state["params"], obs, ov, group, timing=tm)
+            if bad:
+                raise SystemExit("bench: e_step BAD_LUCK on synthetic data")
+            em_state["params"] = p
+            em_state["ll"].append(l)
+            em_state["exchange_ms"].append(tm.get("exchange_ms", 0.0))
     elif args.workload != "estep":
         post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
 
@@ -192,6 +273,9 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if args.workload == "em":
+        ll.zero_()
+        st.zero_()
     if not args.no_check and (not bool(torch.isfinite(ll).all()) or int(st.abs().sum()) != 0):
         raise SystemExit("bench: non-finite log-likelihood / zero-mass status on synthetic data")
 
@@ -202,7 +286,7 @@ def main():
 
     units = B * T * args.steps * world
     value = units / elapsed
-    bpu = algorithmic_bytes_per_seq_step(N, len(ov), args.workload != "estep")
+    bpu = algorithmic_bytes_per_seq_step(N, len(ov), args.workload not in ("estep", "em"))
     narrow = N <= 16 and len(ov) <= 1
     if not narrow and N <= 32 and os.environ.get("NIPAMD_FB_KERNEL") != "wide":
         kname = "chain_mfma_wide_kernel<%d>" % (1 if N <= 16 else 2)
@@ -221,6 +305,12 @@ def main():
         workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
             N, M, B, T)
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
+    elif args.workload == "em":
+        kname = "chain_kernel<true> + tree64 + finalize"
+        workload = ("config4: em_learn iterations of HMM-shaped DBN, %d hidden x %d observed, "
+                    "B=%d seq/GPU x T=%d, %d GPU(s), one packed RCCL all-gather per iteration" % (
+                        N, M, B, T, world))
+        metric = "sequence-timesteps/s em_learn (E-step + exchange + M-step per iteration), 16-state DBN"
     elif args.workload == "generate":
         kname = "generate_kernel"
         bpu = 4 * model.num_vars       # the int32 draws written; the tables stay in cache
@@ -250,9 +340,15 @@ def main():
                          "traffic": traffic, "kernel": kname,
                          "kernel_ms": kern_ms, "bytes_per_unit": bpu},
         }
+        if args.workload == "em":
+            rec["em"] = {"iterations_timed": args.steps, "ll_per_iteration": em_state["ll"][-args.steps:],
+                         "exchange_ms_median": float(np.median(em_state["exchange_ms"][-args.steps:])),
+                         "exchange_bytes_per_rank": 8 * (model.param_size() + 2),
+                         "note": "kernel_ms is the whole iteration on the launch stream "
+                                 "(e_step kernels, exchange, finalize, host m_step)"}
         if world == 1 and not args.no_cpu_baseline and args.workload == "generate":
             rec["cpu_baseline"] = cpu_baseline_generate(nodes, pots, T)
-        elif world == 1 and not args.no_cpu_baseline and args.workload != "estep":
+        elif world == 1 and not args.no_cpu_baseline and args.workload not in ("estep", "em"):
             names = [n[0] for n in nodes]
             rec["cpu_baseline"] = cpu_baseline(
                 nodes, pots, obs_np, [names.index(v) for v in ov_names], names.index(q_name),

@@ -265,6 +265,21 @@ def _stream_ptr(stream):
     return C.c_void_p(stream.cuda_stream)
 
 
+def _out_buf(t, shape, dtype, dev, name):
+    """A caller-supplied output buffer must be exactly what the kernels write
+    through its raw pointer: shape, dtype, device and dense layout; None
+    allocates one."""
+    import torch
+    if t is None:
+        return torch.empty(shape, dtype=dtype, device=dev)
+    if (tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device != dev
+            or not t.is_contiguous()):
+        raise NipError(NIP_ERROR_INVALID_ARGUMENT,
+                       "%s must be a contiguous %s tensor of shape %s on %s (got %s %s on %s)"
+                       % (name, dtype, tuple(shape), dev, t.dtype, tuple(t.shape), t.device))
+    return t
+
+
 def _run_device(fn, model, obs, obs_vars, query, post, ll, status, stream):
     import torch
     if obs.dim() == 2:
@@ -274,12 +289,9 @@ def _run_device(fn, model, obs, obs_vars, query, post, ll, status, stream):
     assert nobs == len(obs_vars)
     width = sum(model.card(v) for v in query)
     dev = obs.device
-    if post is None:
-        post = torch.empty((B, T, width), dtype=torch.float64, device=dev)
-    if ll is None:
-        ll = torch.empty((B,), dtype=torch.float64, device=dev)
-    if status is None:
-        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    post = _out_buf(post, (B, T, width), torch.float64, dev, "post")
+    ll = _out_buf(ll, (B,), torch.float64, dev, "ll")
+    status = _out_buf(status, (B,), torch.int32, dev, "status")
     _check(fn(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
               len(query), _ints(query), C.c_void_p(post.data_ptr()),
               C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
@@ -365,6 +377,9 @@ def likelihood(model: Model, obs, obs_vars, marked):
     if obs.ndim == 2:
         obs = obs[:, :, None]
     B, T, nobs = obs.shape
+    if not (len(obs_vars) == nobs == len(marked)):
+        raise NipError(NIP_ERROR_INVALID_ARGUMENT, "obs_vars (%d) and marked (%d) must name every "
+                       "one of the %d columns" % (len(obs_vars), len(marked), nobs))
     out = [np.zeros((B, T)) for _ in range(3)]
     L = lib()
     L.nipamd_likelihood_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
@@ -471,12 +486,9 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
     if S < 0:
         raise NipError(NIPAMD_ERROR_UNSUPPORTED, "model has no GPU e_step plan")
     dev = obs.device
-    if partial is None:
-        partial = torch.empty((S,), dtype=torch.float64, device=dev)
-    if ll is None:
-        ll = torch.empty((B,), dtype=torch.float64, device=dev)
-    if status is None:
-        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    partial = _out_buf(partial, (S,), torch.float64, dev, "partial")
+    ll = _out_buf(ll, (B,), torch.float64, dev, "ll")
+    status = _out_buf(status, (B,), torch.int32, dev, "status")
     _check(lib().nipamd_estep_partial(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars),
                                       B, T, C.c_void_p(partial.data_ptr()), C.c_void_p(ll.data_ptr()),
                                       C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
@@ -485,7 +497,8 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
 
 def estep_finalize(model: Model, partial, counts, stream=None):
     """counts (CUDA float64 [param_size], em_learn layout) += families of partial."""
-    assert counts.is_cuda and counts.numel() == model.param_size()
+    import torch
+    counts = _out_buf(counts, (model.param_size(),), torch.float64, partial.device, "counts")
     _check(lib().nipamd_estep_finalize(model._h, C.c_void_p(partial.data_ptr()),
                                        C.c_void_p(counts.data_ptr()), _stream_ptr(stream)))
     return counts
@@ -505,10 +518,9 @@ def e_step(model: Model, obs, obs_vars, counts=None, ll=None, status=None, strea
     dev = obs.device
     if counts is None:
         counts = torch.ones((model.param_size(),), dtype=torch.float64, device=dev)
-    if ll is None:
-        ll = torch.empty((B,), dtype=torch.float64, device=dev)
-    if status is None:
-        status = torch.empty((B,), dtype=torch.int32, device=dev)
+    counts = _out_buf(counts, (model.param_size(),), torch.float64, dev, "counts")
+    ll = _out_buf(ll, (B,), torch.float64, dev, "ll")
+    status = _out_buf(status, (B,), torch.int32, dev, "status")
     _check(lib().nipamd_estep(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
                               C.c_void_p(counts.data_ptr()), C.c_void_p(ll.data_ptr()),
                               C.c_void_p(status.data_ptr()), _stream_ptr(stream)))

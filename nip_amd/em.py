@@ -10,13 +10,14 @@ replaced by one batched e_step per iteration.
 
 Data-parallel (util/niptrain.c:151 trains one model on a sequence set): with
 ``group`` set, each process owns a shard of the sequences on its own GPU.
-Every iteration it computes its e_step partial (nipamd_estep_partial), the
-partials are all-gathered over RCCL and combined by the fixed pairwise tree
-(`tree_sum`) in rank order, and every rank applies the same finalize and
-m_step -- so all ranks keep bit-identical models, and with power-of-two
-shards the counts are bit-identical to the single-GPU run.  The only
-collectives are one all-gather of partial_size doubles and one of the
-per-sequence log-likelihoods per iteration.
+Every iteration it computes its e_step partial (nipamd_estep_partial); the
+partial, the tree sum of its sequences' log-likelihoods and its failure
+count are packed into one buffer, all-gathered over RCCL and combined by the
+fixed pairwise tree (`tree_sum`) in rank order (`exchange`), and every rank
+applies the same finalize and m_step -- so all ranks keep bit-identical
+models, and with power-of-two shards the counts and the ll are bit-identical
+to the single-GPU run.  That all-gather (partial_size + 2 doubles per rank,
+4.2 KB for the 16-state HMM) is the only collective of an iteration.
 """
 from __future__ import annotations
 
@@ -47,24 +48,33 @@ def combine_partials(partial, group=None):
     if group is None or dist.get_world_size(group) == 1:
         return partial
     W = dist.get_world_size(group)
-    out = [torch.empty_like(partial) for _ in range(W)]
-    dist.all_gather(out, partial.contiguous(), group=group)
-    return tree_sum(torch.stack(out))
+    x = partial.contiguous()
+    dev = x.device
+    if dist.get_backend(group) == "gloo" and x.is_cuda:
+        x = x.cpu()          # gloo rehearsal of the RCCL path (tests)
+    out = [torch.empty_like(x) for _ in range(W)]
+    dist.all_gather(out, x, group=group)
+    return tree_sum(torch.stack(out)).to(dev)
 
 
-def gather_sequence_ll(ll, status, group=None):
-    """Per-sequence log-likelihoods / statuses of all ranks, in global order
-    (host numpy).  Shards must have equal length."""
+def exchange(partial, ll, status, group=None):
+    """The one collective of an EM iteration.
+
+    Each rank packs [its count partial | the tree sum of its per-sequence
+    log-likelihoods | its number of failed sequences] into one buffer of
+    partial_size + 2 doubles; one all-gather over RCCL (xGMI) and the same
+    rank-ordered pairwise tree on every rank give the global partial and the
+    global ll.  The ll tree has the shape of the count tree, so for
+    power-of-two shards both are bit-identical to the 1-GPU run.
+    Returns (partial, ll_total (python float), n_bad (int))."""
     import torch
-    import torch.distributed as dist
-    if group is None or dist.get_world_size(group) == 1:
-        return ll.cpu().numpy(), status.cpu().numpy()
-    W = dist.get_world_size(group)
-    both = torch.stack([ll, status.to(torch.float64)]).contiguous()
-    out = [torch.empty_like(both) for _ in range(W)]
-    dist.all_gather(out, both, group=group)
-    out = torch.stack(out).cpu().numpy()
-    return out[:, 0].reshape(-1), out[:, 1].reshape(-1).astype(np.int64)
+    ll_part = tree_sum(ll.to(torch.float64).reshape(-1, 1))
+    bad = (status != 0).sum().to(torch.float64).reshape(1).to(partial.device)
+    packed = torch.cat([partial.reshape(-1), ll_part.reshape(1).to(partial.device), bad])
+    comb = combine_partials(packed, group)
+    P = partial.numel()
+    tail = comb[P:].cpu()
+    return comb[:P], float(tail[0]), int(round(float(tail[1])))
 
 
 class GpuEStep:
@@ -79,6 +89,28 @@ class GpuEStep:
         return estep_finalize(model, partial, counts)
 
 
+def iteration(model, params, obs, obs_vars, group=None, backend=None, timing=None):
+    """One em_learn iteration (src/nip.c:2154-2207): m_step(params), e_step
+    of this rank's shard with pseudo-counts 1.0, the one exchange, finalize.
+    Returns (new params (host), global ll, number of failed sequences).
+    ``timing``: optional dict; 'exchange_ms' receives the collective's time."""
+    import time
+    import torch
+    be = backend or GpuEStep()
+    P = model.param_size()
+    model.m_step(params)                          # nip.c:2154
+    counts = torch.ones((P,), dtype=torch.float64, device=obs.device)   # nip.c:2172
+    partial, ll, status = be.partial(model, obs, obs_vars)
+    if timing is not None and obs.is_cuda:
+        torch.cuda.synchronize(obs.device)
+        t0 = time.perf_counter()
+    partial, loglikelihood, n_bad = exchange(partial, ll, status, group)
+    if timing is not None and obs.is_cuda:
+        timing["exchange_ms"] = (time.perf_counter() - t0) * 1e3
+    be.finalize(model, partial, counts)
+    return counts.cpu().numpy(), loglikelihood, n_bad
+
+
 def em_learn(model, obs, obs_vars, threshold, learning_curve=None, init=None,
              max_iterations=None, seed=None, group=None, backend=None):
     """em_learn(ts, n_ts, threshold, learning_curve) (src/nip.c:2076).
@@ -91,15 +123,12 @@ def em_learn(model, obs, obs_vars, threshold, learning_curve=None, init=None,
     Returns NIP_NO_ERROR or NIP_ERROR_BAD_LUCK; the model keeps the
     parameters of the last m_step, as in the reference.
     """
-    import torch
-    be = backend or GpuEStep()
     if learning_curve is not None:
         del learning_curve[:]
     P = model.param_size()
     if init is None:
         init = np.random.default_rng(seed).random(P)
     params = np.array(init, dtype=np.float64).reshape(P)
-    dev = obs.device
     B, T = int(obs.shape[0]), int(obs.shape[1])
     world = 1
     if group is not None:
@@ -109,17 +138,11 @@ def em_learn(model, obs, obs_vars, threshold, learning_curve=None, init=None,
     loglikelihood = -np.finfo(np.float64).max     # -DBL_MAX, nip.c:2082
     i = 0
     while True:
-        model.m_step(params)                      # nip.c:2154
         old_loglikelihood = loglikelihood
-        counts = torch.ones((P,), dtype=torch.float64, device=dev)   # nip.c:2172
-        partial, ll, status = be.partial(model, obs, obs_vars)
-        partial = combine_partials(partial, group)
-        lls, sts = gather_sequence_ll(ll, status, group)
-        if np.any(sts != 0):                      # e_step BAD_LUCK, nip.c:2182-2198
+        new, loglikelihood, n_bad = iteration(model, params, obs, obs_vars, group, backend)
+        if n_bad:                                 # e_step BAD_LUCK, nip.c:2182-2198
             return NIP_ERROR_BAD_LUCK
-        loglikelihood = float(np.sum(lls))
-        be.finalize(model, partial, counts)
-        params = counts.cpu().numpy()
+        params = new
         if learning_curve is not None:
             learning_curve.append(loglikelihood / ts_steps)
         if (old_loglikelihood > loglikelihood + ts_steps * threshold or

@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 
 import nip_amd
 from nip_amd import synth
-from nip_amd.em import tree_sum, combine_partials, gather_sequence_ll, em_learn, NIP_NO_ERROR
+from nip_amd.em import tree_sum, combine_partials, exchange, em_learn, NIP_NO_ERROR
 
 
 def free_port():
@@ -55,10 +55,14 @@ def _worker(rank, world, port, q):
         shard = rows[rank * 32:(rank + 1) * 32]
         comb = combine_partials(tree_sum(shard), g)
         out["combine_exact"] = bool(torch.equal(comb, tree_sum(rows)))
-        # 2. global ll order
-        ll = torch.arange(rank * 4, rank * 4 + 4, dtype=torch.float64)
-        lls, sts = gather_sequence_ll(ll, torch.zeros(4, dtype=torch.int32), g)
-        out["ll_order"] = lls.tolist()
+        # 2. the packed exchange: partial, ll tree sum and failure count in one all-gather
+        ll = torch.from_numpy(rng.random(8) * 1e3)
+        mine = ll[rank * 4:(rank + 1) * 4]
+        st = torch.tensor([0, 0, rank, 0], dtype=torch.int32)
+        p, llt, nbad = exchange(tree_sum(shard), mine, st, g)
+        out["ex_partial"] = bool(torch.equal(p, tree_sum(rows)))
+        out["ex_ll"] = llt == float(tree_sum(ll.reshape(-1, 1))[0])
+        out["ex_bad"] = nbad
         # 3. em_learn over sharded sequences
         nodes, pots = synth.hmm_spec(4, 5, seed=77)
         m = nip_amd.Model.from_spec(nodes, pots)
@@ -98,7 +102,8 @@ def test_two_rank_em_driver():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0]["combine_exact"] and res[1]["combine_exact"]
-    assert res[0]["ll_order"] == [0, 1, 2, 3, 4, 5, 6, 7]
+    for r in range(2):
+        assert res[r]["ex_partial"] and res[r]["ex_ll"] and res[r]["ex_bad"] == 1
     # every rank ends with the same model
     assert res[0]["curve"] == res[1]["curve"] and res[0]["orig"] == res[1]["orig"]
     assert res[0]["rc"] == NIP_NO_ERROR

@@ -1,0 +1,140 @@
+"""Data-parallel EM on the GPU: the product
+e_step backend (GpuEStep: nipamd_estep_partial / _finalize through the C-ABI)
+in a world_size-2 process group on the one GPU of the test box.
+
+Both ranks run on cuda:0 (RCCL refuses two ranks on one device, so the group
+is gloo; em.exchange moves the packed buffer through host memory for gloo and
+over RCCL/xGMI in bench.py --workload em).  Asserted:
+  * the 2-rank learning curve, final model and per-iteration ll are
+    bit-identical to the 1-rank run over the same sequences (power-of-two
+    shards: the rank trees are subtrees of the 1-GPU tree);
+  * at the full per-GPU shard of config 4 (131072 x 1024), count masses and
+    spot oracle parity (per-sequence ll and counts of a 32-sequence subset).
+"""
+import os
+import queue
+import socket
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+import nip_amd
+from nip_amd import synth
+from nip_amd import em as nem
+from oracle.bind import PortOracle
+
+B_TOTAL, T, ITERS = 1024, 96, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(rank, world, group):
+    nodes, pots = synth.hmm_spec(16, 16, seed=31)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = synth.observations(B_TOTAL, T, 16, seed=77)
+    per = B_TOTAL // world
+    mine = torch.from_numpy(np.ascontiguousarray(obs[rank * per:(rank + 1) * per])).cuda()
+    params = synth.uniform01(2024, m.param_size()) + 0.05
+    lls = []
+    for _ in range(ITERS):
+        params, ll, bad = nem.iteration(m, params, mine, [m.variable("M1")], group)
+        assert bad == 0
+        lls.append(ll)
+    orig = np.concatenate([m.original(c) for c in range(len(m.desc()["cliques"]))])
+    return {"lls": lls, "params": params.tolist(), "orig": orig.tolist()}
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run(rank, world, dist.group.WORLD)))
+    except Exception as e:  # report, do not hang the parent
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_em_on_gpu_bit_identical_to_one_rank():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    t0 = time.time()
+    while len(res) < 2 and time.time() - t0 < 100:
+        try:
+            r, out = q.get(timeout=2)
+            res[r] = out
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in ps):
+                break
+    for p in ps:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert len(res) == 2, [p.exitcode for p in ps]
+    for r in range(2):
+        assert "error" not in res[r], res[r]
+    one = _run(0, 1, None)
+    for r in range(2):
+        assert res[r]["lls"] == one["lls"]          # bit-identical, not approximately
+        assert res[r]["params"] == one["params"]
+        assert res[r]["orig"] == one["orig"]
+
+
+def test_config4_shard_scale_and_spot_parity():
+    """One e_step over config 4's per-GPU shard (131072 x 1024)."""
+    nodes, pots = synth.hmm_spec(16, 16)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    B, Tn, N, M = 131072, 1024, 16, 16
+    obs_np = synth.observations(B, Tn, M, seed=4)
+    obs = torch.from_numpy(obs_np).cuda()
+    del obs_np
+    ov = [m.variable("M1")]
+    partial, ll, st = nip_amd.estep_partial(m, obs, ov)
+    counts = torch.ones((m.param_size(),), dtype=torch.float64, device="cuda")
+    nip_amd.estep_finalize(m, partial, counts)
+    cnt = counts.cpu().numpy()
+    assert not st.any().item()
+    assert bool(torch.isfinite(ll).all()) and float(ll.max()) < 0
+    d = m.desc()
+    sizes = []
+    for v in d["vars"]:
+        s = v["card"]
+        for p in v["parents"]:
+            s *= d["vars"][p]["card"]
+        sizes.append(s)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    mass = {d["vars"][i]["symbol"]: cnt[offs[i]:offs[i + 1]].sum() for i in range(3)}
+    assert abs(mass["P0"] - (N + B)) <= 1e-9 * (N + B)
+    assert abs(mass["P1"] - (N * N + B * Tn)) <= 1e-9 * B * Tn
+    assert abs(mass["M1"] - (N * M + B * Tn)) <= 1e-9 * B * Tn
+    # spot parity: 32 sequences spread over the shard, per-sequence ll from
+    # the full-shard launch, counts of the subset against the oracle
+    idx = np.linspace(0, B - 1, 32).astype(np.int64)
+    sub = obs[torch.from_numpy(idx).cuda()].contiguous()
+    sub_np = sub.cpu().numpy()
+    rc, rl, rb = PortOracle(d).estep(sub_np, ov, np.ones(m.param_size()))
+    assert not rb.any()
+    llf = ll.cpu().numpy()[idx]
+    assert np.all(np.abs(llf - rl) <= 1e-12 * np.abs(rl))
+    c32, _, _ = nip_amd.e_step(m, sub, ov)
+    c32 = c32.cpu().numpy()
+    assert np.all(np.abs(c32 - rc) <= 1e-11 * np.maximum(1.0, np.abs(rc)))
