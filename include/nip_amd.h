@@ -113,10 +113,37 @@ int nipamd_graph_cliques(int n, const int* card, int n_edges, const int* edges,
  * variable, a table with the child as dimension 0, then v->parents order. */
 int nipamd_model_param_size(const nipamd_model* m);
 
-/* 1 if the model has a GPU execution plan (SURVEY 8(d) config 2 family). */
+/* 1 if the model has a GPU execution plan for this request: the interface-
+ * chain kernels or the general join-tree engine (any slice whose clique
+ * tables fit; include/nip_amd.h NIPAMD_ENGINE_*). */
 int nipamd_model_gpu_supported(const nipamd_model* m, int n_obs,
                                const int* obs_vars, int n_query,
                                const int* query_vars);
+
+/*
+ * Engine selection for a model (not part of the reference API).
+ *   NIPAMD_ENGINE_AUTO   the interface-chain kernels where the slice is an
+ *                        interface chain and they fit, else the general
+ *                        join-tree engine (jtree.hip)
+ *   NIPAMD_ENGINE_CHAIN  interface-chain kernels only (UNSUPPORTED otherwise)
+ *   NIPAMD_ENGINE_JTREE  the general join-tree engine for every request
+ * Both run on the GPU; there is no CPU path.  Returns the previous value.
+ */
+#define NIPAMD_ENGINE_AUTO  0
+#define NIPAMD_ENGINE_CHAIN 1
+#define NIPAMD_ENGINE_JTREE 2
+int nipamd_model_set_engine(nipamd_model* m, int engine);
+
+/*
+ * The general engine's compiled schedule for a request (host only, no device
+ * work): header hdr[29] (sizes and offsets of jtree.h's JtPlanDev, then L,
+ * LDS flag, query row width), the int pool and the table pool.  sizes[0..1]
+ * receive the pool lengths; pass NULL pools to query them.  A test hook:
+ * tests/jt_emul.py replays the schedule against the CPU oracle.
+ */
+int nipamd_jt_plan_dump(const nipamd_model* m, int n_obs, const int* obs_vars, int n_query,
+                        const int* query, int estep, int* hdr, int hdr_cap, int* ip, long ip_cap,
+                        double* dp, long dp_cap, long* sizes);
 
 /* ------------------------------------------------------------------ */
 /* Hot path (device)                                                    */

@@ -38,6 +38,9 @@ NIPAMD_ERROR_UNSUPPORTED = 100
 NIPAMD_ERROR_DEVICE = 101
 STATUS_ZERO_MASS = 1
 STATUS_BAD_LUCK = 2
+ENGINE_AUTO = 0          # interface-chain kernels where they apply, else the general engine
+ENGINE_CHAIN = 1         # interface-chain kernels only
+ENGINE_JTREE = 2         # the general join-tree engine for every request
 
 # every entry point declared in include/nip_amd.h
 EXPORTS = [
@@ -55,6 +58,7 @@ EXPORTS = [
     "nipamd_model_var_label", "nipamd_model_var_info",
     "nipamd_generate_order", "nipamd_generate", "nipamd_generate_host", "nipamd_rand_windows",
     "nipamd_generate_host_draws", "nipamd_likelihood", "nipamd_likelihood_host",
+    "nipamd_model_set_engine", "nipamd_jt_plan_dump",
 ]
 
 
@@ -215,8 +219,19 @@ class Model:
                                                      len(query), _ints(query)))
 
     def estep_supported(self) -> bool:
-        """Whether the batched e_step has a GPU plan for this model (the HMM slice)."""
+        """Whether the batched e_step has a GPU plan for this model under the
+        selected engine (the chain kernel's HMM slice, or the general engine)."""
         return lib().nipamd_estep_partial_size(self._h) >= 0
+
+    def set_engine(self, engine: int) -> int:
+        """nipamd_model_set_engine: ENGINE_AUTO / ENGINE_CHAIN / ENGINE_JTREE;
+        returns the previous setting."""
+        L = lib()
+        L.nipamd_model_set_engine.argtypes = [C.c_void_p, C.c_int]
+        prev = L.nipamd_model_set_engine(self._h, int(engine))
+        if prev < 0:
+            raise NipError(NIP_ERROR_INVALID_ARGUMENT, "bad engine %r" % engine)
+        return prev
 
     def original(self, c: int) -> np.ndarray:
         n = lib().nipamd_model_original(self._h, c, None, 0)

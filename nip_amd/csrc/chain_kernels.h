@@ -6,6 +6,21 @@
 
 namespace nipamd {
 
+// The dynamic-LDS limit of a kernel is a per-device attribute: raise it on
+// the current device when a launch needs more than the default 64 KB,
+// remembering (per kernel, per device) the largest value already set.
+constexpr int kMaxDevices = 64;
+inline int ensure_dyn_lds(const void* kernel, size_t lds, size_t (&set)[kMaxDevices]) {
+  if (lds <= 65536) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
+  if (lds <= set[dev]) return 0;
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -1;
+  set[dev] = lds;
+  return 0;
+}
+
 struct ChainArgs {
   const int* obs;        // int32 observations
   long obs_bstride;      // elements between sequences

@@ -834,13 +834,8 @@ size_t chain_mfma_lds_bytes(int M, int T) {       // without the DMA buffers
 namespace {
 template <bool DMA>
 int launch_mfma(const ChainArgs& a, size_t lds, hipStream_t stream) {
-  static size_t lds_set = 0;
-  if (lds > 65536 && lds > lds_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return -1;
-    lds_set = lds;
-  }
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA>), lds, lds_set)) return -1;
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
   hipLaunchKernelGGL(chain_fb_mfma_kernel<DMA>, dim3(blocks), dim3(kMThreads), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

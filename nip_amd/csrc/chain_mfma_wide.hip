@@ -543,13 +543,8 @@ size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
 namespace {
 template <int NT, bool FILT>
 int launch_wide(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
-  static size_t set = 0;
-  if (lds > 65536 && lds > set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return -1;
-    set = lds;
-  }
+  static size_t set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT>), lds, set)) return -1;
   const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
   hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
                      lds, stream, a);

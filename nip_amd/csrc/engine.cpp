@@ -66,7 +66,8 @@ struct DevState {
   std::vector<ReqTables> reqs;
   double* S = nullptr;
   size_t S_bytes = 0;
-  double* R = nullptr;     // E-step partial [chain_estep_slab(M)] of nipamd_estep
+  double* R = nullptr;     // E-step partial [nipamd_estep_partial_size] of nipamd_estep
+  int R_size = 0;
   double* W = nullptr;     // E-step work: slabs + tree levels + chunk results + partial
   size_t W_bytes = 0;
   double* Q = nullptr;     // derived marginals: interface marginals / forward messages
@@ -109,12 +110,21 @@ int upload(double** dst, const V& v) {
   return 0;
 }
 
-// Upload the chain plan's tables to the current device (once per version).
-int ensure_tables(nipamd_model* mm) {
+// Bind the model's device state to the current device (a different device
+// drops every buffer of the old one).  Call before taking any DevState
+// pointer that a later ensure_* must not free.
+int ensure_device(nipamd_model* mm) {
   int dev = -1;
   HIP_OK(hipGetDevice(&dev));
   DevState* d = dev_of(mm);
   if (d->device != dev) { dev_release(d); d->device = dev; }
+  return 0;
+}
+
+// Upload the chain plan's tables to the current device (once per version).
+int ensure_tables(nipamd_model* mm) {
+  if (int rc = ensure_device(mm)) return rc;
+  DevState* d = dev_of(mm);
   if (d->version == mm->version && d->A64) return 0;
   const auto& P = mm->m.chain;
   free_tables(d);
@@ -352,6 +362,18 @@ int route_request(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_
   return 1;
 }
 
+// device buffers of a host-buffer call, freed on every return path
+struct DevBufs {
+  std::vector<void*> p;
+  template <typename T> int alloc(T** out, size_t n) {
+    *out = nullptr;
+    HIP_OK(hipMalloc(out, (n ? n : 1) * sizeof(T)));
+    p.push_back(*out);
+    return 0;
+  }
+  ~DevBufs() { for (void* q : p) (void)hipFree(q); }
+};
+
 }  // namespace
 
 namespace nipamd {
@@ -414,6 +436,7 @@ int nipamd_model_from_net(const char* path, nipamd_model** out) {
 void nipamd_model_free(nipamd_model* mm) {
   if (!mm) return;
   nipamd::generate_release(mm);
+  nipamd::jt_release(mm);
   DevState* d = static_cast<DevState*>(mm->m.dev);
   dev_release(d);
   delete d;
@@ -451,7 +474,24 @@ int nipamd_model_gpu_supported(const nipamd_model* mm, int n_obs, const int* obs
                                int n_query, const int* query) {
   if (!mm) return 0;
   Route r; std::string why;
-  return route_request(mm, n_obs, obs_vars, n_query, query, r, why);
+  if (mm->engine != NIPAMD_ENGINE_JTREE && route_request(mm, n_obs, obs_vars, n_query, query, r, why)) return 1;
+  return mm->engine != NIPAMD_ENGINE_CHAIN && nipamd::jt_supported(mm, n_obs, obs_vars, n_query, query, why);
+}
+
+int nipamd_jt_plan_dump(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
+                        const int* query, int estep, int* hdr, int hdr_cap, int* ip, long ip_cap,
+                        double* dp, long dp_cap, long* sizes) {
+  if (!mm || !hdr || !sizes || (n_obs > 0 && !obs_vars) || (n_query > 0 && !query))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  return nipamd::jt_plan_dump(mm, n_obs, obs_vars, n_query, query, estep, hdr, hdr_cap, ip, ip_cap, dp,
+                              dp_cap, sizes);
+}
+
+int nipamd_model_set_engine(nipamd_model* mm, int engine) {
+  if (!mm || engine < NIPAMD_ENGINE_AUTO || engine > NIPAMD_ENGINE_JTREE) return -1;
+  const int prev = mm->engine;
+  mm->engine = engine;
+  return prev;
 }
 
 int nipamd_model_original(const nipamd_model* mm, int c, double* out, int cap) {
@@ -496,24 +536,84 @@ int nipamd_m_step(nipamd_model* mm, const double* params) {
   return rc;
 }
 
-// One launch of the kernel family that serves route r: the interface
-// variable's marginals (smoothed, or filtered) into dst rows (dbs / dts /
-// doff), or only ll / status when dst is null.
-static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, const int32_t* d_obs, int n_obs,
-                      int B, int T, double* dst, long dbs, int dts, int doff,
-                      double* d_ll, uint32_t* d_status, void* stream, bool filt) {
+// Interface-chain kernel for a route, in order of preference; each kernel
+// stages the block's observation codes in LDS, so a long sequence may not fit
+// one and falls through to the next (the 64-state kernel last).  kNoChain:
+// no chain kernel fits -- the request goes to the general engine.
+enum ChainKernel { kNoChain = 0, kMfmaWide, kNarrowMfma, kNarrowDpp, kWide64 };
+
+static int pick_kernel(const nipamd_model* mm, const Route& r, const ReqTables* rt, int T, bool filt) {
   const auto& P = mm->m.chain;
-  DevState* d = dev_of(mm);
-  const long ocols = n_obs > 0 ? n_obs : 1;
   static const bool force_wide = [] {
     const char* e = std::getenv("NIPAMD_FB_KERNEL");
     return e && std::string(e) == "wide";
   }();
-  if ((!r.narrow || filt) && P.N <= 32 && !force_wide) {
+  if ((!r.narrow || filt) && P.N <= 32 && !force_wide &&
+      nipamd::chain_mfma_wide_lds_bytes(P.N <= 16 ? 1 : 2, rt->mtab_rows, r.ncol, T) <= 160 * 1024)
+    return kMfmaWide;
+  if (r.narrow && !filt) {
+    if (use_mfma() && nipamd::chain_mfma_lds_bytes(rt->M0, T) <= 160 * 1024) return kNarrowMfma;
+    if (nipamd::chain_lds_bytes(rt->M0, T, false) <= 96 * 1024) return kNarrowDpp;
+  }
+  if (nipamd::chain_wide_lds_bytes(r.ncol, T) <= 64 * 1024) return kWide64;
+  return kNoChain;
+}
+
+#ifdef NIPAMD_DIAGNOSTICS
+// Timing-only builds: per-block phase timestamps of the matrix-core fb kernel
+// (NIPAMD_PHASE_TIMES=1), printed as a summary after the launch.
+static void phase_report(const unsigned long long* h, int nblk) {
+  double sa = 0, sb = 0, sc = 0;
+  for (int k = 0; k < nblk; k++) {
+    sa += (double)(h[k * 4 + 1] - h[k * 4 + 0]);
+    sb += (double)(h[k * 4 + 2] - h[k * 4 + 1]);
+    sc += (double)(h[k * 4 + 3] - h[k * 4 + 2]);
+  }
+  std::fprintf(stderr, "[nipamd] phase cycles (mean over %d blocks): A %.0f  barrier %.0f  B %.0f\n",
+               nblk, sa / nblk, sb / nblk, sc / nblk);
+  double w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < nblk; k++)
+    for (int i = 0; i < 8; i++) w[i] += (double)h[(size_t)nblk * 4 + k * 8 + i];
+  if (w[0] + w[4] > 0)
+    std::fprintf(stderr, "[nipamd] barrier wait cycles A/B: fwd filter %.0f/%.0f  bwd filter %.0f/%.0f  "
+                 "fwd partner %.0f/%.0f  bwd partner %.0f/%.0f\n", w[0] / nblk, w[4] / nblk, w[1] / nblk,
+                 w[5] / nblk, w[2] / nblk, w[6] / nblk, w[3] / nblk, w[7] / nblk);
+  double pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < nblk; k++)
+    for (int i = 0; i < 8; i++) pp[i] += (double)h[(size_t)nblk * 16 + k * 8 + i];
+  if (pp[0] + pp[4] > 0)
+    std::fprintf(stderr, "[nipamd] phase-B partner cycles (DMA wait / ll / drain): fwd %.0f/%.0f/%.0f  "
+                 "bwd %.0f/%.0f/%.0f\n", pp[0] / nblk, pp[1] / nblk, pp[2] / nblk, pp[4] / nblk, pp[5] / nblk,
+                 pp[6] / nblk);
+  const unsigned long long* rt = h + (size_t)nblk * 12;   // s_memrealtime (100 MHz)
+  unsigned long long t0 = ~0ull, e0 = 0, e1 = ~0ull, s1 = 0;
+  double mhz = 0, me = 0, st0 = 0;
+  for (int k = 0; k < nblk; k++) {
+    t0 = std::min(t0, rt[k * 4 + 0]); s1 = std::max(s1, rt[k * 4 + 0]);
+    e0 = std::max(e0, rt[k * 4 + 2]); e1 = std::min(e1, rt[k * 4 + 2]);
+    me += (double)(rt[k * 4 + 2] - rt[k * 4 + 0]);
+    st0 += (double)(h[k * 4] - rt[k * 4 + 1]);
+    if (rt[k * 4 + 2] > rt[k * 4 + 0])
+      mhz += 100.0 * (double)(rt[k * 4 + 3] - rt[k * 4 + 1]) / (double)(rt[k * 4 + 2] - rt[k * 4 + 0]);
+  }
+  std::fprintf(stderr, "[nipamd] wall us: last entry %.2f  first end %.2f  last end %.2f  mean block %.2f  "
+               "clock %.0f MHz; entry->stamp0 cycles %.0f\n", (s1 - t0) / 100.0, (e1 - t0) / 100.0,
+               (e0 - t0) / 100.0, me / nblk / 100.0, mhz / nblk, st0 / nblk);
+}
+#endif
+
+// One launch of the chain kernel `kind` for route r: the interface
+// variable's marginals (smoothed, or filtered) into dst rows (dbs / dts /
+// doff), or only ll / status when dst is null.
+static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind, const int32_t* d_obs,
+                      int n_obs, int B, int T, double* dst, long dbs, int dts, int doff,
+                      double* d_ll, uint32_t* d_status, void* stream, bool filt) {
+  const auto& P = mm->m.chain;
+  DevState* d = dev_of(mm);
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  if (kind == kMfmaWide) {
     // matrix-core interface chain: N <= 32, up to four observed children
     const int NT = P.N <= 16 ? 1 : 2;
-    if (nipamd::chain_mfma_wide_lds_bytes(NT, rt->mtab_rows, r.ncol, T) > 160 * 1024)
-      return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
     if (int rc = ensure_scratch(mm, filt ? 64 * sizeof(double) : nipamd::chain_mfma_wide_scratch_bytes(NT, B, T)))
       return rc;
     nipamd::WideMfmaArgs w{};
@@ -534,10 +634,8 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, const int
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return 0;
   }
-  if (!r.narrow) {
+  if (kind == kWide64) {
     // wide interface chain: N <= 64, up to four observed children
-    if (nipamd::chain_wide_lds_bytes(r.ncol, T) > 64 * 1024)
-      return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
     if (int rc = ensure_scratch(mm, filt ? 64 * sizeof(double)
                                          : (size_t)(B + 2) * nipamd::chain_scratch_row64(T) * sizeof(double)))
       return rc;
@@ -560,16 +658,15 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, const int
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return 0;
   }
-  const int M0 = rt->M0;
-  if (nipamd::chain_lds_bytes(M0, T, false) > 96 * 1024)
-    return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long for the LDS-resident observation codes");
+  if (kind != kNarrowMfma && kind != kNarrowDpp)
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "no interface-chain kernel fits this request");
   if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes(B, T))) return rc;
   nipamd::ChainArgs a{};
   a.obs = r.pcol >= 0 ? d_obs : nullptr;
   a.obs_bstride = (long)T * ocols;
   a.obs_tstride = (int)ocols;
   a.obs_col = r.pcol;
-  a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = M0;
+  a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = rt->M0;
   a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
   a.post = dst;
   a.post_bstride = dbs;
@@ -577,67 +674,29 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, const int
   a.post_off = doff;
   a.ll = d_ll;
   a.status = d_status;
-  {
-    const bool mf = use_mfma() && nipamd::chain_mfma_lds_bytes(M0, T) <= 160 * 1024;
-    // diagnostics: NIPAMD_PHASE_TIMES=1 records per-block phase timestamps
-    // (start / end of phase A / start of phase B / end) and prints a summary
-    static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
-    unsigned long long* dst = nullptr;
-    const int nblk = (int)((B + 15) / 16);
-    if (mf && times) {
-      HIP_OK(hipMalloc(&dst, (size_t)nblk * 24 * sizeof(unsigned long long)));
-      HIP_OK(hipMemsetAsync(dst, 0, (size_t)nblk * 24 * sizeof(unsigned long long), (hipStream_t)stream));
-      a.counts = reinterpret_cast<double*>(dst);
-    }
-    const int rc = mf ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
-                      : nipamd::chain_fb_launch(a, (hipStream_t)stream);
-    a.counts = nullptr;
-    if (dst) {
-      std::vector<unsigned long long> h((size_t)nblk * 24);
-      HIP_OK(hipStreamSynchronize((hipStream_t)stream));
-      HIP_OK(hipMemcpy(h.data(), dst, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      (void)hipFree(dst);
-      double sa = 0, sb = 0, sc = 0;
-      for (int k = 0; k < nblk; k++) {
-        sa += (double)(h[k * 4 + 1] - h[k * 4 + 0]);
-        sb += (double)(h[k * 4 + 2] - h[k * 4 + 1]);
-        sc += (double)(h[k * 4 + 3] - h[k * 4 + 2]);
-      }
-      std::fprintf(stderr, "[nipamd] phase cycles (mean over %d blocks): A %.0f  barrier %.0f  B %.0f\n",
-                   nblk, sa / nblk, sb / nblk, sc / nblk);
-      double w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int k = 0; k < nblk; k++)
-        for (int i = 0; i < 8; i++) w[i] += (double)h[(size_t)nblk * 4 + k * 8 + i];
-      if (w[0] + w[4] > 0)
-        std::fprintf(stderr, "[nipamd] barrier wait cycles A/B: fwd filter %.0f/%.0f  bwd filter %.0f/%.0f  "
-                     "fwd partner %.0f/%.0f  bwd partner %.0f/%.0f\n", w[0] / nblk, w[4] / nblk, w[1] / nblk,
-                     w[5] / nblk, w[2] / nblk, w[6] / nblk, w[3] / nblk, w[7] / nblk);
-      double pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int k = 0; k < nblk; k++)
-        for (int i = 0; i < 8; i++) pp[i] += (double)h[(size_t)nblk * 16 + k * 8 + i];
-      if (pp[0] + pp[4] > 0)
-        std::fprintf(stderr, "[nipamd] phase-B partner cycles (DMA wait / ll / drain): fwd %.0f/%.0f/%.0f  "
-                     "bwd %.0f/%.0f/%.0f\n", pp[0] / nblk, pp[1] / nblk, pp[2] / nblk, pp[4] / nblk, pp[5] / nblk,
-                     pp[6] / nblk);
-      // wall-clock view (s_memrealtime, 100 MHz): block entry and partner end
-      const unsigned long long* rt = h.data() + (size_t)nblk * 12;
-      unsigned long long t0 = ~0ull, e0 = 0, e1 = ~0ull, s1 = 0;
-      double mhz = 0, me = 0;
-      for (int k = 0; k < nblk; k++) {
-        t0 = std::min(t0, rt[k * 4 + 0]); s1 = std::max(s1, rt[k * 4 + 0]);
-        e0 = std::max(e0, rt[k * 4 + 2]); e1 = std::min(e1, rt[k * 4 + 2]);
-        me += (double)(rt[k * 4 + 2] - rt[k * 4 + 0]);
-        if (rt[k * 4 + 2] > rt[k * 4 + 0])
-          mhz += 100.0 * (double)(rt[k * 4 + 3] - rt[k * 4 + 1]) / (double)(rt[k * 4 + 2] - rt[k * 4 + 0]);
-      }
-      std::fprintf(stderr, "[nipamd] wall us: last entry %.2f  first end %.2f  last end %.2f  mean block %.2f  "
-                   "clock %.0f MHz; entry->stamp0 cycles %.0f\n", (s1 - t0) / 100.0, (e1 - t0) / 100.0,
-                   (e0 - t0) / 100.0, me / nblk / 100.0, mhz / nblk,
-                   [&] { double x = 0; for (int k = 0; k < nblk; k++) x += (double)(h[k * 4] - rt[k * 4 + 1]); return x / nblk; }());
-    }
-    if (rc)
-      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+#ifdef NIPAMD_DIAGNOSTICS
+  static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
+  unsigned long long* stamps = nullptr;
+  const int nblk = (int)((B + 15) / 16);
+  if (kind == kNarrowMfma && times) {
+    HIP_OK(hipMalloc(&stamps, (size_t)nblk * 24 * sizeof(unsigned long long)));
+    HIP_OK(hipMemsetAsync(stamps, 0, (size_t)nblk * 24 * sizeof(unsigned long long), (hipStream_t)stream));
+    a.counts = reinterpret_cast<double*>(stamps);
   }
+#endif
+  const int rc = kind == kNarrowMfma ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
+                                     : nipamd::chain_fb_launch(a, (hipStream_t)stream);
+#ifdef NIPAMD_DIAGNOSTICS
+  if (stamps) {
+    std::vector<unsigned long long> h((size_t)nblk * 24);
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    HIP_OK(hipMemcpy(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    (void)hipFree(stamps);
+    phase_report(h.data(), nblk);
+  }
+#endif
+  if (rc)
+    return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   return 0;
 }
 
@@ -656,12 +715,24 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
   if (B == 0) return 0;
   Route r;
   std::string why;
-  if (!route_request(mm, n_obs, obs_vars, n_query, query, r, why))
-    return fail(NIPAMD_ERROR_UNSUPPORTED, why);
-  const auto& P = mm->m.chain;
-  if (int rc = ensure_tables(mm)) return rc;
+  int kk = kNoChain;
   ReqTables* rt = nullptr;
-  if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
+  if (mm->engine != NIPAMD_ENGINE_JTREE && route_request(mm, n_obs, obs_vars, n_query, query, r, why)) {
+    if (int rc = ensure_tables(mm)) return rc;
+    if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
+    kk = pick_kernel(mm, r, rt, T, filt);
+    // smoothed hidden parents also need the forward messages of a filter pass
+    for (int i = 0; i < n_query && kk != kNoChain && !filt; i++)
+      if (query_kind(mm->m.chain, query[i]) >= 1000 && pick_kernel(mm, r, rt, T, true) == kNoChain) kk = kNoChain;
+    if (kk == kNoChain) why = "sequence too long for the interface-chain kernels' LDS-resident codes";
+  }
+  if (kk == kNoChain) {
+    // the general join-tree engine (jtree.hip): any slice, any T
+    if (mm->engine == NIPAMD_ENGINE_CHAIN) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+    return nipamd::jt_fb(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_status,
+                         stream, filt);
+  }
+  const auto& P = mm->m.chain;
   std::vector<int> kind(n_query), off(n_query);
   int stride = 0, first_cur = -1;
   bool derived = false, fwd_msgs = false;
@@ -692,14 +763,15 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
   bool first = true;
   for (int i = 0; i < n_query; i++) {
     if (kind[i] != 0) continue;
-    if (int rc = launch_cur(mm, r, rt, d_obs, n_obs, B, T, d_post, pbs, stride, off[i],
+    if (int rc = launch_cur(mm, r, rt, kk, d_obs, n_obs, B, T, d_post, pbs, stride, off[i],
                             first ? d_ll : nullptr, first ? d_status : nullptr, stream, filt)) return rc;
     first = false;
   }
   if (first)       // no query slot names the interface variable
-    if (int rc = launch_cur(mm, r, rt, d_obs, n_obs, B, T, cur, cbs, cts, 0, d_ll, d_status, stream, filt)) return rc;
+    if (int rc = launch_cur(mm, r, rt, kk, d_obs, n_obs, B, T, cur, cbs, cts, 0, d_ll, d_status, stream, filt)) return rc;
   if (fwd_msgs)    // the forward messages: a filter pass
-    if (int rc = launch_cur(mm, r, rt, d_obs, n_obs, B, T, fwd, (long)T * N, N, 0, nullptr, nullptr, stream, true))
+    if (int rc = launch_cur(mm, r, rt, pick_kernel(mm, r, rt, T, true), d_obs, n_obs, B, T, fwd, (long)T * N, N, 0,
+                            nullptr, nullptr, stream, true))
       return rc;
   if (!derived) return 0;
   DevState* d = dev_of(mm);
@@ -760,17 +832,21 @@ int nipamd_filter(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* 
 static int fb_host_impl(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,
                         int B, int T, int n_query, const int* query, double* post,
                         double* ll, uint32_t* status, bool filt) {
-  if (!mm || B < 0 || T < 1) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (!mm || B < 0 || T < 1 || n_query < 0 || (n_query > 0 && !query) || (n_obs > 0 && (!obs || !obs_vars)))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  for (int i = 0; i < n_query; i++)
+    if (query[i] < 0 || query[i] >= (int)mm->m.vars.size()) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad query variable");
   if (B == 0) return 0;
   int stride = 0;
   for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
+  DevBufs db;
   int32_t* d_obs = nullptr; double* d_post = nullptr; double* d_ll = nullptr; uint32_t* d_st = nullptr;
   const size_t nob = (size_t)B * T * (n_obs > 0 ? n_obs : 1);
   const size_t npo = (size_t)B * T * (stride > 0 ? stride : 1);
-  HIP_OK(hipMalloc(&d_obs, nob * sizeof(int32_t)));
-  HIP_OK(hipMalloc(&d_post, npo * sizeof(double)));
-  HIP_OK(hipMalloc(&d_ll, (size_t)B * sizeof(double)));
-  HIP_OK(hipMalloc(&d_st, (size_t)B * sizeof(uint32_t)));
+  if (int rc = db.alloc(&d_obs, nob)) return rc;
+  if (int rc = db.alloc(&d_post, npo)) return rc;
+  if (int rc = db.alloc(&d_ll, (size_t)B)) return rc;
+  if (int rc = db.alloc(&d_st, (size_t)B)) return rc;
   if (n_obs > 0) HIP_OK(hipMemcpy(d_obs, obs, nob * sizeof(int32_t), hipMemcpyHostToDevice));
   int rc = fb_impl(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_st, nullptr, filt);
   if (rc == 0) {
@@ -779,7 +855,6 @@ static int fb_host_impl(nipamd_model* mm, const int32_t* obs, int n_obs, const i
     if (ll) HIP_OK(hipMemcpy(ll, d_ll, (size_t)B * sizeof(double), hipMemcpyDeviceToHost));
     if (status) HIP_OK(hipMemcpy(status, d_st, (size_t)B * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
-  (void)hipFree(d_obs); (void)hipFree(d_post); (void)hipFree(d_ll); (void)hipFree(d_st);
   return rc;
 }
 
@@ -795,9 +870,24 @@ int nipamd_filter_host(nipamd_model* mm, const int32_t* obs, int n_obs, const in
   return fb_host_impl(mm, obs, n_obs, obs_vars, B, T, n_query, query, post, ll, status, true);
 }
 
+// The chain e_step kernel serves the HMM slice with evidence on its child
+// only; every other e_step runs on the general engine, whose partial is the
+// em_learn layout itself.  The partial buffer holds either (the larger of the
+// two sizes); the route of the last partial decides the finalize.
 int nipamd_estep_partial_size(const nipamd_model* mm) {
-  if (!mm || !mm->m.chain.valid || !mm->m.chain.hmm) return -1;
-  return nipamd::chain_estep_slab(mm->m.chain.emits[0].M);
+  if (!mm) return -1;
+  const int ps = nipamd::param_size(mm->m);
+  if (mm->engine != NIPAMD_ENGINE_JTREE && mm->m.chain.valid && mm->m.chain.hmm)
+    return std::max(ps, nipamd::chain_estep_slab(mm->m.chain.emits[0].M));
+  return mm->engine == NIPAMD_ENGINE_CHAIN ? -1 : ps;
+}
+
+static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r) {
+  std::string why;
+  if (mm->engine == NIPAMD_ENGINE_JTREE || !mm->m.chain.valid || !mm->m.chain.hmm) return false;
+  if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why)) return false;
+  if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0)) return false;   // evidence on the child only
+  return nipamd::chain_lds_bytes(mm->m.chain.emits[0].M, T, true) <= 96 * 1024;
 }
 
 int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
@@ -806,18 +896,18 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   if (!mm || B < 0 || T < 1 || !d_partial || (n_obs > 0 && (!d_obs || !obs_vars)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   Route r;
-  std::string why;
-  if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why))
-    return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+  if (!chain_estep_ok(mm, n_obs, obs_vars, T, r)) {
+    if (mm->engine == NIPAMD_ENGINE_CHAIN)
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step covers the HMM slice with evidence on its child");
+    std::string why;
+    if (!nipamd::jt_supported(mm, n_obs, obs_vars, 0, nullptr, why)) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
+    mm->estep_route = 1;
+    return nipamd::jt_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream);
+  }
+  mm->estep_route = 0;
   const auto& P = mm->m.chain;
-  if (!P.hmm)
-    return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice (prev, cur, one child)");
-  if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0))
-    return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan: evidence on the observed child only");
   const int col = r.pcol;
   const int Mo = P.emits[0].M;
-  if (nipamd::chain_lds_bytes(Mo, T, true) > 96 * 1024)
-    return fail(NIPAMD_ERROR_UNSUPPORTED, "sequence too long / observation cardinality too large for the LDS count tables");
   const int S = nipamd::chain_estep_slab(Mo);
   hipStream_t st = (hipStream_t)stream;
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
@@ -864,6 +954,7 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
 
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (mm->estep_route == 1) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
   const auto& P = mm->m.chain;
   if (!P.valid || !P.hmm) return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
   if (int rc = ensure_tables(mm)) return rc;
@@ -893,10 +984,16 @@ int nipamd_estep(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* o
                  int B, int T, double* d_counts, double* d_ll, uint32_t* d_status, void* stream) {
   if (!mm || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   const int S = nipamd_estep_partial_size(mm);
-  if (S < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "model slice is not chain-shaped (GPU plan: HMM-shaped DBN)");
-  if (int rc = ensure_tables(mm)) return rc;
+  if (S < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "no e_step plan for this model under the selected engine");
+  if (int rc = ensure_device(mm)) return rc;
   DevState* d = dev_of(mm);
-  if (!d->R) HIP_OK(hipMalloc(&d->R, (size_t)S * sizeof(double)));
+  if (d->R_size < S) {
+    (void)hipFree(d->R);
+    d->R = nullptr;
+    d->R_size = 0;
+    HIP_OK(hipMalloc(&d->R, (size_t)S * sizeof(double)));
+    d->R_size = S;
+  }
   double* part = d->R;
   int rc = nipamd_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, part, d_ll, d_status, stream);
   if (rc) return rc;

@@ -99,8 +99,9 @@ struct Model {
   std::vector<int> outgoing, previous_outgoing, independent, children;
 
   ChainPlan chain;
-  // device-side state (engine.cpp)
+  // device-side state (engine.cpp) and the general engine's caches (jtree_plan.cpp)
   void* dev = nullptr;
+  void* jt = nullptr;
 };
 
 // compile.cpp
@@ -132,9 +133,24 @@ int write_net_file(const Model& m, const std::string& path, std::string& err);
 struct nipamd_model {
   nipamd::Model m;
   unsigned version = 1;          // bumped whenever the tables change
+  int engine = 0;                // NIPAMD_ENGINE_* (nipamd_model_set_engine)
+  int estep_route = 0;           // layout of the last e_step partial: 0 chain, 1 general
 };
 
 namespace nipamd {
 // generate.cpp: drop a model's cached generate_data tables (nipamd_model_free)
 void generate_release(const nipamd_model* mm);
+// jtree_plan.cpp: the general join-tree engine (jtree.h)
+int jt_supported(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
+                 const int* query, std::string& why);
+int jt_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T,
+          int n_query, const int* query, double* d_post, double* d_ll, uint32_t* d_status,
+          void* stream, bool filt);
+int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B,
+                     int T, double* d_partial, double* d_ll, uint32_t* d_status, void* stream);
+int jt_estep_finalize(const nipamd_model* mm, const double* d_partial, double* d_counts, void* stream);
+void jt_release(nipamd_model* mm);
+int jt_plan_dump(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query, const int* query,
+                 int estep, int* hdr, int hdr_cap, int* ip, long ip_cap, double* dp, long dp_cap,
+                 long* sizes);
 }  // namespace nipamd

@@ -76,6 +76,50 @@ def wide_spec(card: int = 64, obs_card: int = 16, seed: int = 12345):
     return nodes, pots
 
 
+def factorial_spec(a: int = 4, b: int = 3, m: int = 5, seed: int = 12345):
+    """Factorial HMM: two hidden chains X (a states) and Y (b states) with one
+    observation O1 of both -- a two-variable interface {X1, Y1} (general
+    join-tree engine)."""
+    nodes = [("X0", a, "X1"), ("Y0", b, "Y1"), ("X1", a, None), ("Y1", b, None), ("O1", m, None)]
+    pots = [
+        ("X1", ["X0"], cpt(seed, a, a)),
+        ("Y1", ["Y0"], cpt(seed + 1, b, b)),
+        ("O1", ["X1", "Y1"], cpt(seed + 2, m, a * b)),
+        ("X0", [], cpt(seed + 3, a, 1)),
+        ("Y0", [], cpt(seed + 4, b, 1)),
+    ]
+    return nodes, pots
+
+
+def coupled_spec(a: int = 3, b: int = 4, m: int = 3, seed: int = 12345):
+    """Two coupled chains: X1 | X0 Y0 and Y1 | Y0 X0, each with its own
+    observed child (A1 | X1, B1 | Y1)."""
+    nodes = [("X0", a, "X1"), ("Y0", b, "Y1"), ("X1", a, None), ("Y1", b, None),
+             ("A1", m, None), ("B1", m + 1, None)]
+    pots = [
+        ("X1", ["X0", "Y0"], cpt(seed, a, a * b)),
+        ("Y1", ["Y0", "X0"], cpt(seed + 1, b, a * b)),
+        ("A1", ["X1"], cpt(seed + 2, m, a)),
+        ("B1", ["Y1"], cpt(seed + 3, m + 1, b)),
+        ("X0", [], cpt(seed + 4, a, 1)),
+        ("Y0", [], cpt(seed + 5, b, 1)),
+    ]
+    return nodes, pots
+
+
+def nonleaf_spec(n: int = 4, m: int = 3, k: int = 3, seed: int = 12345):
+    """HMM whose observation O1 has an observed child Q1 of its own (a
+    non-leaf observed variable)."""
+    nodes = [("P0", n, "P1"), ("P1", n, None), ("O1", m, None), ("Q1", k, None)]
+    pots = [
+        ("P1", ["P0"], cpt(seed, n, n)),
+        ("O1", ["P1"], cpt(seed + 1, m, n)),
+        ("Q1", ["O1"], cpt(seed + 2, k, m)),
+        ("P0", [], cpt(seed + 3, n, 1)),
+    ]
+    return nodes, pots
+
+
 def observations(B: int, T: int, card: int, seed: int = 1, n_obs: int = 1) -> np.ndarray:
     """int32 [B, T, n_obs] uniform states."""
     u = splitmix64(seed, B * T * n_obs) % np.uint64(card)

@@ -87,10 +87,20 @@ def test_chain_plan_recognition():
     assert d.gpu_supported([d.variable("B1")], [d.variable("C1")])
     # every variable of the slice can be queried (derived marginals: prev, hidden parent, children)
     assert d.gpu_supported([d.variable("A1")], [d.variable(v) for v in ("D1", "C0", "B1", "A1")])
-    assert not d.gpu_supported([d.variable("D1")], [d.variable("C1")])      # evidence on a folded parent
+    # evidence on a folded parent: outside the chain plan, served by the general engine
+    d.set_engine(nip_amd.ENGINE_CHAIN)
+    assert not d.gpu_supported([d.variable("D1")], [d.variable("C1")])
+    d.set_engine(nip_amd.ENGINE_AUTO)
+    assert d.gpu_supported([d.variable("D1")], [d.variable("C1")])
     # a slice with two interface variables is not an interface chain
     nodes = [("a0", 2, "a1"), ("b0", 2, "b1"), ("a1", 2, None), ("b1", 2, None), ("o", 2, None)]
     pots = [("a0", [], None), ("b0", [], None), ("a1", ["a0"], None), ("b1", ["b0", "a1"], None),
             ("o", ["b1"], None)]
     w = nip_amd.Model.from_spec(nodes, pots)
+    w.set_engine(nip_amd.ENGINE_CHAIN)
     assert not w.gpu_supported([w.variable("o")], [w.variable("a1")])
+    assert not w.estep_supported()
+    w.set_engine(nip_amd.ENGINE_AUTO)
+    assert w.gpu_supported([w.variable("o")], [w.variable("a1")])
+    assert w.estep_supported()
+    assert w.set_engine(nip_amd.ENGINE_JTREE) == nip_amd.ENGINE_AUTO
