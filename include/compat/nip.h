@@ -1,33 +1,45 @@
 /*
- * nip.h -- drop-in for the reference's time-series API (src/nip.h) on the
- * nip_amd GPU engine: libnip.so (nip_amd/compat/compat.cpp).
+ * nip.h -- drop-in for the reference's src/nip.h on the nip_amd GPU engine:
+ * libnip.so (the sources under nip_amd/compat).
  *
  * Programs written against the reference's nip.h -- util/nipinference.c,
- * util/nipmap.c, util/niptrain.c -- compile unmodified against this header
- * and link against libnip.so instead of the reference's objects.  The structs
- * a caller reads directly keep the reference's field order and types
- * (nip_model_struct nip.h:71-104, time_series_struct nip.h:112-122,
- * uncertain_series_struct nip.h:131-136, nip_variable_struct
- * nipvariable.h:51-78).  The join tree is compiled and held by the engine
- * (an nipamd_model behind each nip_model), so the clique fields are opaque
- * and the potential / join-tree API of nippotential.h / nipjointree.h is not
- * part of this layer.
+ * nipmap.c, niptrain.c, nipsample.c, niplikelihood.c, nipjoint.c -- compile
+ * unmodified against this header and link against libnip.so instead of the
+ * reference's objects.  The structs a caller reads directly keep the
+ * reference's field order and types (nip_model_struct nip.h:71-104,
+ * time_series_struct nip.h:112-122, uncertain_series_struct nip.h:131-136),
+ * and a parsed model carries a real join tree (model->cliques, in_clique,
+ * out_clique; nipjointree.h) with the reference's clique order, variable
+ * order, sepset lists and tables.
  *
- * forward_inference / forward_backward_inference / em_learn run on the GPU
- * (nipamd_filter / nipamd_fb / nipamd_em_learn); a model without a GPU plan
- * for the request fails with NULL / an error code -- there is no CPU path.
+ * Where the work goes:
+ *   forward_inference / forward_backward_inference / em_learn / generate_data
+ *       the batched GPU engine (nipamd_filter / nipamd_fb / nipamd_em_learn /
+ *       nipamd_generate); a model without a GPU plan for the request fails
+ *       with NULL / an error code -- there is no CPU path
+ *   make_consistent (and insert_hard/soft_evidence, which end with it)
+ *       GPU Hugin propagation over the model's tables (nipamd_hugin_passes)
+ *   reset_model / use_priors / insert_*_step / model_prob_mass /
+ *   get_probability / get_joint_probability
+ *       the reference's bookkeeping over the host tables (nipjointree.h)
  */
 #ifndef NIP_AMD_COMPAT_NIP_H
 #define NIP_AMD_COMPAT_NIP_H
 
+#include <assert.h>
 #include <float.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "niperrorhandler.h"
+#include "nipjointree.h"
 #include "niplists.h"
+#include "nipparsers.h"
+#include "nippotential.h"
 #include "nipvariable.h"
 
 #ifdef __cplusplus
@@ -42,12 +54,9 @@ extern "C" {
 enum nip_direction_type { BACKWARD, FORWARD };
 typedef enum nip_direction_type nip_direction;
 
-/* the join tree is the engine's: cliques are opaque here */
-typedef struct nip_clique_type* nip_clique;
-
 typedef struct {
   int num_of_cliques;
-  nip_clique* cliques;                      /* NULL */
+  nip_clique* cliques;
   int num_of_vars;
   nip_variable* variables;
   int num_of_nexts;
@@ -58,8 +67,8 @@ typedef struct {
   nip_variable* previous_outgoing_interface;
   int incoming_interface_size;
   nip_variable* incoming_interface;
-  nip_clique in_clique;                     /* NULL */
-  nip_clique out_clique;                    /* NULL */
+  nip_clique in_clique;
+  nip_clique out_clique;
   int num_of_children;
   nip_variable* children;
   nip_variable* independent;
@@ -86,6 +95,19 @@ typedef struct {
   double*** data;                           /* data[t][i][state] */
 } uncertain_series_struct;
 typedef uncertain_series_struct* uncertain_series;
+
+/* the single-slice state (src/nip.c:61-119, 951-1027, 1600-1617, 2254-2321) */
+void reset_model(nip_model model);
+void total_reset(nip_model model);
+void use_priors(nip_model model, int has_history);
+int insert_hard_evidence(nip_model model, char* varname, char* observation);
+int insert_soft_evidence(nip_model model, char* varname, double* distribution);
+int insert_ts_step(time_series ts, int t, nip_model model, char mark_mask);
+int insert_ucs_step(uncertain_series ucs, int t, nip_model model, char mark_mask);
+void make_consistent(nip_model model);
+double model_prob_mass(nip_model model);
+double* get_probability(nip_model model, nip_variable v);
+nip_potential get_joint_probability(nip_model model, nip_variable* vars, int num_of_vars);
 
 nip_model parse_model(char* file);
 int write_model(nip_model model, char* filename);

@@ -250,6 +250,24 @@ int nipamd_write_model(const nipamd_model* m, const char* path);
 /* Current clique original table / prior of an independent variable. */
 int nipamd_model_original(const nipamd_model* m, int clique, double* out, int cap);
 int nipamd_model_prior(const nipamd_model* m, int v, double* out);
+/* The compiled join tree: clique c's variables
+ * (ascending ID = model index order) and its sepset list in the reference's
+ * list order (nipjointree.c:211-234); sepset s's neighbours (first, second)
+ * and variables (the first neighbour's order, nipvariable.c:506-557); the
+ * in / out cliques of src/nip.c:249-264 (-1 without an interface).  Arrays
+ * need room for the model's variable / sepset counts. */
+int nipamd_model_num_cliques(const nipamd_model* m);
+int nipamd_model_num_sepsets(const nipamd_model* m);
+int nipamd_model_clique(const nipamd_model* m, int c, int* vars, int* n_vars, int* links, int* n_links);
+int nipamd_model_sepset(const nipamd_model* m, int s, int* a, int* b, int* vars, int* n_vars);
+int nipamd_model_interface_cliques(const nipamd_model* m, int* in_clique, int* out_clique);
+/* Replace the model's tables: originals[c] (NULL: keep) is clique c's
+ * original_p, priors[v] (NULL: keep; ignored for variables with parents) the
+ * prior of variable v.  What a caller of the reference achieves by writing
+ * clique->original_p / nip_set_prior before inference; libnip.so forwards
+ * such edits of its host join tree before every engine call. */
+int nipamd_model_set_tables(nipamd_model* m, int n_cliques, const double* const* originals,
+                            int n_vars, const double* const* priors);
 
 /* Last error message (thread-local), for diagnostics. */
 const char* nipamd_last_error(void);
@@ -335,6 +353,30 @@ int nipamd_likelihood(nipamd_model* m, const int32_t* d_obs, int n_obs, const in
                       void* stream);
 int nipamd_likelihood_host(nipamd_model* m, const int32_t* obs, int n_obs, const int* obs_vars,
                            const int* marked, int B, int T, double* m1, double* m2, double* ll);
+
+/*
+ * Hugin message passes on the GPU over explicit potential tables: the
+ * propagation under libnip.so's single-slice API (nip_collect_evidence /
+ * nip_distribute_evidence, src/nipjointree.c:580-673; make_consistent,
+ * src/nip.c:1600-1617), which records the passes of the reference's
+ * traversal and hands them here.
+ *   tables[k]   host pointer to table k (flat, dimension 0 fastest,
+ *               src/nippotential.c:58-68); ndim[k] dimensions with the
+ *               cardinalities concatenated in card[] (table after table)
+ *   passes[6p]  (src, s_new, s_old, dst, map_src, map_dst) for pass p =
+ *               nip_message_pass(src, s, dst) (nipjointree.c:676-709):
+ *                 s_new := marginalise(src) onto the sepset
+ *                          (nip_general_marginalise, nippotential.c:267-311)
+ *                 dst   *= s_new / s_old, 0 where s_old is 0
+ *                          (nip_update_potential, :436-496)
+ *               maps[map_src ...] / maps[map_dst ...]: the position of each
+ *               sepset dimension in src / dst (nip_mapper)
+ * Passes run in order with the reference's arithmetic, so the tables end
+ * bit-identical to the reference's.  Synchronous: the tables are read before
+ * and the written ones (s_new, dst) copied back after.
+ */
+int nipamd_hugin_passes(int n_tables, double* const* tables, const int* ndim, const int* card,
+                        int n_passes, const int* passes, const int* maps);
 
 #ifdef __cplusplus
 }

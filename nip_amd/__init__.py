@@ -58,7 +58,9 @@ EXPORTS = [
     "nipamd_model_var_label", "nipamd_model_var_info",
     "nipamd_generate_order", "nipamd_generate", "nipamd_generate_host", "nipamd_rand_windows",
     "nipamd_generate_host_draws", "nipamd_likelihood", "nipamd_likelihood_host",
-    "nipamd_model_set_engine", "nipamd_jt_plan_dump",
+    "nipamd_model_set_engine", "nipamd_jt_plan_dump", "nipamd_hugin_passes",
+    "nipamd_model_num_cliques", "nipamd_model_num_sepsets", "nipamd_model_clique",
+    "nipamd_model_sepset", "nipamd_model_interface_cliques", "nipamd_model_set_tables",
 ]
 
 

@@ -96,16 +96,28 @@ COMPAT_LIB = os.path.join(LIB_DIR, "libnip.so")
 # compat headers and linked with libnip.so (drop-in check, oracle/_ref is
 # git-ignored; only built where /root/reference exists)
 REF_UTIL = os.environ.get("NIPAMD_REF_UTIL", "/root/reference/util")
-REF_PROGRAMS = ["nipinference", "nipmap", "niptrain", "nipsample"]
+REF_PROGRAMS = ["nipinference", "nipmap", "niptrain", "nipsample", "niplikelihood", "nipjoint"]
 REF_BIN_DIR = os.path.join(ROOT, "oracle", "_ref", "compat")
+REF_TEST = os.environ.get("NIPAMD_REF_TEST", "/root/reference/test")
+REF_TESTS = ["cliquetest", "potentialtest"]
+TEST_BIN_DIR = os.path.join(ROOT, "tests", "_bin")
 
 
 def build_compat(verbose: bool = False):
     """libnip.so: the reference's nip.h API over the engine (nip_amd/compat)."""
     inc = ["-I" + os.path.join(ROOT, "include", "compat"), "-I" + os.path.join(ROOT, "include")]
     cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-fPIC", "-shared", *inc,
-           os.path.join(PKG, "compat", "compat.cpp"), "-L" + LIB_DIR, "-lnip_amd",
+           *sorted(glob.glob(os.path.join(PKG, "compat", "*.cpp"))), "-L" + LIB_DIR, "-lnip_amd",
            "-Wl,-rpath,$ORIGIN", "-o", COMPAT_LIB]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    # test driver over libnip.so (tests/capi; test infrastructure, not shipped)
+    os.makedirs(TEST_BIN_DIR, exist_ok=True)
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-std=gnu99", "-Wall", *inc,
+           "-I" + os.path.join(ROOT, "oracle", "ref"), os.path.join(ROOT, "tests", "capi", "slice_driver.c"),
+           "-L" + LIB_DIR, "-lnip", "-lnip_amd", "-lm", "-Wl,-rpath," + LIB_DIR,
+           "-Wl,-rpath,$ORIGIN/../../nip_amd/_lib", "-o", os.path.join(TEST_BIN_DIR, "slice_driver")]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
@@ -114,6 +126,15 @@ def build_compat(verbose: bool = False):
     os.makedirs(REF_BIN_DIR, exist_ok=True)
     for p in REF_PROGRAMS:
         cmd = [os.environ.get("CC", "gcc"), "-O2", "-w", *inc, os.path.join(REF_UTIL, p + ".c"),
+               "-L" + LIB_DIR, "-lnip", "-lnip_amd", "-lm", "-Wl,-rpath," + LIB_DIR,
+               "-Wl,-rpath,$ORIGIN/../../../nip_amd/_lib", "-o", os.path.join(REF_BIN_DIR, p)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    # the reference's unit-test programs over libnip.so (expected outputs: the
+    # same programs over the reference's sources, oracle/Makefile reftests)
+    for p in REF_TESTS:
+        cmd = [os.environ.get("CC", "gcc"), "-O2", "-w", *inc, os.path.join(REF_TEST, p + ".c"),
                "-L" + LIB_DIR, "-lnip", "-lnip_amd", "-lm", "-Wl,-rpath," + LIB_DIR,
                "-Wl,-rpath,$ORIGIN/../../../nip_amd/_lib", "-o", os.path.join(REF_BIN_DIR, p)]
         if verbose:

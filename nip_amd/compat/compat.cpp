@@ -1,18 +1,23 @@
-// libnip.so -- the reference's time-series API (src/nip.h) over the nip_amd
-// GPU engine (the drop-in boundary with the reference's struct
+// libnip.so -- the reference's nip.h API (src/nip.h) over the nip_amd GPU
+// engine (the drop-in boundary with the reference's struct
 // layouts).  Declared in include/compat/nip.h.
 //
 // Each nip_model owns an engine handle (nipamd_model) in a side table keyed
 // by the nip_model pointer, so the public struct keeps the reference's layout
-// (nip.h:71-104).  The variable records (nipvariable.h:51-78) are filled from
-// the engine's compiled model.  Inference and learning go to the engine:
+// (nip.h:71-104).  The variable records (nipvariable.h:51-78) and the join
+// tree (nipjointree.h:43-63: cliques with the compiled original_p, sepsets,
+// sepset lists in the reference's order) are built from the engine's
+// compiled model.  Work goes to the GPU:
 //   forward_inference           -> nipamd_filter_host   (nip.c:1103-1315)
 //   forward_backward_inference  -> nipamd_fb_host       (nip.c:1320-1581)
 //   em_learn                    -> nipamd_em_learn      (nip.c:2076-2243)
+//   make_consistent             -> nipamd_hugin_passes  (nip.c:1600-1617)
 // with the evidence of MARKED observed variables only (insert_ts_step with
 // NIP_MARK_ON, nip.c:982-1003, 1240, 1455, 1816).  There is no CPU path: a
 // request the engine has no GPU plan for fails (NULL / error code) after
-// nip_report_error.
+// nip_report_error.  Edits a caller makes to the host join tree's
+// original_p tables or to priors (nip_init_clique, nip_set_prior, ...) are
+// forwarded to the engine before each engine call (sync_engine).
 #include <array>
 #include <cerrno>
 #include <cstdio>
@@ -27,19 +32,23 @@
 
 #include "nip.h"
 
+extern "C" unsigned long nipamd_compat_take_ids(int n);   // variable_api.cpp
+
 namespace {
 
 struct Compat {
   nip_model_struct pub{};
   nipamd_model* eng = nullptr;
+  unsigned long id0 = 0;                  // ID of variable 0 (IDs are consecutive)
+  // the records; their arrays are malloc'd because the reference's API frees
+  // or replaces them (nip_set_parents, nip_set_prior, nip_find_family_mapping)
   std::vector<nip_variable_struct> vars;
-  std::vector<std::string> symbols, labels;
-  std::vector<std::vector<std::string>> states;
-  std::vector<std::vector<char*>> state_ptrs;
-  std::vector<std::vector<double>> likelihood, prior;
-  std::vector<std::vector<nip_variable>> parents;
   std::vector<nip_variable> all, next, previous, outgoing, prev_outgoing, incoming, children,
       independent;
+  std::vector<nip_clique> cliques;
+  std::vector<nip_sepset> sepsets;
+  // the tables the engine holds (what sync_engine compares host edits against)
+  std::vector<std::vector<double>> eng_orig, eng_prior;
 };
 
 std::unordered_map<const nip_model_struct*, Compat*> g_models;
@@ -49,11 +58,10 @@ Compat* lookup(nip_model m) {
   return it == g_models.end() ? nullptr : it->second;
 }
 
-// model variable index of v (ids are 1.. in declaration order), -1 if v is not
-// one of c's variables
+// model variable index of v, -1 if v is not one of c's variables
 int index_of(const Compat* c, nip_variable v) {
-  if (!v || v->id < NIP_VAR_MIN_ID || v->id > c->vars.size()) return -1;
-  const int i = (int)v->id - 1;
+  if (!v || v->id < c->id0 || v->id >= c->id0 + c->vars.size()) return -1;
+  const int i = (int)(v->id - c->id0);
   return &c->vars[i] == v ? i : -1;
 }
 
@@ -75,11 +83,51 @@ void engine_error(int e) {
   REPORT(e);
 }
 
-void refresh_priors(Compat* c) {
+// Forward host-side edits of original_p / priors to the engine.
+int sync_engine(Compat* c) {
+  const int nc = (int)c->cliques.size(), nv = (int)c->vars.size();
+  std::vector<const double*> orig(nc, nullptr), pri(nv, nullptr);
+  bool dirty = false;
+  for (int k = 0; k < nc; k++) {
+    nip_potential o = c->cliques[k]->original_p;
+    auto& e = c->eng_orig[k];
+    if ((size_t)o->size_of_data == e.size() &&
+        std::memcmp(o->data, e.data(), e.size() * sizeof(double)) != 0) {
+      orig[k] = o->data;
+      e.assign(o->data, o->data + e.size());
+      dirty = true;
+    }
+  }
+  for (int i = 0; i < nv; i++) {
+    nip_variable v = &c->vars[i];
+    auto& e = c->eng_prior[i];
+    if (v->num_of_parents > 0 || !v->prior || e.size() != (size_t)v->cardinality) continue;
+    if (std::memcmp(v->prior, e.data(), e.size() * sizeof(double)) != 0) {
+      pri[i] = v->prior;
+      e.assign(v->prior, v->prior + e.size());
+      dirty = true;
+    }
+  }
+  if (!dirty) return NIP_NO_ERROR;
+  return nipamd_model_set_tables(c->eng, nc, orig.data(), nv, pri.data());
+}
+
+// After the engine changed its tables (em_learn's m_step): the host join
+// tree's original_p and p, and the priors, take the engine's values.
+void pull_engine(Compat* c) {
+  for (size_t k = 0; k < c->cliques.size(); k++) {
+    nip_potential o = c->cliques[k]->original_p;
+    nipamd_model_original(c->eng, (int)k, o->data, o->size_of_data);
+    std::memcpy(c->cliques[k]->p->data, o->data, sizeof(double) * o->size_of_data);
+    c->eng_orig[k].assign(o->data, o->data + o->size_of_data);
+  }
   for (size_t i = 0; i < c->vars.size(); i++) {
-    if (!c->vars[i].prior) continue;
-    if (nipamd_model_prior(c->eng, (int)i, nullptr) == (int)c->prior[i].size())
-      nipamd_model_prior(c->eng, (int)i, c->prior[i].data());
+    nip_variable v = &c->vars[i];
+    if (!v->prior || v->num_of_parents > 0) continue;
+    if (nipamd_model_prior(c->eng, (int)i, nullptr) == v->cardinality) {
+      nipamd_model_prior(c->eng, (int)i, v->prior);
+      c->eng_prior[i].assign(v->prior, v->prior + v->cardinality);
+    }
   }
 }
 
@@ -125,6 +173,7 @@ int run_inference(time_series* ts, int n, nip_variable vars[], int nvars, bool f
   for (int s = 0; s < n; s++) out[s] = nullptr;
   Compat* c = ts[0] ? lookup(ts[0]->model) : nullptr;
   if (!c) return NIP_ERROR_INVALID_ARGUMENT;
+  if (int e = sync_engine(c)) return e;
   std::vector<int> q(nvars), off(nvars);
   int stride = 0;
   for (int i = 0; i < nvars; i++) {
@@ -183,27 +232,6 @@ int run_inference(time_series* ts, int n, nip_variable vars[], int nvars, bool f
   return rc;
 }
 
-std::string desc_json(nipamd_model* e) {
-  const int len = nipamd_model_desc_json(e, nullptr, 0);
-  std::string d((size_t)len + 1, '\0');
-  nipamd_model_desc_json(e, d.data(), len + 1);
-  d.resize(len);
-  return d;
-}
-
-// the integer list starting at the first '[' at or after p
-std::vector<int> ints_at(const std::string& d, size_t p) {
-  std::vector<int> out;
-  p = d.find('[', p) + 1;
-  while (p < d.size() && d[p] != ']') {
-    char* end;
-    out.push_back((int)std::strtol(d.c_str() + p, &end, 10));
-    p = end - d.c_str();
-    if (d[p] == ',') p++;
-  }
-  return out;
-}
-
 }  // namespace
 
 extern "C" {
@@ -236,91 +264,79 @@ void nip_reset_error_handler(void) { g_error_code = g_error_counter = 0; }
 int nip_check_error_type(void) { return g_error_code; }
 int nip_check_error_counter(void) { return g_error_counter; }
 
-/* ---- double lists (src/niplists.c) ---- */
+/* ---- models (src/nip.c:122-508, 1584-1597, 2523-2553) ---- */
 
-nip_double_list nip_new_double_list(void) {
-  auto* l = (nip_double_list)std::malloc(sizeof(nip_double_list_struct));
-  if (l) {
-    l->length = 0;
-    l->first = l->last = nullptr;
-  }
-  return l;
+namespace {
+char* copy_text(const std::string& s) {
+  char* r = (char*)std::malloc(s.size() + 1);
+  if (r) std::memcpy(r, s.c_str(), s.size() + 1);
+  return r;
 }
 
-int nip_append_double(nip_double_list l, double d) {
-  if (!l) return REPORT(NIP_ERROR_NULLPOINTER);
-  auto* k = (nip_double_link)std::malloc(sizeof(nip_double_link_struct));
-  if (!k) return REPORT(NIP_ERROR_OUTOFMEMORY);
-  k->data = d;
-  k->fwd = nullptr;
-  k->bwd = l->last;
-  if (l->last) l->last->fwd = k; else l->first = k;
-  l->last = k;
-  l->length++;
+void free_compat(Compat* c) {
+  for (nip_clique q : c->cliques) nip_free_clique(q);   // frees the sepsets too
+  for (auto& v : c->vars) {
+    std::free(v.symbol);
+    std::free(v.name);
+    if (v.state_names)
+      for (int s = 0; s < v.cardinality; s++) std::free(v.state_names[s]);
+    std::free(v.state_names);
+    std::free(v.likelihood);
+    std::free(v.prior);
+    std::free(v.parents);
+    std::free(v.family_mapping);
+  }
+  if (c->eng) nipamd_model_free(c->eng);
+  delete c;
+}
+
+// the join tree of the compiled model as the reference's structs: clique c
+// holds its variables in ascending ID order and p = original_p = the
+// compiled CPT product (nip_init_clique into both, nipjointree.c:713-772);
+// sepsets start as ones (nipjointree.c:265-325) and are linked into each
+// clique's list in the compiled list order
+int build_join_tree(Compat* c) {
+  nipamd_model* e = c->eng;
+  const int nc = nipamd_model_num_cliques(e), ns = nipamd_model_num_sepsets(e);
+  const int nv = (int)c->vars.size();
+  std::vector<int> vars(nv + 1), links(ns + 1);
+  std::vector<std::vector<int>> clinks(nc);
+  for (int k = 0; k < nc; k++) {
+    int n = 0, nl = 0;
+    nipamd_model_clique(e, k, vars.data(), &n, links.data(), &nl);
+    std::vector<nip_variable> vs(n > 0 ? n : 1);
+    for (int i = 0; i < n; i++) vs[i] = &c->vars[vars[i]];
+    nip_clique q = nip_new_clique(vs.data(), n);
+    if (!q) return NIP_ERROR_OUTOFMEMORY;
+    c->cliques.push_back(q);
+    nipamd_model_original(e, k, q->original_p->data, q->original_p->size_of_data);
+    std::memcpy(q->p->data, q->original_p->data, sizeof(double) * q->p->size_of_data);
+    c->eng_orig.emplace_back(q->original_p->data, q->original_p->data + q->original_p->size_of_data);
+    clinks[k].assign(links.begin(), links.begin() + nl);
+  }
+  for (int s = 0; s < ns; s++) {
+    int a = -1, b = -1, n = 0;
+    nipamd_model_sepset(e, s, &a, &b, vars.data(), &n);
+    nip_sepset q = nip_new_sepset(c->cliques[a], c->cliques[b]);
+    if (!q) return NIP_ERROR_OUTOFMEMORY;
+    c->sepsets.push_back(q);
+  }
+  for (int k = 0; k < nc; k++) {   // the list order of each clique, front to back
+    nip_sepset_link prev = nullptr;
+    for (int s : clinks[k]) {
+      auto* l = (nip_sepset_link)std::malloc(sizeof(nip_sepsetlink_struct));
+      if (!l) return NIP_ERROR_OUTOFMEMORY;
+      l->data = c->sepsets[s];
+      l->fwd = nullptr;
+      l->bwd = prev;
+      if (prev) prev->fwd = l; else c->cliques[k]->sepsets = l;
+      prev = l;
+    }
+    c->cliques[k]->num_of_sepsets = (int)clinks[k].size();
+  }
   return NIP_NO_ERROR;
 }
-
-int nip_prepend_double(nip_double_list l, double d) {
-  if (!l) return REPORT(NIP_ERROR_NULLPOINTER);
-  auto* k = (nip_double_link)std::malloc(sizeof(nip_double_link_struct));
-  if (!k) return REPORT(NIP_ERROR_OUTOFMEMORY);
-  k->data = d;
-  k->bwd = nullptr;
-  k->fwd = l->first;
-  if (l->first) l->first->bwd = k; else l->last = k;
-  l->first = k;
-  l->length++;
-  return NIP_NO_ERROR;
-}
-
-double* nip_double_list_to_array(nip_double_list l) {
-  if (!l || l->length < 1) return nullptr;
-  auto* a = (double*)std::calloc(l->length, sizeof(double));
-  int i = 0;
-  for (nip_double_link k = l->first; a && k; k = k->fwd) a[i++] = k->data;
-  return a;
-}
-
-void nip_empty_double_list(nip_double_list l) {
-  if (!l) return;
-  for (nip_double_link k = l->first; k;) {
-    nip_double_link n = k->fwd;
-    std::free(k);
-    k = n;
-  }
-  l->first = l->last = nullptr;
-  l->length = 0;
-}
-
-/* ---- variables (src/nipvariable.c:201-315) ---- */
-
-void nip_mark_variable(nip_variable v) { if (v) v->mark = NIP_MARK_ON; }
-void nip_unmark_variable(nip_variable v) { if (v) v->mark = NIP_MARK_OFF; }
-int nip_variable_marked(nip_variable v) { return v ? v->mark != NIP_MARK_OFF : 0; }
-char* nip_variable_symbol(nip_variable v) { return v ? v->symbol : nullptr; }
-
-int nip_variable_state_index(nip_variable v, char* state) {
-  if (!v->state_names) return -1;
-  for (int i = 0; i < v->cardinality; i++)
-    if (std::strcmp(state, v->state_names[i]) == 0) return i;
-  return -1;
-}
-
-char* nip_variable_state_name(nip_variable v, int index) {
-  return v->state_names ? v->state_names[index] : nullptr;
-}
-
-int nip_equal_variables(nip_variable v1, nip_variable v2) { return v1 && v2 ? v1->id == v2->id : 0; }
-
-int nip_number_of_parents(nip_variable v) {
-  if (!v) {
-    nip_report_error((char*)__FILE__, __LINE__, EFAULT, 1);
-    return -1;
-  }
-  return v->num_of_parents;
-}
-
-/* ---- models (src/nip.c:122-508, 1584-1597) ---- */
+}  // namespace
 
 nip_model parse_model(char* file) {
   nipamd_model* e = nullptr;
@@ -332,52 +348,51 @@ nip_model parse_model(char* file) {
   auto* c = new Compat;
   c->eng = e;
   const int n = nipamd_model_num_vars(e);
-  c->vars.resize(n);
-  c->symbols.resize(n);
-  c->labels.resize(n);
-  c->states.resize(n);
-  c->state_ptrs.resize(n);
-  c->likelihood.resize(n);
-  c->prior.resize(n);
-  c->parents.resize(n);
+  c->id0 = nipamd_compat_take_ids(n);   // the parser numbers variables from the global counter
+  c->vars.assign(n, nip_variable_struct{});
+  c->eng_prior.resize(n);
   std::vector<std::array<int, 9>> info(n);
   std::vector<std::vector<int>> par(n);
   char buf[4096];
-  for (int i = 0; i < n; i++) {
-    nipamd_model_var_symbol(e, i, buf, sizeof buf);
-    c->symbols[i] = buf;
-    nipamd_model_var_label(e, i, buf, sizeof buf);
-    c->labels[i] = buf;
+  bool ok = true;
+  for (int i = 0; i < n && ok; i++) {
+    nip_variable_struct& v = c->vars[i];
     const int np = nipamd_model_var_info(e, i, info[i].data(), nullptr, 0);
     par[i].resize(np);
     nipamd_model_var_info(e, i, info[i].data(), par[i].data(), np);
     const int card = info[i][0];
-    for (int s = 0; s < card; s++) {
+    v.id = c->id0 + (unsigned long)i;
+    nipamd_model_var_symbol(e, i, buf, sizeof buf);
+    v.symbol = copy_text(buf);
+    nipamd_model_var_label(e, i, buf, sizeof buf);
+    v.name = copy_text(buf);
+    v.cardinality = card;
+    v.state_names = (char**)std::calloc(card > 0 ? card : 1, sizeof(char*));
+    v.likelihood = (double*)std::malloc(sizeof(double) * (card > 0 ? card : 1));
+    ok = v.symbol && v.name && v.state_names && v.likelihood;
+    for (int s = 0; ok && s < card; s++) {
       nipamd_model_state_name(e, i, s, buf, sizeof buf);
-      c->states[i].push_back(buf);
+      ok = (v.state_names[s] = copy_text(buf)) != nullptr;
+      v.likelihood[s] = 1.0;
     }
-    c->likelihood[i].assign(card, 1.0);
-    if (np == 0) {
-      c->prior[i].assign(card, 0.0);  // nip.c:175-180: a missing prior reads as zeros
-      nipamd_model_prior(e, i, c->prior[i].data());
+    if (ok && np == 0) {   // nip.c:175-180: a missing prior reads as zeros
+      v.prior = (double*)std::calloc(card > 0 ? card : 1, sizeof(double));
+      ok = v.prior != nullptr;
+      if (ok) nipamd_model_prior(e, i, v.prior);
+      if (ok) c->eng_prior[i].assign(v.prior, v.prior + card);
     }
   }
-  for (int i = 0; i < n; i++) {
+  for (int i = 0; i < n && ok; i++) {
     nip_variable_struct& v = c->vars[i];
-    v.id = (unsigned long)i + NIP_VAR_MIN_ID;
-    v.symbol = c->symbols[i].data();
-    v.name = c->labels[i].data();
-    v.cardinality = info[i][0];
-    for (auto& s : c->states[i]) c->state_ptrs[i].push_back(s.data());
-    v.state_names = c->state_ptrs[i].data();
-    v.likelihood = c->likelihood[i].data();
-    v.prior = c->prior[i].empty() ? nullptr : c->prior[i].data();
     v.prior_entered = 0;
     v.next = info[i][1] >= 0 ? &c->vars[info[i][1]] : nullptr;
     v.previous = info[i][2] >= 0 ? &c->vars[info[i][2]] : nullptr;
-    for (int p : par[i]) c->parents[i].push_back(&c->vars[p]);
     v.num_of_parents = (int)par[i].size();
-    v.parents = c->parents[i].empty() ? nullptr : c->parents[i].data();
+    if (!par[i].empty()) {
+      v.parents = (nip_variable*)std::calloc(par[i].size(), sizeof(nip_variable));
+      if (!(ok = v.parents != nullptr)) break;
+      for (size_t j = 0; j < par[i].size(); j++) v.parents[j] = &c->vars[par[i][j]];
+    }
     v.family_clique = nullptr;
     v.family_mapping = nullptr;
     v.interface_status = info[i][3];
@@ -385,6 +400,12 @@ nip_model parse_model(char* file) {
     v.pos_x = info[i][4];
     v.pos_y = info[i][5];
     c->all.push_back(&v);
+  }
+  if (ok) ok = build_join_tree(c) == NIP_NO_ERROR;
+  if (!ok) {
+    REPORT(NIP_ERROR_OUTOFMEMORY);
+    free_compat(c);
+    return nullptr;
   }
   // the special-purpose arrays of nip.c:216-247
   for (int i = 0; i < n; i++) {
@@ -400,13 +421,11 @@ nip_model parse_model(char* file) {
     }
     (v->parents ? c->children : c->independent).push_back(v);
   }
+  int in_c = -1, out_c = -1;
+  nipamd_model_interface_cliques(e, &in_c, &out_c);
   nip_model_struct& m = c->pub;
-  const std::string d = desc_json(e);
-  const size_t cs = d.find("\"cliques\":["), ss = d.find("],\"sepsets\"");
-  m.num_of_cliques = 0;
-  for (size_t p = d.find("{\"vars\":", cs); p != std::string::npos && p < ss; p = d.find("{\"vars\":", p + 1))
-    m.num_of_cliques++;
-  m.cliques = nullptr;
+  m.num_of_cliques = (int)c->cliques.size();
+  m.cliques = c->cliques.data();
   m.num_of_vars = n;
   m.variables = c->all.data();
   m.num_of_nexts = (int)c->next.size();
@@ -417,7 +436,8 @@ nip_model parse_model(char* file) {
   m.previous_outgoing_interface = c->prev_outgoing.data();
   m.incoming_interface_size = (int)c->incoming.size();
   m.incoming_interface = c->incoming.data();
-  m.in_clique = m.out_clique = nullptr;
+  m.in_clique = in_c >= 0 ? c->cliques[in_c] : nullptr;
+  m.out_clique = out_c >= 0 ? c->cliques[out_c] : nullptr;
   m.num_of_children = (int)c->children.size();
   m.children = c->children.data();
   m.independent = c->independent.data();
@@ -431,13 +451,16 @@ void free_model(nip_model model) {
   Compat* c = lookup(model);
   if (!c) return;
   g_models.erase(model);
-  nipamd_model_free(c->eng);
-  delete c;
+  free_compat(c);
 }
 
 int write_model(nip_model model, char* filename) {
   Compat* c = lookup(model);
   if (!c || !filename) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  if (int e = sync_engine(c)) {
+    engine_error(e);
+    return e;
+  }
   const int e = nipamd_write_model(c->eng, filename);
   if (e != NIP_NO_ERROR) engine_error(e);
   return e;
@@ -453,28 +476,22 @@ nip_variable model_variable(nip_model model, char* symbol) {
   return nullptr;
 }
 
-// nip.c:2523-2553 prints every clique, then its sepsets in link order; the
-// potentials are device-resident in the engine and are not printed here
+// every clique with its belief, then its sepsets in list order with their
+// latest messages (nip.c:2523-2553)
 void print_cliques(nip_model model) {
-  Compat* c = lookup(model);
-  if (!c) {
+  if (!model) {
     REPORT(NIP_ERROR_NULLPOINTER);
     return;
   }
-  const std::string d = desc_json(c->eng);
-  const size_t cs = d.find("\"cliques\":["), ss = d.find("],\"sepsets\":["), se = d.find("],\"in_clique\"");
-  std::vector<std::vector<int>> sep;
-  for (size_t p = d.find("{\"a\":", ss); p != std::string::npos && p < se; p = d.find("{\"a\":", p + 1))
-    sep.push_back(ints_at(d, d.find("\"vars\":", p)));
   std::printf("Cliques of the model:\n");
-  for (size_t p = d.find("{\"vars\":", cs); p != std::string::npos && p < ss; p = d.find("{\"vars\":", p + 1)) {
-    std::printf("clique ");
-    for (int v : ints_at(d, p)) std::printf("%s ", c->symbols[v].c_str());
-    std::printf("\n");
-    for (int s : ints_at(d, d.find("\"links\":", p))) {
-      std::printf("sepset ");
-      for (int v : sep[s]) std::printf("%s ", c->symbols[v].c_str());
-      std::printf("\n");
+  for (int i = 0; i < model->num_of_cliques; i++) {
+    nip_clique c = model->cliques[i];
+    nip_fprintf_clique(stdout, c);
+    nip_fprintf_potential(stdout, c->p);
+    for (nip_sepset_link l = c->sepsets; l; l = l->fwd) {
+      auto* s = (nip_sepset)l->data;
+      nip_fprintf_sepset(stdout, s);
+      nip_fprintf_potential(stdout, s->new_);
     }
     std::printf("\n");
   }
@@ -693,6 +710,10 @@ int em_learn(time_series* ts, int n_ts, double threshold, nip_double_list learni
   if (!ts || n_ts < 1 || !ts[0] || !ts[0]->model) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
   Compat* c = lookup(ts[0]->model);
   if (!c) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  if (int e = sync_engine(c)) {
+    engine_error(e);
+    return e;
+  }
   if (learning_curve && NIP_LIST_LENGTH(learning_curve) > 0) nip_empty_double_list(learning_curve);
   std::vector<int> col, var, ov;
   marked_columns(ts[0], c, col, ov);
@@ -727,7 +748,7 @@ int em_learn(time_series* ts, int n_ts, double threshold, nip_double_list learni
     e = nipamd_em_learn(c->eng, n_ts, lengths.data(), obs.data(), k, ov.data(), threshold,
                         init.data(), 0, curve.data(), (int)curve.size(), &curve_len);
   }
-  refresh_priors(c);
+  pull_engine(c);
   if (e != NIP_NO_ERROR && e != NIP_ERROR_BAD_LUCK) {
     engine_error(e);
     return e;
@@ -749,6 +770,10 @@ time_series generate_data(nip_model model, int length) {
   Compat* c = lookup(model);
   if (!c || length < 0) {
     REPORT(NIP_ERROR_INVALID_ARGUMENT);
+    return nullptr;
+  }
+  if (int e = sync_engine(c)) {
+    engine_error(e);
     return nullptr;
   }
   const int nv = nipamd_generate_order(c->eng, nullptr);
@@ -790,6 +815,126 @@ time_series generate_data(nip_model model, int length) {
     return nullptr;
   }
   return ts;
+}
+
+/* ---- the single-slice state (src/nip.c:61-119, 951-1027, 1600-1617,
+ *      2254-2321): the reference's bookkeeping over the host join tree;
+ *      make_consistent propagates on the GPU ---- */
+
+void reset_model(nip_model model) {
+  for (int i = 0; i < model->num_of_vars; i++) {
+    nip_variable v = model->variables[i];
+    nip_reset_likelihood(v);
+    v->prior_entered = 0;
+  }
+  if (nip_global_retraction(model->variables, model->num_of_vars, model->cliques,
+                            model->num_of_cliques) != NIP_NO_ERROR)
+    REPORT(NIP_ERROR_GENERAL);
+}
+
+void total_reset(nip_model model) {
+  for (int i = 0; i < model->num_of_cliques; i++) nip_uniform_potential(model->cliques[i]->original_p, 1.0);
+  reset_model(model);
+}
+
+// priors of the independent variables, once each; with has_history the
+// previous slice's interface variables get none (nip.c:88-119)
+void use_priors(nip_model model, int has_history) {
+  for (int i = 0; i < model->num_of_vars - model->num_of_children; i++) {
+    nip_variable v = model->independent[i];
+    if (v->prior_entered) continue;
+    if (has_history && (v->interface_status & NIP_INTERFACE_OLD_OUTGOING)) continue;
+    if (nip_enter_prior(model->variables, model->num_of_vars, model->cliques, model->num_of_cliques,
+                        v, v->prior) != NIP_NO_ERROR)
+      REPORT(NIP_ERROR_GENERAL);
+    v->prior_entered = 1;
+  }
+}
+
+void make_consistent(nip_model model) {
+  if (nipamd_compat_make_consistent(model->cliques, model->num_of_cliques) != NIP_NO_ERROR)
+    REPORT(NIP_ERROR_GENERAL);
+}
+
+int insert_hard_evidence(nip_model model, char* varname, char* observation) {
+  nip_variable v = model_variable(model, varname);
+  if (!v) return NIP_ERROR_INVALID_ARGUMENT;
+  const int ret = nip_enter_observation(model->variables, model->num_of_vars, model->cliques,
+                                        model->num_of_cliques, v, observation);
+  if (ret != NIP_NO_ERROR) REPORT(NIP_ERROR_GENERAL);
+  make_consistent(model);
+  return ret;
+}
+
+int insert_soft_evidence(nip_model model, char* varname, double* distribution) {
+  nip_variable v = model_variable(model, varname);
+  if (!v) return NIP_ERROR_INVALID_ARGUMENT;
+  const int ret = nip_enter_evidence(model->variables, model->num_of_vars, model->cliques,
+                                     model->num_of_cliques, v, distribution);
+  make_consistent(model);
+  return ret;
+}
+
+// the observations of step t whose variables' marks match mark_mask;
+// missing values (< 0) are skipped (nip.c:982-1001)
+int insert_ts_step(time_series ts, int t, nip_model model, char mark_mask) {
+  if (t < 0 || t >= timeseries_length(ts)) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  for (int i = 0; i < ts->model->num_of_vars - ts->num_of_hidden; i++) {
+    nip_variable v = ts->observed[i];
+    if ((NIP_MARK(v) & mark_mask) && ts->data[t][i] >= 0)
+      nip_enter_index_observation(model->variables, model->num_of_vars, model->cliques,
+                                  model->num_of_cliques, v, ts->data[t][i]);
+  }
+  return NIP_NO_ERROR;
+}
+
+int insert_ucs_step(uncertain_series ucs, int t, nip_model model, char mark_mask) {
+  if (t < 0 || t >= uncertainseries_length(ucs)) return REPORT(NIP_ERROR_INVALID_ARGUMENT);
+  for (int i = 0; i < ucs->num_of_vars; i++) {
+    nip_variable v = ucs->variables[i];
+    if (!(NIP_MARK(v) & mark_mask)) continue;
+    const int e = nip_enter_evidence(model->variables, model->num_of_vars, model->cliques,
+                                     model->num_of_cliques, v, ucs->data[t][i]);
+    if (e != NIP_NO_ERROR) return REPORT(e);
+  }
+  return NIP_NO_ERROR;
+}
+
+double model_prob_mass(nip_model model) {
+  return nip_probability_mass(model->cliques, model->num_of_cliques);
+}
+
+double* get_probability(nip_model model, nip_variable v) {
+  if (!model || !v) {
+    REPORT(NIP_ERROR_NULLPOINTER);
+    return nullptr;
+  }
+  const int card = NIP_CARDINALITY(v);
+  auto* r = (double*)std::calloc(card > 0 ? card : 1, sizeof(double));
+  if (!r) {
+    REPORT(NIP_ERROR_OUTOFMEMORY);
+    return nullptr;
+  }
+  nip_clique c = nip_find_family(model->cliques, model->num_of_cliques, v);
+  if (!c) {
+    REPORT(NIP_ERROR_GENERAL);
+    std::free(r);
+    return nullptr;
+  }
+  nip_marginalise_clique(c, v, r);
+  nip_normalise_array(r, card);
+  return r;
+}
+
+nip_potential get_joint_probability(nip_model model, nip_variable* vars, int num_of_vars) {
+  for (int i = 0; i < model->num_of_cliques; i++) nip_unmark_clique(model->cliques[i]);
+  nip_potential p = nip_gather_joint_probability(model->cliques[0], vars, num_of_vars, nullptr, 0);
+  if (!p) {
+    REPORT(NIP_ERROR_GENERAL);
+    return nullptr;
+  }
+  nip_normalise_potential(p);
+  return p;
 }
 
 /* ---- random numbers (src/nip.c:2482-2520) ---- */

@@ -510,6 +510,56 @@ int nipamd_model_prior(const nipamd_model* mm, int v, double* out) {
   return (int)var.prior.size();
 }
 
+int nipamd_model_num_cliques(const nipamd_model* mm) { return mm ? (int)mm->m.cliques.size() : -1; }
+int nipamd_model_num_sepsets(const nipamd_model* mm) { return mm ? (int)mm->m.sepsets.size() : -1; }
+
+int nipamd_model_clique(const nipamd_model* mm, int c, int* vars, int* n_vars, int* links, int* n_links) {
+  if (!mm || c < 0 || c >= (int)mm->m.cliques.size()) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad clique");
+  const auto& q = mm->m.cliques[c];
+  if (n_vars) *n_vars = (int)q.vars.size();
+  if (n_links) *n_links = (int)q.links.size();
+  if (vars) std::copy(q.vars.begin(), q.vars.end(), vars);
+  if (links) std::copy(q.links.begin(), q.links.end(), links);
+  return NIP_NO_ERROR;
+}
+
+int nipamd_model_sepset(const nipamd_model* mm, int s, int* a, int* b, int* vars, int* n_vars) {
+  if (!mm || s < 0 || s >= (int)mm->m.sepsets.size()) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad sepset");
+  const auto& q = mm->m.sepsets[s];
+  if (a) *a = q.a;
+  if (b) *b = q.b;
+  if (n_vars) *n_vars = (int)q.vars.size();
+  if (vars) std::copy(q.vars.begin(), q.vars.end(), vars);
+  return NIP_NO_ERROR;
+}
+
+int nipamd_model_interface_cliques(const nipamd_model* mm, int* in_clique, int* out_clique) {
+  if (!mm) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad model");
+  if (in_clique) *in_clique = mm->m.in_clique;
+  if (out_clique) *out_clique = mm->m.out_clique;
+  return NIP_NO_ERROR;
+}
+
+int nipamd_model_set_tables(nipamd_model* mm, int n_cliques, const double* const* originals,
+                            int n_vars, const double* const* priors) {
+  if (!mm || n_cliques != (int)mm->m.cliques.size() || n_vars != (int)mm->m.vars.size() ||
+      (n_cliques > 0 && !originals) || (n_vars > 0 && !priors))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "nipamd_model_set_tables: bad arguments");
+  for (int c = 0; c < n_cliques; c++) {
+    auto& o = mm->m.cliques[c].original;
+    if (originals[c]) std::memcpy(o.data(), originals[c], o.size() * sizeof(double));
+  }
+  for (int v = 0; v < n_vars; v++) {
+    auto& var = mm->m.vars[v];
+    if (!priors[v] || !var.parents.empty()) continue;
+    var.prior.assign(priors[v], priors[v] + var.card);
+    var.has_prior = true;
+  }
+  nipamd::build_chain_plan(mm->m);
+  mm->version++;
+  return NIP_NO_ERROR;
+}
+
 int nipamd_graph_cliques(int n, const int* card, int n_edges, const int* edges,
                          int set_parents, int* clique_off, int* clique_vars, int cap) {
   if (n <= 0 || !card || (n_edges > 0 && !edges) || !clique_off) return -NIP_ERROR_INVALID_ARGUMENT;

@@ -946,3 +946,47 @@ int nh_graph_cliques(int n, const int* card, int ne, const int* edges, int set_p
   for(i = 0; i < 256; i++) free(st[i]);
   return nc;
 }
+
+/* ------------------------------------------------------------------ */
+/* single-slice scripts (oracle/ref/slice_script.h) over the reference */
+/* ------------------------------------------------------------------ */
+
+/* get_probability, src/nip.c:2261-2298 */
+static double* h_get_probability(nh_model* m, nip_variable v){
+  nip_clique c = nip_find_family(m->cliques, m->num_of_cliques, v);
+  double* r;
+  if(!c) return NULL;
+  r = (double*) calloc(NIP_CARDINALITY(v), sizeof(double));
+  nip_marginalise_clique(c, v, r);
+  nip_normalise_array(r, NIP_CARDINALITY(v));
+  return r;
+}
+
+/* get_joint_probability, src/nip.c:2301-2321 */
+static nip_potential h_get_joint(nh_model* m, nip_variable* vars, int n){
+  int i;
+  nip_potential p;
+  for(i = 0; i < m->num_of_cliques; i++) nip_unmark_clique(m->cliques[i]);
+  p = nip_gather_joint_probability(m->cliques[0], vars, n, NULL, 0);
+  if(p) nip_normalise_potential(p);
+  return p;
+}
+
+#define SS_MODEL nh_model*
+#define SS_RESET(m) h_reset_model(m)
+#define SS_PRIORS(m, h) h_use_priors(m, h)
+#define SS_CONSISTENT(m) h_make_consistent(m)
+#define SS_PROB(m, v) h_get_probability(m, v)
+#define SS_JOINT(m, vs, n) h_get_joint(m, vs, n)
+#define ss_put(ctx, ...) nh_put((nh_out*)(ctx), __VA_ARGS__)
+#include "slice_script.h"
+
+/* run a slice script (slice_script.h) on model h; the output text goes to
+ * buf (returns its length, which may exceed cap: call again with more room),
+ * -1 on a bad script */
+int nh_slice(int h, const char* script, char* buf, int cap){
+  nh_out o = { buf, cap, 0 };
+  if(cap > 0) buf[0] = 0;
+  if(ss_run(&o, nh_models[h], script)) return -1;
+  return o.len;
+}
