@@ -142,7 +142,10 @@ def test_reference_nipjoint(tmp_path):
         f.write("M1\n3\n1\n")
     spec = netfile.read_net(net)
     syms = [n.symbol for n in spec.nodes]
-    for args, vs in ((["P1"], [1]), (["P0", "P1"], [0, 1]), ([], [0, 1])):
+    # (without variable arguments nipjoint frees ts->hidden twice, nipjoint.c:118
+    # then :145 and free_timeseries, nip.c:800 -- the reference program's own
+    # double free, so that form is not run)
+    for args, vs in ((["P1"], [1]), (["P0", "P1"], [0, 1]), (["P1", "P0"], [1, 0])):
         out = subprocess.run([prog, net, str(tmp_path / "d.txt"), *args], capture_output=True,
                              text=True, timeout=120)
         assert out.returncode == 0, out.stderr
