@@ -147,13 +147,28 @@ __device__ __forceinline__ void recip_n(const double (&c)[n], double (&r)[n]) {
   for (int i = 0; i < n; i++) r[i] = c[i] != 0.0 ? r[i] : 0.0;
 }
 
+#ifndef NIPAMD_MFMA_SPLITK
+#define NIPAMD_MFMA_SPLITK 0       // 1: the K=16 contraction as two independent 2-MFMA chains + adds
+#endif
+
 __device__ __forceinline__ v4d matvec(const double (&Aop)[4], v4d X) {
+#if NIPAMD_MFMA_SPLITK
+  // two accumulators: the second chain's MFMAs issue in the first chain's
+  // dependency shadow (one wave per SIMD: nothing else would fill it)
+  v4d d0 = {0.0, 0.0, 0.0, 0.0}, d1 = {0.0, 0.0, 0.0, 0.0};
+  d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0], X.x, d0, 0, 0, 0);
+  d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[1], X.y, d1, 0, 0, 0);
+  d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[2], X.z, d0, 0, 0, 0);
+  d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[3], X.w, d1, 0, 0, 0);
+  return d0 + d1;
+#else
   v4d d = {0.0, 0.0, 0.0, 0.0};
   d = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0], X.x, d, 0, 0, 0);
   d = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[1], X.y, d, 0, 0, 0);
   d = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[2], X.z, d, 0, 0, 0);
   d = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[3], X.w, d, 0, 0, 0);
   return d;
+#endif
 }
 
 __device__ __forceinline__ v4d ldexp4(v4d v, int k) {
