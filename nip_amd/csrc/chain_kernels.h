@@ -40,6 +40,7 @@ struct ChainArgs {
   double* ll;            // [B] or nullptr
   unsigned* status;      // [B] or nullptr
   double* counts;        // E-step only: per-sequence slabs [B][chain_estep_slab(M)]
+  unsigned long long* diag;   // diagnostics builds only: per-block wall-clock stamps, else null
 };
 
 // Scratch layout: per sequence kGuard + T + kGuard steps of 16 doubles
@@ -199,6 +200,10 @@ int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block
 size_t chain_mfma_lds_bytes(int M, int T);
 int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream);
+// matrix-core e_step (N, M <= 16): one slab row per 16-sequence block (the
+// sums over its sequences); -2 when the request does not fit the kernel
+size_t chain_estep_mfma_lds_bytes(int M, int T);
+int chain_estep_mfma_launch(const ChainArgs& a, hipStream_t stream);
 int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);

@@ -247,16 +247,22 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
+// diagnostics builds: s_memrealtime (100 MHz) stamp k of this block, lane 0
+__device__ __forceinline__ void diag_stamp(const ChainArgs& a, int k, int lane) {
+  if (a.diag && lane == 0) a.diag[blockIdx.x * 24 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 struct WaveCtx {
   const double* Et;         // LDS evidence table + 2g (row stride 16)
   const uint8_t* codes;     // LDS codes of chain j, index t in [-kMG, T + kMG)
   double* out;              // this direction's LDS ring [2][kMChunk][kStepD]
   double* zr;               // forward: LDS ring of step masses z2 [2][kMChunk][16], else null
+  int* scr;                 // e_step: LDS ring of applied scale exponents [2][kMChunk][16], else null
   int wo0, wo1;             // this lane's two piece offsets within a step
   bool zw;                  // this lane writes its chain's z2 (lane group 0)
 };
 
-template <bool FWD>
+template <bool FWD, bool ES = false>
 struct Chain {
   double Aop[4];
   v4d X;          // next mat-vec input (fwd: alpha_{t-1}; bwd: e_{t+1} o beta_{t+1})
@@ -265,7 +271,8 @@ struct Chain {
   // one step: the interface vector (alpha_t or beta_t, scaled) to LDS row L;
   // the forward filter also publishes its step mass z2 for the partner's ll
   template <bool SUM = true>
-  __device__ __forceinline__ void step(const WaveCtx& c, double* L, double* Z, v4d e) {
+  __device__ __forceinline__ void step(const WaveCtx& c, double* L, double* Z, int* SC, v4d e) {
+    if (ES && c.zw) *SC = sc;                  // e_step partners need the exponent applied at t
     const v4d u = ldexp4(matvec(Aop, X), sc);
     const v4d p = u * e;
     const v4d keep = FWD ? p : u;
@@ -296,18 +303,21 @@ struct Chain {
                                         const v4d (&e)[kMChunk], v4d (&en)[kMChunk]) {
     double* slot = c.out + (ci & 1) * kSlotD;
     double* zs = FWD ? c.zr + (ci & 1) * kMChunk * kMSeq + (lane & 15) : nullptr;
+    int* ss = ES ? c.scr + (ci & 1) * kMChunk * kMSeq + (lane & 15) : nullptr;
     const int base = ci * kMChunk;
     load_chunk(c, t0, base + kMChunk, en);       // the next chunk's inputs, one chunk ahead
     if (base + kMChunk <= n) {
 #pragma unroll
       for (int k = 0; k < kMChunk; k++) {
-        if (!SPARSE || (k & (kRescale - 1)) == kRescale - 1) step<true>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
-        else step<false>(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+        if (!SPARSE || (k & (kRescale - 1)) == kRescale - 1)
+          step<true>(c, slot + k * kStepD, zs + k * kMSeq, ss + k * kMSeq, e[k]);
+        else
+          step<false>(c, slot + k * kStepD, zs + k * kMSeq, ss + k * kMSeq, e[k]);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < kMChunk; k++)
-        if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, e[k]);
+        if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, ss + k * kMSeq, e[k]);
     }
     barrier_lds(w);
   }
@@ -331,19 +341,24 @@ struct Chain {
   }
 };
 
-template <bool FWD>
+template <bool FWD, bool ES = false>
 __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c, const double* Et,
                                             double* Sw, int lane, bool active, long b,
                                             int nchA, int nchB, unsigned long long* stamps) {
   const int j = lane & 15, g = lane >> 4;
   const int sj = state_of(j & 3, j >> 2);       // actual state of D row j
   const int T = a.T, H = a.H;
-  Chain<FWD> ch;
+  Chain<FWD, ES> ch;
 #pragma unroll
   for (int r = 0; r < 4; r++)
     ch.Aop[r] = FWD ? a.A[state_of(g, r) * 16 + sj] : a.A[sj * 16 + state_of(g, r)];
   if (FWD) {
     ch.X = load4(a.pi + 2 * g);
+    if (ES) {                                   // S[-1] = alpha_{-1} = prior: the backward partner's P0 step
+      double* q = Sw - kSStep;
+      *reinterpret_cast<double2*>(q) = make_double2(ch.X.x, ch.X.y);
+      *reinterpret_cast<double2*>(q + 8) = make_double2(ch.X.z, ch.X.w);
+    }
   } else {
     v4d beta;                                   // beta_{T-1} = 1 on the real states
     beta.x = state_of(g, 0) < a.N ? 1.0 : 0.0; beta.y = state_of(g, 1) < a.N ? 1.0 : 0.0;
@@ -363,9 +378,11 @@ __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c
   if (stamps && lane == 0) stamps[blockIdx.x * 4 + 1] = __builtin_readcyclecounter();
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   if (stamps && lane == 0) stamps[blockIdx.x * 4 + 2] = __builtin_readcyclecounter();
-  // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
+  if (ES && FWD) diag_stamp(a, 2, lane);
+  // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0 (e_step:
+  // ..beta_{-1}, the step against alpha_{-1} = prior that yields P0 and xi_0)
   if (FWD) ch.template run<false>(c, T - H, nchB, H, lane, &wb);
-  else ch.template run<false>(c, H, nchB, H - 1, lane, &wb);
+  else ch.template run<false>(c, ES ? H + 1 : H, nchB, H - 1, lane, &wb);
   if (NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
     unsigned long long* st = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 4;
     st[blockIdx.x * 8 + (FWD ? 0 : 1)] = wa.cyc;
@@ -387,11 +404,11 @@ struct LL {
   int e2, e1;
   double w[16];
 
-  __device__ __forceinline__ void init(const ChainArgs& a, int lane) {
+  __device__ __forceinline__ void init(const ChainArgs& a, int lane, bool miss0) {
     double ym = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; i++) { w[i] = a.ts[i]; ym = __builtin_fma(a.pi[i], w[i], ym); }   // y_{-1}
-    m2 = 1.0; m1 = (lane >> 4) == 0 ? ym : 1.0; zmin = 1.0; e2 = 0; e1 = 0;
+    m2 = 1.0; m1 = ((lane >> 4) == 0 && !miss0) ? ym : 1.0; zmin = 1.0; e2 = 0; e1 = 0;
   }
   __device__ __forceinline__ double dot(const double (&v)[16]) const {
     double y0 = v[0] * w[0], y1 = v[1] * w[1], y2 = v[2] * w[2], y3 = v[3] * w[3];
@@ -405,14 +422,21 @@ struct LL {
   // one step: y = alpha_t . w, z2 = sum(alpha_t); zf = the filter's z2 on
   // the steps where it rescales (rs), whose exponent is sc_{t+1}; `valid`
   // masks steps past the phase, last = (t == T-1).  Branch-free.
-  __device__ __forceinline__ void step(double y, double z2, double zf, bool rs, bool valid, bool last) {
+  // A step whose observation is missing (cm; nm: the next step's) enters
+  // m1 with m2's own factor instead of y_{t-1} 2^sc_t: both masses are the
+  // same there (nip.c:1461-1474 with no evidence entered), so such a step
+  // contributes exactly nothing (a fully missing sequence has ll = 0).
+  __device__ __forceinline__ void step(double y, double z2, double zf, bool rs, bool valid, bool last,
+                                       bool cm = false, bool nm = false) {
     // factors enter as mantissa and exponent: between two rescales the
     // filter's vectors (hence z2 and y) may be far below 2^-500
-    const double z = valid ? z2 : 1.0, yy = (valid && !last) ? y : 1.0;
+    const double z = valid ? z2 : 1.0, yy = (valid && !last && !nm) ? y : 1.0;
+    const double zz = (valid && cm) ? z2 : 1.0;
     zmin = __builtin_fmin(zmin, z);
     m2 *= __builtin_amdgcn_frexp_mant(z); e2 += __builtin_amdgcn_frexp_exp(z);
     m1 *= __builtin_amdgcn_frexp_mant(yy); e1 += __builtin_amdgcn_frexp_exp(yy);
-    e1 -= (valid && !last && rs) ? __builtin_amdgcn_frexp_exp(zf) : 0;   // 2^sc_{t+1}
+    m1 *= __builtin_amdgcn_frexp_mant(zz); e1 += __builtin_amdgcn_frexp_exp(zz);
+    e1 -= (valid && !last && !nm && rs) ? __builtin_amdgcn_frexp_exp(zf) : 0;   // 2^sc_{t+1}
   }
   __device__ __forceinline__ static double sum16(const double (&v)[16]) {
     double s0 = v[0] + v[1], s1 = v[2] + v[3], s2 = v[4] + v[5], s3 = v[6] + v[7];
@@ -423,7 +447,7 @@ struct LL {
     const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
     const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
   }
-  __device__ __forceinline__ void write(const ChainArgs& a, long b0, int lane) {
+  __device__ __forceinline__ void write(const ChainArgs& a, long b0, int lane, unsigned dead_status = 1u) {
     renorm();
     // combine the chain's four lanes (l, l ^ 32, l ^ 16); every operation is
     // symmetric, so both lanes of a pair hold identical bits
@@ -455,9 +479,218 @@ struct LL {
     const bool dead = zmin == 0.0;
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
-    if (a.status) a.status[b] = dead ? 1u : 0u;
+    if (a.status) a.status[b] = dead ? dead_status : 0u;
   }
 };
+
+// e_step partner context (LDS): the direction's applied-exponent ring, the
+// partner's M1 count table, the block's observation codes and evidence table.
+struct EsCtx {
+  const int* scr;           // [2 slots][kMChunk][16 chains]
+  double* H;                // M1 counts [M][16] (this partner's, block sums)
+  const uint8_t* codes;     // chain c at codes + c * Tr + kMG
+  int Tr;
+  const double* Et;         // [(M+2)][16]
+};
+
+// e_step, phase B of one partner (nip.c:1925-1967 per sequence, summed over
+// the block's 16 sequences).  Per chunk, after the filter's barrier:
+//   1. in-lane pass (lane: chain c = L & 15, slot steps kq = L >> 4 and kq + 4),
+//      from the ring vector v, the other direction's vector o (LDS-DMA, one
+//      chunk ahead, as the fb partner) and the evidence row e of the step:
+//      c_t = v . o, the posterior q = v o / c_t (kept in registers), the ll
+//      (forward), and the xi operands written back in place:
+//        forward  (t >= H):   o <- e o 2^sc_t / c_t           (b of xi_t)
+//        backward (t <  H-1): o <- o 2^sc_t / c_t             (a of xi_{t+1})
+//                             v <- e o v  (= e_t o beta_t, b of xi_t for step t-1)
+//      (xi without the A(x,y) factor, applied once by estep_finalize; sc_t =
+//      the exponent the filter applied at t, published per step);
+//   2. matrix-core pass (lane: step kq, state y), per chain and 4-step half:
+//        xi += a (x) b over the four steps, one v_mfma_f64_16x16x4 (K = time),
+//        forward a = alpha_{t-1} (ring, previous step), backward b = e_{t+1} o
+//        beta_{t+1} (ring, previous step); the chunk's first step takes the
+//        previous chunk's last vector, kept in registers;
+//   3. q written over o;
+//   4. M1 counts: H[code][y] += q(y), one ds_add_f64 per 16-lane row at a time
+//      (rows in a fixed order: no two lanes of an instruction share an
+//      address, so the sums are deterministic); missing observations summed
+//      apart (row M, split by finalize); P0 = posterior at t = -1 (backward).
+// The accumulators are the block's slab row (the tree over blocks replaces
+// the tree over sequences: sums of the same terms in a fixed order).
+template <bool FWD>
+__device__ __forceinline__ void estep_phase_b(const ChainArgs& a, double* out, const double* zr, double* Sblk,
+                                              double* ob_lds, int lane, long b0, int nchB, const EsCtx& es,
+                                              LL& ll, double (&pv)[kMSeq]) {
+  const int T = a.T, H = a.H, M = a.M;
+  const int s = lane & 7, hi = lane >> 3;
+  const int c = lane & 15, kq = lane >> 4, y = lane & 15;
+  const int nB = FWD ? T - H : H + 1;                    // this direction's phase-B steps
+  const int tB = FWD ? H : H - 1;
+  auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
+  const unsigned ob_base = (unsigned)(uintptr_t)ob_lds;
+  auto dma_other = [&](int k, int ci) {
+    const double* q = Sblk + (long)(tlow(ci) + hi) * kSStep + 2 * s;
+    dma16(q, __builtin_amdgcn_readfirstlane(ob_base + (unsigned)k * (kMSeq * kOBRow * 8u)),
+          std::make_integer_sequence<int, kMSeq>{});
+  };
+  const int nact = (int)(a.B - b0 < kMSeq ? a.B - b0 : kMSeq);    // sequences present in this block
+  const v4d zero4 = {0.0, 0.0, 0.0, 0.0};
+  v4d dx0 = zero4, dx1 = zero4;
+  double miss = 0.0, p0 = 0.0;
+  const uint8_t* cdl = es.codes + c * es.Tr + kMG;       // in-lane pass: chain c's codes
+  const int last = nchB > 0 ? nchB - 1 : 0;
+  unsigned long long pc[5] = {0, 0, 0, 0, 0}, tc = 0;   // diagnostics: cycles per pass
+  auto tick = [&](int k) {
+    if (a.diag) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const unsigned long long n = __builtin_readcyclecounter();
+      pc[k] += n - tc; tc = n;
+    }
+  };
+  dma_other(0, 0);
+  for (int ci = 0; ci < nchB; ci++) {
+    dma_other((ci + 1) & 1, ci + 1 < last ? ci + 1 : last);    // over-run reloads the last chunk
+    if (a.diag) tc = __builtin_readcyclecounter();
+    barrier_lds();
+    wait_vm<16>();
+    tick(0);
+    double* slot = out + (ci & 1) * kSlotD;
+    double* obb = ob_lds + (ci & 1) * (kMSeq * kOBRow);
+    const int* scs = es.scr + (ci & 1) * kMChunk * kMSeq;
+    // 1. in-lane pass
+    double q[2][16];
+    {
+      const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int k = kq + 4 * h;
+        const int row = FWD ? k : kMChunk - 1 - k;
+        const int i = ci * kMChunk + k;
+        const int t = FWD ? tB + i : tB - i;
+        double* vr = slot + k * kStepD;
+        double* orow = obb + c * kOBRow + row * 16;
+        const int code = cdl[t];
+        const double* er = es.Et + code * 16;
+        double v[16], o[16], e[16];
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+          const double2 x = *reinterpret_cast<const double2*>(vr + piece_off(c, p));
+          v[2 * p] = x.x; v[2 * p + 1] = x.y;
+          const double2 w = *reinterpret_cast<const double2*>(orow + 2 * p);
+          o[2 * p] = w.x; o[2 * p + 1] = w.y;
+          const double2 u = *reinterpret_cast<const double2*>(er + 2 * p);
+          e[2 * p] = u.x; e[2 * p + 1] = u.y;
+        }
+        if (FWD) {
+          const double zf = zs[k * kMSeq + c];
+          ll.step(ll.dot(v), zf, zf, true, i < nB, t == T - 1, code == M, cdl[t + 1] == M);
+        }
+        double z0 = v[0] * o[0], z1 = v[1] * o[1], z2 = v[2] * o[2], z3 = v[3] * o[3];
+#pragma unroll
+        for (int p = 4; p < 16; p += 4) {
+          z0 = __builtin_fma(v[p], o[p], z0); z1 = __builtin_fma(v[p + 1], o[p + 1], z1);
+          z2 = __builtin_fma(v[p + 2], o[p + 2], z2); z3 = __builtin_fma(v[p + 3], o[p + 3], z3);
+        }
+        const double ct = (z0 + z1) + (z2 + z3);
+        const double rc = recip(ct);
+        const bool ok = i < nB && c < nact && ct != 0.0;  // a present sequence's step with alpha.beta != 0
+        const double fs = __builtin_ldexp(rc, scs[k * kMSeq + c]);
+        const bool okx = FWD ? ok : ok && i > 0;          // xi_H belongs to the forward partner
+        double w[16];
+#pragma unroll
+        for (int p = 0; p < 16; p++) {
+          q[h][p] = ok ? v[p] * o[p] * rc : 0.0;
+          w[p] = okx ? (FWD ? e[p] * o[p] * fs : o[p] * fs) : 0.0;
+        }
+#pragma unroll
+        for (int p = 0; p < 8; p++)
+          *reinterpret_cast<double2*>(orow + 2 * p) = make_double2(w[2 * p], w[2 * p + 1]);
+        if (!FWD) {
+#pragma unroll
+          for (int p = 0; p < 8; p++)
+            *reinterpret_cast<double2*>(vr + piece_off(c, p)) =
+                make_double2(ok ? e[2 * p] * v[2 * p] : 0.0, ok ? e[2 * p + 1] * v[2 * p + 1] : 0.0);
+        }
+      }
+      if (FWD) ll.renorm();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tick(1);
+    // 2. xi on the matrix cores
+#pragma unroll
+    for (int cc = 0; cc < kMSeq; cc++) {
+      const int po = piece_off(cc, y >> 1) + (y & 1);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int k = 4 * h + kq;
+        const int row = FWD ? k : kMChunk - 1 - k;
+        const double rp = slot[(k > 0 ? k - 1 : 0) * kStepD + po];
+        const double ringv = k > 0 ? rp : pv[cc];
+        const double dmav = obb[cc * kOBRow + row * 16 + y];
+        if (h == 0)
+          dx0 = __builtin_amdgcn_mfma_f64_16x16x4f64(FWD ? ringv : dmav, FWD ? dmav : ringv, dx0, 0, 0, 0);
+        else
+          dx1 = __builtin_amdgcn_mfma_f64_16x16x4f64(FWD ? ringv : dmav, FWD ? dmav : ringv, dx1, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int cc = 0; cc < kMSeq; cc++) pv[cc] = slot[(kMChunk - 1) * kStepD + piece_off(cc, y >> 1) + (y & 1)];
+    tick(2);
+    // 3. posteriors over the xi operands
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = kq + 4 * h;
+      double* orow = obb + c * kOBRow + (FWD ? k : kMChunk - 1 - k) * 16;
+#pragma unroll
+      for (int p = 0; p < 8; p++)
+        *reinterpret_cast<double2*>(orow + 2 * p) = make_double2(q[h][2 * p], q[h][2 * p + 1]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tick(3);
+    // 4. M1 counts, missing, P0
+#pragma unroll 4
+    for (int cc = 0; cc < kMSeq; cc++) {
+      const uint8_t* cd = es.codes + cc * es.Tr + kMG;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int k = 4 * h + kq;
+        const int i = ci * kMChunk + k;
+        const int t = FWD ? tB + i : tB - i;
+        const double qv = obb[cc * kOBRow + (FWD ? k : kMChunk - 1 - k) * 16 + y];
+        const int code = cd[t];
+        const bool obs = t >= 0 && code < M;
+        miss += (t >= 0 && code == M) ? qv : 0.0;
+        if (!FWD) p0 += t == -1 ? qv : 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          if (kq == r && obs)
+            __hip_atomic_fetch_add(es.H + code * 16 + y, qv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    tick(4);
+  }
+  if (a.diag && lane == 0)
+    for (int k = 0; k < 5; k++) a.diag[blockIdx.x * 24 + 8 + (FWD ? 0 : 5) + k] = pc[k];
+  wait_vm<0>();                      // no DMA left in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // the block's slab row (chain_estep_slab layout, summed over its sequences)
+  double* slab = a.counts + (size_t)blockIdx.x * chain_estep_slab(M);
+  const v4d dx = dx0 + dx1;
+  const int hoff = kSlabH + (FWD ? 0 : (M + 2) * 16);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int x = (lane >> 4) + 4 * r;                   // D row: the previous state
+    slab[(FWD ? kSlabKf : kSlabKb) + x * 16 + y] = dx[r];
+  }
+  for (int p = lane; p < M * 16; p += 64) slab[hoff + p] = es.H[p];
+  miss = sum_lanes16(sum_lanes32(miss));                  // the four steps kq of state y
+  if (!FWD) p0 = sum_lanes16(sum_lanes32(p0));
+  if (lane < 16) {
+    slab[hoff + M * 16 + y] = miss;
+    slab[hoff + (M + 1) * 16 + y] = 0.0;
+    if (!FWD) slab[chain_slab_p0(M) + y] = p0;
+  }
+}
 
 // Partner wave of one direction.
 // Phase A: each step's 2 KB of the block's scratch as two contiguous 1 KB
@@ -470,9 +703,10 @@ struct LL {
 // each chain's 8 steps as one contiguous 1 KB run per instruction (lane
 // L: step L >> 3 in address order, piece L & 7).  Without the 16-state
 // layout (PVEC false) or the LDS-DMA budget, the older 8-lane form is used.
-template <bool FWD, bool PVEC, bool DMA>
+template <bool FWD, bool PVEC, bool DMA, bool ES = false>
 __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, const double* zr,
-                                             double* Sblk, double* ob_lds, int lane, long b0, int nchA, int nchB) {
+                                             double* Sblk, double* ob_lds, int lane, long b0, int nchA, int nchB,
+                                             const uint8_t* codes, int Tr, const EsCtx* es = nullptr) {
   const int T = a.T, H = a.H;
   const int s = lane & 7, hi = lane >> 3;
   const int c = lane & 15, kq = lane >> 4;
@@ -485,8 +719,9 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
   const int kB = FWD ? hi : kMChunk - 1 - hi;
   auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
 
+  const uint8_t* lc = codes + c * Tr + kMG;   // chain c's codes (missing-step pairing of the ll)
   LL ll;
-  if (FWD) ll.init(a, lane);
+  if (FWD) ll.init(a, lane, lc[0] == a.M);
   // chain c's ring vector at slot step k (16 states, in lane)
   auto ring_vec = [&](const double* slot, int k, double (&v)[16]) {
 #pragma unroll
@@ -510,8 +745,9 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
     const bool all = dense || ci * kMChunk + kMChunk > n;
     const bool rs0 = all || (kq & (kRescale - 1)) == kRescale - 1;
     const bool rs1 = all || ((kq + 4) & (kRescale - 1)) == kRescale - 1;
-    ll.step(ll.dot(v0), LL::sum16(v0), za, rs0, i < n, t0 + i == T - 1);
-    ll.step(ll.dot(v1), LL::sum16(v1), zb, rs1, i + 4 < n, t0 + i + 4 == T - 1);
+    const int ta = t0 + i, tb = t0 + i + 4;
+    ll.step(ll.dot(v0), LL::sum16(v0), za, rs0, i < n, ta == T - 1, lc[ta] == a.M, lc[ta + 1] == a.M);
+    ll.step(ll.dot(v1), LL::sum16(v1), zb, rs1, i + 4 < n, tb == T - 1, lc[tb] == a.M, lc[tb + 1] == a.M);
     ll.renorm();
   };
   auto drainA = [&](int ci) {
@@ -536,6 +772,18 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
     barrier_lds(&wa);
   }
   if (nchA > 0) drainA(nchA - 1);
+  double pv[kMSeq];                  // e_step: previous step's vectors (lane: state lane & 15)
+  if (ES) {
+    // the forward partner's first xi (t = H) needs alpha_{H-1}: the last step
+    // of phase A in the ring (overwritten by phase B's first chunk), or the
+    // prior; the backward partner's first xi operand is unused (zero)
+    const int kl = (nA - 1) - (nchA - 1) * kMChunk;
+    const double* src = out + ((nchA - 1) & 1) * kSlotD + (kl > 0 ? kl : 0) * kStepD;
+    const int yy = lane & 15;
+#pragma unroll
+    for (int cc = 0; cc < kMSeq; cc++)
+      pv[cc] = !FWD ? 0.0 : nA > 0 ? src[piece_off(cc, yy >> 1) + (yy & 1)] : a.pi[yy];
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 
@@ -543,7 +791,9 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
   double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
   unsigned long long pw = 0, pl = 0, pd = 0;     // NIPAMD_WAIT_TIMES: DMA wait / drain / store cycles
 
-  if constexpr (PVEC && DMA) {
+  if constexpr (ES) {
+    estep_phase_b<FWD>(a, out, zr, Sblk, ob_lds, lane, b0, nchB, *es, ll, pv);
+  } else if constexpr (PVEC && DMA) {
     // LDS-DMA prefetch of the other direction's vectors: buffer k, chain C at
     // C * kOBRow doubles, rows = the chunk's 8 steps in address order
     const unsigned ob_base = (unsigned)(uintptr_t)ob_lds;
@@ -571,7 +821,8 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
         if (FWD && NIPAMD_MFMA_ABLATE != 14) {
           const int i = ci * kMChunk + k;
           const double zf = zs[k * kMSeq + c];           // phase B: the filter rescales every step
-          ll.step(ll.dot(v), zf, zf, true, i < nB, tB + i == T - 1);
+          const int t = tB + i;
+          ll.step(ll.dot(v), zf, zf, true, i < nB, t == T - 1, lc[t] == a.M, lc[t + 1] == a.M);
         }
         double pr[16];
 #pragma unroll
@@ -725,8 +976,8 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
       drainB(ci + 1, ob);
     }
   }
-  if (FWD) ll.write(a, b0, lane);
-  if (NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
+  if (FWD) ll.write(a, b0, lane, ES ? 3u : 1u);   // e_step: BAD_LUCK (nip.c:1827-1854)
+  if (!ES && NIPAMD_WAIT_TIMES && a.counts && lane == 0) {
     unsigned long long* st = reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 4;
     st[blockIdx.x * 8 + 2 + (FWD ? 0 : 1)] = wa.cyc;
     st[blockIdx.x * 8 + 6 + (FWD ? 0 : 1)] = wb.cyc;
@@ -739,7 +990,12 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
 
 constexpr int kOBD = 2 * 2 * kMSeq * kOBRow;       // DMA buffers [2 partners][2][16 chains][1 KB + 16 B pad]
 
-template <bool DMA>
+// e_step extras after the evidence table: applied-exponent rings [2 dirs][2][8][16]
+// (ints), the partners' M1 count tables [2][M][16]
+constexpr int kEsScrI = 2 * 2 * kMChunk * kMSeq;
+
+
+template <bool DMA, bool ES>
 __global__ __launch_bounds__(kMThreads, 1)
 void chain_fb_mfma_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -747,19 +1003,23 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   double* zr = out + kOutD;                                          // [2 slots][8][16]
   double* obuf = zr + kZD;                                           // DMA ? [2][2][16][128] : none
   double* Et = obuf + (DMA ? kOBD : 0);                              // [(M+2)][16]
-  uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * 16);   // [16][Tr]
+  int* scr = reinterpret_cast<int*>(Et + (a.M + 2) * 16);            // ES: [2 dirs][2][8][16]
+  double* Hc = reinterpret_cast<double*>(scr + (ES ? kEsScrI : 0));  // ES: [2][M][16]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(Hc + (ES ? 2 * a.M * 16 : 0));   // [16][Tr]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * kMSeq;
-  unsigned long long* rts = a.counts ? reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 12
-                                     : nullptr;     // diagnostics: wall-clock stamps
+  // diagnostics (fb only): a.counts carries the stamp buffer
+  unsigned long long* rts = (!ES && a.counts) ? reinterpret_cast<unsigned long long*>(a.counts) + (size_t)gridDim.x * 12
+                                              : nullptr;     // wall-clock stamps
   if (rts && tid == 0) {
     rts[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
     rts[blockIdx.x * 4 + 1] = __builtin_readcyclecounter();
   }
   const int T = a.T;
   const int Tr = chain_codes_row(T);
+  if (ES) diag_stamp(a, 0, tid);
 
   // --- stage the evidence table and the 16 sequences' observation codes
   for (int i = tid; i < (a.M + 2) * 16; i += kMThreads) Et[i] = a.Etab[i];
@@ -767,6 +1027,10 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
   for (int i = tid; i < kMSeq * Tr / 4; i += kMThreads)
     reinterpret_cast<uint32_t*>(codes)[i] = 0x01010101u * (uint32_t)a.M;   // missing / guard
+  if (ES) {     // e_step: ring slots a partial chunk leaves unwritten stay finite; counts start at 0
+    for (int i = tid; i < kOutD / 2; i += kMThreads) reinterpret_cast<double2*>(out)[i] = make_double2(0.0, 0.0);
+    for (int i = tid; i < 2 * a.M * 16; i += kMThreads) Hc[i] = 0.0;
+  }
   __syncthreads();
   if (a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kMSeq) {
     const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * (long)T);
@@ -795,33 +1059,49 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   }
   __syncthreads();
 
+  if (ES) diag_stamp(a, 1, tid);
   // optional phase timestamps (a.counts != nullptr in fb: NIPAMD_PHASE_TIMES)
-  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(a.counts);
+  unsigned long long* stamps = ES ? nullptr : reinterpret_cast<unsigned long long*>(a.counts);
   if (stamps && tid == 0) stamps[blockIdx.x * 4 + 0] = __builtin_readcyclecounter();
   const int H = a.H;
-  const int nA = (H > T - 1 - H ? H : T - 1 - H), nB = (T - H > H ? T - H : H);
+  const int nA = (H > T - 1 - H ? H : T - 1 - H);
+  const int nB = ES ? (T - H > H + 1 ? T - H : H + 1) : (T - H > H ? T - H : H);
   const int nchA = (nA + kMChunk - 1) / kMChunk, nchB = (nB + kMChunk - 1) / kMChunk;
   const bool fwd = (wave & 1) == 0;
   double* ring = out + (fwd ? 0 : 2 * kSlotD);
+  int* scr_d = scr + (fwd ? 0 : kEsScrI / 2);
   double* Sblk = a.S + (size_t)blockIdx.x * block_scratch(T) + kMG * kSStep;   // t = 0
-  const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
-                    ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
-                    ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
   if (wave >= 2) {
     double* ob = obuf + (fwd ? 0 : kOBD / 2);
-    if (pvec) {
-      if (fwd) partner_wave<true, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
-      else partner_wave<false, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+    if constexpr (ES) {
+      EsCtx es;
+      es.scr = scr_d;
+      es.H = Hc + (fwd ? 0 : a.M * 16);
+      es.codes = codes;
+      es.Tr = Tr;
+      es.Et = Et;
+      if (fwd) partner_wave<true, true, true, true>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB, codes, Tr, &es);
+      else partner_wave<false, true, true, true>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB, codes, Tr, &es);
+      diag_stamp(a, fwd ? 5 : 6, lane);
+      return;
     } else {
-      if (fwd) partner_wave<true, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
-      else partner_wave<false, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB);
+      const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
+                        ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
+                        ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
+      if (pvec) {
+        if (fwd) partner_wave<true, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB, codes, Tr);
+        else partner_wave<false, true, DMA>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB, codes, Tr);
+      } else {
+        if (fwd) partner_wave<true, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB, codes, Tr);
+        else partner_wave<false, false, false>(a, ring, zr, Sblk, ob, lane, b0, nchA, nchB, codes, Tr);
+      }
+      if (rts && fwd && lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rts[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+        rts[blockIdx.x * 4 + 3] = __builtin_readcyclecounter();
+      }
+      return;
     }
-    if (rts && fwd && lane == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      rts[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-      rts[blockIdx.x * 4 + 3] = __builtin_readcyclecounter();
-    }
-    return;
   }
   const long b = b0 + j;
   const bool active = b < a.B;
@@ -831,11 +1111,13 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   c.codes = codes + j * Tr + kMG;
   c.out = ring;
   c.zr = zr;
+  c.scr = ES ? scr_d : nullptr;
   c.zw = g == 0;
   c.wo0 = piece_off(j, g);
   c.wo1 = piece_off(j, 4 + g);
-  if (fwd) filter_wave<true>(a, c, Et, Sw, lane, active, b, nchA, nchB, stamps);
-  else filter_wave<false>(a, c, Et, Sw, lane, active, b, nchA, nchB, nullptr);
+  if (fwd) filter_wave<true, ES>(a, c, Et, Sw, lane, active, b, nchA, nchB, stamps);
+  else filter_wave<false, ES>(a, c, Et, Sw, lane, active, b, nchA, nchB, nullptr);
+  if (ES) diag_stamp(a, fwd ? 3 : 4, lane);
   if (stamps && tid == 0) stamps[blockIdx.x * 4 + 3] = __builtin_readcyclecounter();
 }
 
@@ -846,13 +1128,18 @@ size_t chain_mfma_lds_bytes(int M, int T) {       // without the DMA buffers
          (size_t)kMSeq * chain_codes_row(T);
 }
 
+size_t chain_estep_mfma_lds_bytes(int M, int T) {
+  return chain_mfma_lds_bytes(M, T) + (size_t)kOBD * sizeof(double) + (size_t)kEsScrI * sizeof(int) +
+         (size_t)2 * M * 16 * sizeof(double);
+}
+
 namespace {
-template <bool DMA>
+template <bool DMA, bool ES>
 int launch_mfma(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA>), lds, lds_set)) return -1;
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA, ES>), lds, lds_set)) return -1;
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
-  hipLaunchKernelGGL(chain_fb_mfma_kernel<DMA>, dim3(blocks), dim3(kMThreads), lds, stream, a);
+  hipLaunchKernelGGL((chain_fb_mfma_kernel<DMA, ES>), dim3(blocks), dim3(kMThreads), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace
@@ -861,8 +1148,14 @@ int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream) {
   const size_t base = (chain_mfma_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
   const size_t with_dma = base + (size_t)kOBD * sizeof(double);
   if (NIPAMD_MFMA_DMA && NIPAMD_MFMA_ABLATE != 12 && with_dma <= 160 * 1024)
-    return launch_mfma<true>(a, with_dma, stream);
-  return launch_mfma<false>(a, base, stream);
+    return launch_mfma<true, false>(a, with_dma, stream);
+  return launch_mfma<false, false>(a, base, stream);
+}
+
+int chain_estep_mfma_launch(const ChainArgs& a, hipStream_t stream) {
+  const size_t lds = (chain_estep_mfma_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024 || a.N > 16 || a.M > 16 || !a.counts) return -2;
+  return launch_mfma<true, true>(a, lds, stream);
 }
 
 }  // namespace nipamd

@@ -932,12 +932,28 @@ int nipamd_estep_partial_size(const nipamd_model* mm) {
   return mm->engine == NIPAMD_ENGINE_CHAIN ? -1 : ps;
 }
 
+// e_step kernel of the chain route: 2 = the 16-lane DPP kernel (one slab row
+// per sequence; the default), 1 = the matrix-core kernel (one row per
+// 16-sequence block), selected by NIPAMD_ESTEP_KERNEL=mfma.  Measured on
+// config 4: the matrix-core form is partner-bound (per 8-step
+// chunk ~19K cycles of xi / count / normaliser work against the filter's
+// ~4K), 22.4 ms against the DPP kernel's 13.4 ms per 131072 x 1024 shard.
+static int chain_estep_kernel(const nipamd_model* mm, int T) {
+  const auto& P = mm->m.chain;
+  const int M = P.emits[0].M;
+  const char* ek = std::getenv("NIPAMD_ESTEP_KERNEL");
+  const bool want_mfma = ek && std::string(ek) == "mfma";
+  if (want_mfma && P.N <= 16 && M <= 16 && nipamd::chain_estep_mfma_lds_bytes(M, T) <= 160 * 1024) return 1;
+  if (nipamd::chain_lds_bytes(M, T, true) <= 96 * 1024) return 2;
+  return 0;
+}
+
 static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r) {
   std::string why;
   if (mm->engine == NIPAMD_ENGINE_JTREE || !mm->m.chain.valid || !mm->m.chain.hmm) return false;
   if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why)) return false;
   if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0)) return false;   // evidence on the child only
-  return nipamd::chain_lds_bytes(mm->m.chain.emits[0].M, T, true) <= 96 * 1024;
+  return chain_estep_kernel(mm, T) != 0;
 }
 
 int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
@@ -959,6 +975,8 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   const int col = r.pcol;
   const int Mo = P.emits[0].M;
   const int S = nipamd::chain_estep_slab(Mo);
+  const bool mfma = chain_estep_kernel(mm, T) == 1;
+  const int per_row = mfma ? 16 : 1;            // sequences per slab row
   hipStream_t st = (hipStream_t)stream;
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   if (int rc = ensure_tables(mm)) return rc;
@@ -968,13 +986,14 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
   const long chunk = B < kEstepChunk ? B : kEstepChunk;
   const long nchunks = (B + kEstepChunk - 1) / kEstepChunk;
-  const long lvl = (chunk + 63) / 64;
-  const size_t work = ((size_t)chunk + 2 * lvl + nchunks + 64) * S * sizeof(double);
+  const long rows = (chunk + per_row - 1) / per_row;
+  const long lvl = (rows + 63) / 64;
+  const size_t work = ((size_t)rows + 2 * lvl + nchunks + 64) * S * sizeof(double);
   if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes((int)chunk, T))) return rc;
   if (int rc = ensure_work(mm, work)) return rc;
   DevState* d = dev_of(mm);
   double* slab = d->W;
-  double* tA = slab + (size_t)chunk * S;
+  double* tA = slab + (size_t)rows * S;
   double* tB = tA + (size_t)lvl * S;
   double* cres = tB + (size_t)lvl * S;
   const long ocols = n_obs > 0 ? n_obs : 1;
@@ -991,10 +1010,45 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.counts = slab;
-    if (nipamd::chain_estep_launch(a, st))
+#ifdef NIPAMD_DIAGNOSTICS
+    static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
+    const int nblk = (nb + 15) / 16;
+    if (mfma && times && c == 0) {
+      HIP_OK(hipMalloc(&a.diag, (size_t)nblk * 24 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 24 * sizeof(unsigned long long), st));
+    }
+#endif
+    const int lrc = mfma ? nipamd::chain_estep_mfma_launch(a, st) : nipamd::chain_estep_launch(a, st);
+    if (lrc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+#ifdef NIPAMD_DIAGNOSTICS
+    if (a.diag) {
+      std::vector<unsigned long long> h((size_t)nblk * 24);
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(h.data(), a.diag, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      (void)hipFree(a.diag);
+      unsigned long long t0 = ~0ull, tend = 0;
+      double d[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < nblk; k++) {
+        const unsigned long long* r = h.data() + (size_t)k * 24;
+        t0 = std::min(t0, r[0]);
+        for (int i = 1; i < 7; i++) { d[i] += (double)(r[i] - r[0]); tend = std::max(tend, r[i]); }
+      }
+      std::fprintf(stderr, "[nipamd] e_step blocks %d, launch span %.1f us; mean us from block entry: staged %.1f  "
+                   "phase A end %.1f  fwd filter end %.1f  bwd filter end %.1f  fwd partner end %.1f  "
+                   "bwd partner end %.1f\n", nblk, (tend - t0) / 100.0, d[1] / nblk / 100.0, d[2] / nblk / 100.0,
+                   d[3] / nblk / 100.0, d[4] / nblk / 100.0, d[5] / nblk / 100.0, d[6] / nblk / 100.0);
+      double pcs[10] = {0};
+      for (int k = 0; k < nblk; k++)
+        for (int i = 0; i < 10; i++) pcs[i] += (double)h[(size_t)k * 24 + 8 + i];
+      std::fprintf(stderr, "[nipamd] e_step partner phase-B cycles (wait / in-lane / xi / q / counts): "
+                   "fwd %.0f %.0f %.0f %.0f %.0f  bwd %.0f %.0f %.0f %.0f %.0f\n", pcs[0] / nblk, pcs[1] / nblk,
+                   pcs[2] / nblk, pcs[3] / nblk, pcs[4] / nblk, pcs[5] / nblk, pcs[6] / nblk, pcs[7] / nblk,
+                   pcs[8] / nblk, pcs[9] / nblk);
+    }
+#endif
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
-    if (reduce_rows(slab, nb, S, tA, tB, out, st))
+    if (reduce_rows(slab, (nb + per_row - 1) / per_row, S, tA, tB, out, st))
       return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
   }
   if (nchunks > 1 && reduce_rows(cres, nchunks, S, tA, tB, d_partial, st))
