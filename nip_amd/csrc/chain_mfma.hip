@@ -719,9 +719,13 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
   const int kB = FWD ? hi : kMChunk - 1 - hi;
   auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
 
-  const uint8_t* lc = codes + c * Tr + kMG;   // chain c's codes (missing-step pairing of the ll)
+  // e_step: chain c's codes, for the missing-step pairing of the ll (its
+  // em_learn stops on a positive total ll, nip.c:2224-2234); fb keeps the
+  // plain products (a missing step there contributes only rounding)
+  const uint8_t* lc = codes + c * Tr + kMG;
+  auto miss = [&](int t) { return ES && lc[t] == a.M; };
   LL ll;
-  if (FWD) ll.init(a, lane, lc[0] == a.M);
+  if (FWD) ll.init(a, lane, miss(0));
   // chain c's ring vector at slot step k (16 states, in lane)
   auto ring_vec = [&](const double* slot, int k, double (&v)[16]) {
 #pragma unroll
@@ -746,8 +750,8 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
     const bool rs0 = all || (kq & (kRescale - 1)) == kRescale - 1;
     const bool rs1 = all || ((kq + 4) & (kRescale - 1)) == kRescale - 1;
     const int ta = t0 + i, tb = t0 + i + 4;
-    ll.step(ll.dot(v0), LL::sum16(v0), za, rs0, i < n, ta == T - 1, lc[ta] == a.M, lc[ta + 1] == a.M);
-    ll.step(ll.dot(v1), LL::sum16(v1), zb, rs1, i + 4 < n, tb == T - 1, lc[tb] == a.M, lc[tb + 1] == a.M);
+    ll.step(ll.dot(v0), LL::sum16(v0), za, rs0, i < n, ta == T - 1, miss(ta), miss(ta + 1));
+    ll.step(ll.dot(v1), LL::sum16(v1), zb, rs1, i + 4 < n, tb == T - 1, miss(tb), miss(tb + 1));
     ll.renorm();
   };
   auto drainA = [&](int ci) {
@@ -821,8 +825,7 @@ __device__ __forceinline__ void partner_wave(const ChainArgs& a, double* out, co
         if (FWD && NIPAMD_MFMA_ABLATE != 14) {
           const int i = ci * kMChunk + k;
           const double zf = zs[k * kMSeq + c];           // phase B: the filter rescales every step
-          const int t = tB + i;
-          ll.step(ll.dot(v), zf, zf, true, i < nB, t == T - 1, lc[t] == a.M, lc[t + 1] == a.M);
+          ll.step(ll.dot(v), zf, zf, true, i < nB, tB + i == T - 1);
         }
         double pr[16];
 #pragma unroll
@@ -1022,25 +1025,24 @@ void chain_fb_mfma_kernel(ChainArgs a) {
   if (ES) diag_stamp(a, 0, tid);
 
   // --- stage the evidence table and the 16 sequences' observation codes
-  for (int i = tid; i < (a.M + 2) * 16; i += kMThreads) Et[i] = a.Etab[i];
   const int nseq = (int)((a.B - b0) < kMSeq ? (a.B - b0) : kMSeq);
   auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
-  for (int i = tid; i < kMSeq * Tr / 4; i += kMThreads)
-    reinterpret_cast<uint32_t*>(codes)[i] = 0x01010101u * (uint32_t)a.M;   // missing / guard
-  if (ES) {     // e_step: ring slots a partial chunk leaves unwritten stay finite; counts start at 0
-    for (int i = tid; i < kOutD / 2; i += kMThreads) reinterpret_cast<double2*>(out)[i] = make_double2(0.0, 0.0);
-    for (int i = tid; i < 2 * a.M * 16; i += kMThreads) Hc[i] = 0.0;
-  }
-  __syncthreads();
-  if (a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kMSeq) {
+  const bool fast = a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kMSeq;
+  if (fast) {
+    // contiguous [16][T] int32: every 16-byte load of the first pass issued
+    // before anything else (T = 1024: all of them), the guard bytes and the
+    // evidence table staged while they are in flight
     const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * (long)T);
     const int n4 = (kMSeq * T) >> 2;
-    for (int i0 = tid; i0 < n4; i0 += kMThreads * 8) {
-      int4 r[8];
+    constexpr int kLd = 16;
+    int4 r[kLd];
+    auto load = [&](int i0) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) if (i0 + k * kMThreads < n4) r[k] = src[i0 + k * kMThreads];
+      for (int k = 0; k < kLd; k++) if (i0 + k * kMThreads < n4) r[k] = src[i0 + k * kMThreads];
+    };
+    auto put = [&](int i0) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+      for (int k = 0; k < kLd; k++) {
         const int i4 = i0 + k * kMThreads;
         if (i4 < n4) {
           const int i = i4 << 2, cq = i / T, t = i - cq * T;
@@ -1049,12 +1051,39 @@ void chain_fb_mfma_kernel(ChainArgs a) {
           *reinterpret_cast<uint32_t*>(codes + cq * Tr + kMG + t) = packed;
         }
       }
+    };
+    load(tid);
+    for (int i = tid; i < (a.M + 2) * 16; i += kMThreads) Et[i] = a.Etab[i];
+    const int gw = kMG / 4, tw = (Tr - kMG - T) / 4;             // guard words before / after
+    for (int i = tid; i < kMSeq * (gw + tw); i += kMThreads) {
+      const int cq = i / (gw + tw), w = i - cq * (gw + tw);
+      const int off = w < gw ? 4 * w : kMG + T + 4 * (w - gw);
+      *reinterpret_cast<uint32_t*>(codes + cq * Tr + off) = 0x01010101u * (uint32_t)a.M;   // missing / guard
     }
-  } else if (a.obs) {
-    for (int i = tid; i < nseq * T; i += kMThreads) {
-      const int cq = i / T, t = i - cq * T;
-      codes[cq * Tr + kMG + t] =
-          (uint8_t)code_of(a.obs[(b0 + cq) * a.obs_bstride + (long)t * a.obs_tstride + a.obs_col]);
+    if (ES) {   // e_step: ring slots a partial chunk leaves unwritten stay finite; counts start at 0
+      for (int i = tid; i < kOutD / 2; i += kMThreads) reinterpret_cast<double2*>(out)[i] = make_double2(0.0, 0.0);
+      for (int i = tid; i < 2 * a.M * 16; i += kMThreads) Hc[i] = 0.0;
+    }
+    put(tid);
+    for (int i0 = tid + kMThreads * kLd; i0 < n4; i0 += kMThreads * kLd) {
+      load(i0);
+      put(i0);
+    }
+  } else {
+    for (int i = tid; i < (a.M + 2) * 16; i += kMThreads) Et[i] = a.Etab[i];
+    for (int i = tid; i < kMSeq * Tr / 4; i += kMThreads)
+      reinterpret_cast<uint32_t*>(codes)[i] = 0x01010101u * (uint32_t)a.M;   // missing / guard
+    if (ES) {
+      for (int i = tid; i < kOutD / 2; i += kMThreads) reinterpret_cast<double2*>(out)[i] = make_double2(0.0, 0.0);
+      for (int i = tid; i < 2 * a.M * 16; i += kMThreads) Hc[i] = 0.0;
+    }
+    __syncthreads();
+    if (a.obs) {
+      for (int i = tid; i < nseq * T; i += kMThreads) {
+        const int cq = i / T, t = i - cq * T;
+        codes[cq * Tr + kMG + t] =
+            (uint8_t)code_of(a.obs[(b0 + cq) * a.obs_bstride + (long)t * a.obs_tstride + a.obs_col]);
+      }
     }
   }
   __syncthreads();
