@@ -301,7 +301,8 @@ def main():
         workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (
             N, M, B, T)
     elif args.workload == "estep":
-        kname = "chain_kernel<true> + tree64 + finalize"
+        kname = ("chain_fb_mfma_kernel<true, true>" if os.environ.get("NIPAMD_ESTEP_KERNEL") == "mfma"
+                 else "chain_kernel<true>") + " + tree64 + finalize"
         workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
             N, M, B, T)
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
@@ -346,6 +347,29 @@ def main():
                          "exchange_bytes_per_rank": 8 * (model.param_size() + 2),
                          "note": "kernel_ms is the whole iteration on the launch stream "
                                  "(e_step kernels, exchange, finalize, host m_step)"}
+        if world == 1 and args.workload in ("fb", "config3", "config5"):
+            # PCIe-inclusive figure: the same batch from host
+            # buffers through nipamd_fb_host (H2D obs, kernels, D2H posteriors)
+            host_obs = np.ascontiguousarray(obs_np)
+            nip_amd.forward_backward_inference_host(model, host_obs, ov, [q])
+            t1 = time.perf_counter()
+            nip_amd.forward_backward_inference_host(model, host_obs, ov, [q])
+            el1 = time.perf_counter() - t1
+            rec["pcie_inclusive"] = {"value": B * T / el1, "unit": "sequence-timesteps/s", "ms": el1 * 1e3,
+                                     "note": "host buffers in and out (pageable), one call; not the headline"}
+        if args.workload == "config5":
+            # the in-clique marginalisation: 64^4 entries summed over the hidden
+            # parents on the GPU (fold.hip), once per model version
+            fms, fby = [], 0.0
+            for _ in range(5):
+                _, ms_f, fby = model.fold()
+                fms.append(ms_f)
+            fk = float(np.median(fms))
+            rec["fold"] = {"kernel": "fold_kernel", "kernel_ms": fk, "bytes": fby,
+                           "roofline": {"bound": "hbm", "achieved": fby / (fk * 1e-3) / 1e9,
+                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": fby / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                           "note": "A[x][y] = sum over Y1, Z1 of the 134 MB clique x priors, per model version"}
         if world == 1 and not args.no_cpu_baseline and args.workload == "generate":
             rec["cpu_baseline"] = cpu_baseline_generate(nodes, pots, T)
         elif world == 1 and not args.no_cpu_baseline and args.workload not in ("estep", "em"):

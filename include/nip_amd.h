@@ -135,6 +135,20 @@ int nipamd_model_gpu_supported(const nipamd_model* m, int n_obs,
 int nipamd_model_set_engine(nipamd_model* m, int engine);
 
 /*
+ * The interface chain's transition folded on the GPU (fold.hip): the
+ * in-clique's hidden parents summed out under their priors -- the
+ * marginalisation the reference repeats every time slice
+ * (nip_general_marginalise over the in-clique, src/nippotential.c:267-311),
+ * done once per model version.  keep = -1: out = A [64][64] (row = previous
+ * state); keep = j: out = hidden parent j's table [card_j][64][64].  cap =
+ * doubles available in out.  *kernel_ms: the kernel's time (HIP events),
+ * *bytes: in-clique bytes it streamed.  Synchronous, current device.  The
+ * engine calls the same code itself for in-cliques of >= 2^22 summed entries
+ * (config 5's 64^4); smaller ones fold on the host while compiling.
+ */
+int nipamd_model_fold(nipamd_model* m, int keep, double* out, long cap, double* kernel_ms, double* bytes);
+
+/*
  * The general engine's compiled schedule for a request (host only, no device
  * work): header hdr[29] (sizes and offsets of jtree.h's JtPlanDev, then L,
  * LDS flag, query row width), the int pool and the table pool.  sizes[0..1]

@@ -60,7 +60,7 @@ EXPORTS = [
     "nipamd_generate_host_draws", "nipamd_likelihood", "nipamd_likelihood_host",
     "nipamd_model_set_engine", "nipamd_jt_plan_dump", "nipamd_hugin_passes",
     "nipamd_model_num_cliques", "nipamd_model_num_sepsets", "nipamd_model_clique",
-    "nipamd_model_sepset", "nipamd_model_interface_cliques", "nipamd_model_set_tables",
+    "nipamd_model_sepset", "nipamd_model_interface_cliques", "nipamd_model_set_tables", "nipamd_model_fold",
 ]
 
 
@@ -234,6 +234,20 @@ class Model:
         if prev < 0:
             raise NipError(NIP_ERROR_INVALID_ARGUMENT, "bad engine %r" % engine)
         return prev
+
+    def fold(self, keep: int = -1, cards: int = 0):
+        """nipamd_model_fold: the interface chain's transition summed over the
+        in-clique's hidden parents on the GPU ([64][64], row = previous state),
+        or hidden parent `keep`'s table ([card][64][64], `cards` = its card).
+        Returns (table, kernel_ms, bytes streamed)."""
+        n = (cards if keep >= 0 else 1) * 64 * 64
+        out = np.zeros(n)
+        ms, by = C.c_double(0.0), C.c_double(0.0)
+        L = lib()
+        L.nipamd_model_fold.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_long, C.c_void_p, C.c_void_p]
+        _check(L.nipamd_model_fold(self._h, int(keep), out.ctypes.data_as(C.c_void_p), n,
+                                   C.byref(ms), C.byref(by)))
+        return (out.reshape(64, 64) if keep < 0 else out.reshape(cards, 64, 64)), ms.value, by.value
 
     def original(self, c: int) -> np.ndarray:
         n = lib().nipamd_model_original(self._h, c, None, 0)

@@ -657,11 +657,13 @@ void build_chain_plan(Model& m) {
     emits.push_back(std::move(E));
   }
   for (size_t v = 0; v < V.size(); v++) if (!seen[v]) return;   // every variable accounted for
-  // transition with the hidden parents summed out under their priors
+  // transition with the hidden parents summed out under their priors (large
+  // in-cliques: on the GPU, fold.hip, when the engine first needs it)
   P.A64.assign(64 * 64, 0.0);
   std::vector<int> val(V.size(), 0);
   std::vector<int> hv(hidden.size(), 0);
-  for (long hi = 0; hi < hsize; hi++) {
+  P.fold_gpu = !hidden.empty() && hsize * N * N >= kGpuFoldMin;
+  for (long hi = 0; hi < (P.fold_gpu ? 0 : hsize); hi++) {
     long r = hi;
     double w = 1.0;
     for (size_t k = 0; k < hidden.size(); k++) {

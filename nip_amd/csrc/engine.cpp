@@ -121,11 +121,34 @@ int ensure_device(nipamd_model* mm) {
   return 0;
 }
 
+}  // namespace
+
+// A deferred fold (large in-clique, ChainPlan::fold_gpu): A64 on the GPU, then
+// on the host for every host-side use (derived tables, likelihood, P.A).
+int nipamd::ensure_fold(nipamd_model* mm) {
+  auto& P = mm->m.chain;
+  if (!P.valid || !P.fold_gpu || P.folded) return 0;
+  if (int rc = ensure_device(mm)) return rc;
+  std::vector<double> A;
+  std::string err;
+  if (nipamd::chain_fold_gpu(mm->m, -1, A, &mm->fold_ms, &mm->fold_bytes, err))
+    return fail(NIPAMD_ERROR_DEVICE, "transition fold: " + err);
+  P.A64 = std::move(A);
+  if (P.N <= 16)
+    for (int x = 0; x < P.N; x++)
+      for (int y = 0; y < P.N; y++) P.A[x * 16 + y] = P.A64[x * 64 + y];
+  P.folded = true;
+  return 0;
+}
+
+namespace {
+
 // Upload the chain plan's tables to the current device (once per version).
 int ensure_tables(nipamd_model* mm) {
   if (int rc = ensure_device(mm)) return rc;
   DevState* d = dev_of(mm);
   if (d->version == mm->version && d->A64) return 0;
+  if (int rc = nipamd::ensure_fold(mm)) return rc;
   const auto& P = mm->m.chain;
   free_tables(d);
   if (P.N <= 16) {
@@ -152,7 +175,13 @@ int ensure_hidden(nipamd_model* mm, int j) {
   DevState* d = dev_of(mm);
   if (d->G[j]) return 0;
   std::vector<double> g;
-  nipamd::hidden_table(mm->m, j, g);
+  if (mm->m.chain.fold_gpu) {
+    std::string err;
+    double ms = 0, bytes = 0;
+    if (nipamd::chain_fold_gpu(mm->m, j, g, &ms, &bytes, err)) return fail(NIPAMD_ERROR_DEVICE, "hidden fold: " + err);
+  } else {
+    nipamd::hidden_table(mm->m, j, g);
+  }
   return upload(&d->G[j], g);
 }
 
@@ -485,6 +514,24 @@ int nipamd_jt_plan_dump(const nipamd_model* mm, int n_obs, const int* obs_vars, 
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   return nipamd::jt_plan_dump(mm, n_obs, obs_vars, n_query, query, estep, hdr, hdr_cap, ip, ip_cap, dp,
                               dp_cap, sizes);
+}
+
+int nipamd_model_fold(nipamd_model* mm, int keep, double* out, long cap, double* kernel_ms, double* bytes) {
+  if (!mm || !out) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const auto& P = mm->m.chain;
+  if (!P.valid) return fail(NIPAMD_ERROR_UNSUPPORTED, "the model has no interface-chain plan");
+  if (keep < -1 || keep >= (int)P.hidden.size()) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad hidden parent");
+  const long need = (keep < 0 ? 1L : (long)mm->m.vars[P.hidden[keep]].card) * 64 * 64;
+  if (cap < need) return fail(NIP_ERROR_INVALID_ARGUMENT, "output buffer too small");
+  if (int rc = ensure_device(mm)) return rc;
+  std::vector<double> v;
+  std::string err;
+  double ms = 0, by = 0;
+  if (nipamd::chain_fold_gpu(mm->m, keep, v, &ms, &by, err)) return fail(NIPAMD_ERROR_DEVICE, "fold: " + err);
+  std::copy(v.begin(), v.end(), out);
+  if (kernel_ms) *kernel_ms = ms;
+  if (bytes) *bytes = by;
+  return 0;
 }
 
 int nipamd_model_set_engine(nipamd_model* mm, int engine) {

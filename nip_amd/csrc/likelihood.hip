@@ -91,6 +91,7 @@ extern "C" int nipamd_likelihood(nipamd_model* mm, const int32_t* d_obs, int n_o
     return set_error(NIP_ERROR_INVALID_ARGUMENT, "likelihood: bad arguments");
   const ChainPlan& P = mm->m.chain;
   if (!P.valid) return set_error(NIPAMD_ERROR_UNSUPPORTED, "likelihood: the model has no interface-chain plan");
+  if (int rc = ensure_fold(mm)) return rc;
   const int N = P.N;
   LikArgs a{};
   a.ncol = n_obs;

@@ -89,7 +89,12 @@ struct ChainPlan {
   std::vector<double> pi;           // [16]
   // classic HMM (exactly prev, cur and one child): the e_step plan
   bool hmm = false;
+  // large in-cliques (>= kGpuFoldMin entries summed): A64 / A are folded on
+  // the GPU when the engine first needs them (fold.hip), not here
+  bool fold_gpu = false;
+  bool folded = false;
 };
+constexpr long kGpuFoldMin = 1L << 22;
 struct Model {
   std::vector<Var> vars;
   int node_size_x = 80, node_size_y = 60;
@@ -135,9 +140,17 @@ struct nipamd_model {
   unsigned version = 1;          // bumped whenever the tables change
   int engine = 0;                // NIPAMD_ENGINE_* (nipamd_model_set_engine)
   int estep_route = 0;           // layout of the last e_step partial: 0 chain, 1 general
+  double fold_ms = 0.0;          // the last GPU fold: kernel time and clique bytes streamed
+  double fold_bytes = 0.0;
 };
 
 namespace nipamd {
+// fold.hip: the chain plan's transition (keep = -1: A [64][64]) or hidden
+// parent j's table (keep = j: G_j [card][64][64]) summed on the current GPU
+int chain_fold_gpu(const Model& m, int keep, std::vector<double>& out, double* ms, double* bytes,
+                   std::string& err);
+// engine.cpp: complete a deferred fold (ChainPlan::fold_gpu) before host use of A64
+int ensure_fold(nipamd_model* mm);
 // generate.cpp: drop a model's cached generate_data tables (nipamd_model_free)
 void generate_release(const nipamd_model* mm);
 // jtree_plan.cpp: the general join-tree engine (jtree.h)
