@@ -91,10 +91,14 @@ struct WideArgs {
   double* ll;
   unsigned* status;
   int filter;            // forward_inference: H = 0, filtered posteriors, no scratch reads
+  unsigned long long* diag;   // diagnostics builds only (chain_wide4): per-block cycle counts, else null
 };
 __host__ __device__ inline long chain_scratch_row64(int T) { return (long)(T + 2 * kScratchGuard) * 64; }
 size_t chain_wide_lds_bytes(int ncol, int T);
 int chain_wide_launch(const WideArgs& a, hipStream_t stream);
+// 33..64 states, four filter waves per direction (chain_wide4.hip); -2: LDS does not fit
+size_t chain_wide4_lds_bytes(const WideArgs& a);
+int chain_wide4_launch(const WideArgs& a, hipStream_t stream);
 
 // matrix-core interface chains (chain_mfma_wide.hip): N <= 16 * NT states (NT = 1, 2),
 // up to four observed children, 16 sequences per 4-wave block

@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cstdint>
+#include <cstdlib>
+#include <string>
 #include <type_traits>
 
 #include "chain_kernels.h"
@@ -207,6 +209,16 @@ size_t chain_wide_lds_bytes(int ncol, int T) {
 }
 
 int chain_wide_launch(const WideArgs& a, hipStream_t stream) {
+  // 33..64 states: the four-waves-per-direction kernel (chain_wide4.hip);
+  // NIPAMD_WIDE_KERNEL=wave1 keeps this one-wave form for A/B measurements
+  static const bool wave1 = [] {
+    const char* e = std::getenv("NIPAMD_WIDE_KERNEL");
+    return e && std::string(e) == "wave1";
+  }();
+  if (a.N > 32 && !wave1) {
+    const int rc = chain_wide4_launch(a, stream);
+    if (rc != -2) return rc;
+  }
   const size_t lds = (chain_wide_lds_bytes(a.ncol, a.T) + 15) & ~(size_t)15;
   const dim3 grid((unsigned)a.B), block(128);
   if (a.N <= 16) hipLaunchKernelGGL(chain_wide_kernel<16>, grid, block, lds, stream, a);

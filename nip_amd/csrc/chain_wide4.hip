@@ -1,0 +1,382 @@
+// chain_wide4.hip -- forward-backward for interface chains of 33..64 states
+// (SURVEY 8(d) config 5 after the 64^4 in-clique is folded, fold.hip), up to
+// four observed children.  Same recursion as chain_wide.hip:
+//   alpha_t = e_t o A^T alpha_{t-1},  beta_t = A (e_{t+1} o beta_{t+1}),
+//   post_t = normalise(alpha_t o beta_t),  ll = sum_t log z2_t - log z1_t
+// (nip.c:1320-1581; two-filter smoothing, phase A / barrier / phase B).
+//
+// The 64-state mat-vec is latency-bound for one wave (a 64-deep FMA chain
+// per step), and B = 256 sequences give only 512 waves, so each direction of
+// a sequence gets four filter waves, wave w contracting the 16 inputs
+// k in [16w, 16w + 16) against its lane's column of A for all 64 outputs:
+//   part_w[y] = sum_k A[k][y] x[k]    (forward; backward: A[y][k])
+// The partials meet in LDS after one block barrier per step and every filter
+// wave sums them in the same order, so all four hold identical bits of u, p
+// and the next input (each keeps its own LDS copy of x for its broadcasts).
+// Rescaling (exact powers of two) happens every 4th step only.  Two partner
+// waves take the interface vectors from an LDS ring one step behind: scratch
+// stores (phase A), the other direction's vector from HBM and the normalised
+// posterior (phase B), and the forward ll -- all off the recursion's path.
+// Block: 8 filter waves + 2 partners = 640 threads, one sequence.
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cstdint>
+
+#include "chain_kernels.h"
+
+namespace nipamd {
+
+namespace {
+
+constexpr int kQ = 4;                    // filter waves per direction
+constexpr int kW4Threads = (2 * kQ + 2) * 64;
+constexpr int kW4Ring = 16;              // LDS ring depth (steps): two partner batches
+constexpr int kW4G = kScratchGuard;
+constexpr int kW4Rescale = 4;            // rescale interval (steps)
+
+template <int K>
+__device__ __forceinline__ double ror(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x120 + K, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x120 + K, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// fixed-order sum over the wave (identical bits in every lane)
+__device__ __forceinline__ double wave_sum(double x) {
+  x += ror<8>(x);
+  x += ror<4>(x);
+  x += ror<2>(x);
+  x += ror<1>(x);
+  {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    x = __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+  }
+  {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    x = __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+  }
+  return x;
+}
+
+// wave_sum of n independent values, stage by stage so their dependency
+// chains interleave
+__device__ __forceinline__ double pl16(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+__device__ __forceinline__ double pl32(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+template <int n>
+__device__ __forceinline__ void wave_sum_n(double (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += ror<8>(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += ror<4>(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += ror<2>(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] += ror<1>(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] = pl16(x[i]);
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] = pl32(x[i]);
+}
+
+__device__ __forceinline__ double recip(double c) {
+  double r = __builtin_amdgcn_rcp(c);
+  r = __builtin_fma(r, __builtin_fma(-c, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-c, r, 1.0), r);
+  return c != 0.0 ? r : 0.0;
+}
+
+__device__ __forceinline__ void block_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// LDS pointers typed as such, so every access is a ds_ instruction (a flat
+// access would also count in vmcnt and serialise on the HBM prefetches)
+typedef __attribute__((address_space(3))) double lds_d;
+typedef double v2d __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v2d lds_v2d;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+struct W4Lds {
+  lds_d* xb;         // [2 dirs][kQ][64]      each filter wave's copy of its next input
+  lds_d* pb;         // [2 dirs][2][kQ][64]   partials, double-buffered by step parity
+  lds_d* ring;       // [2 dirs][kW4Ring][64] interface vector of each step (fwd: alpha, bwd: beta)
+  lds_d* uring;      // [kW4Ring][64]         forward: u_t (the ll's m1 = sum u s)
+  lds_d* tab;        // evidence tables [(M_k + 2)][64] at toff_k, ebase [64] at eoff
+  int toff0, toff1, toff2, toff3;
+  int eoff;
+  lds_u8* codes;     // [ncol][Tr]
+  int Tr;
+};
+
+// e_t[y] = ebase[y] prod_k tab_k[code_k(t)][y]  (row M_k: the child's row sum,
+// for a missing value and the guards; row M_k + 1: 0, out of range)
+__device__ __forceinline__ double evidence(const WideArgs& a, const W4Lds& L, int t, int y) {
+  double e = L.tab[L.eoff + y];
+  const int toff[4] = {L.toff0, L.toff1, L.toff2, L.toff3};
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (k < a.ncol) e *= L.tab[toff[k] + L.codes[k * L.Tr + kW4G + t] * 64 + y];
+  return e;
+}
+
+// Phase loops: n_iter + 1 block barriers per phase for every wave; a filter
+// computes step i before barrier i + 1 (its partial before, the rest after
+// barrier i), a partner processes step i - 1 after barrier i.
+template <bool FWD>
+__device__ __forceinline__ void w4_filter(const WideArgs& a, const W4Lds& L, int w, int y, int nA, int nAi, int nB, int nBi) {
+  const int T = a.T, H = a.H;
+  const int d = FWD ? 0 : 1;
+  double Acol[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int kk = 16 * w + k;
+    Acol[k] = FWD ? a.A[kk * 64 + y] : a.A[y * 64 + kk];
+  }
+  lds_d* xb = L.xb + (d * kQ + w) * 64;   // this wave's copy of the next mat-vec input
+  int sc = 0;
+  if (FWD) {
+    xb[y] = a.pi[y];
+  } else if (nA + nB > 0) {
+    const double X = evidence(a, L, T - 1, y) * (y < a.N ? 1.0 : 0.0);   // e_{T-1} o beta_{T-1}
+    sc = -__builtin_amdgcn_frexp_exp(wave_sum(X));
+    xb[y] = X;
+  }
+  // diagnostics (a.diag): cycles before the barrier, waiting in it, after it
+  const bool dg = a.diag != nullptr;
+  unsigned long long tpre = 0, twait = 0, tpost = 0, tm = dg ? __builtin_readcyclecounter() : 0;
+  auto stamp = [&](unsigned long long& acc) {
+    if (dg) { const unsigned long long n = __builtin_readcyclecounter(); acc += n - tm; tm = n; }
+  };
+  const unsigned long long c0 = tm;
+  auto phase = [&](int n, int ni, int t0) {
+    double en = n > 0 ? evidence(a, L, t0, y) : 1.0;
+    for (int i = 0; i <= ni; i++) {
+      const bool act = i < n;
+      const int t = FWD ? t0 + i : t0 - i;
+      const double e = en;
+      lds_d* pb = L.pb + (d * 2 + (i & 1)) * kQ * 64;
+      if (act) {
+        const lds_v2d* xs = reinterpret_cast<const lds_v2d*>(xb + 16 * w);   // broadcast reads
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const v2d v = xs[k];
+          x[2 * k] = v.x; x[2 * k + 1] = v.y;
+        }
+        double p0 = Acol[0] * x[0], p1 = Acol[1] * x[1], p2 = Acol[2] * x[2], p3 = Acol[3] * x[3];
+#pragma unroll
+        for (int k = 4; k < 16; k += 4) {
+          p0 = __builtin_fma(Acol[k], x[k], p0); p1 = __builtin_fma(Acol[k + 1], x[k + 1], p1);
+          p2 = __builtin_fma(Acol[k + 2], x[k + 2], p2); p3 = __builtin_fma(Acol[k + 3], x[k + 3], p3);
+        }
+        pb[w * 64 + y] = (p0 + p1) + (p2 + p3);
+        if (i + 1 < n) en = evidence(a, L, FWD ? t + 1 : t - 1, y);     // the next step's
+      }
+      if (dg) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stamp(tpre);
+      block_barrier();
+      stamp(twait);
+      if (act) {
+        const double u = __builtin_ldexp((pb[y] + pb[64 + y]) + (pb[128 + y] + pb[192 + y]), sc);
+        const double p = u * e;
+        if (w == 0) {
+          const int slot = i & (kW4Ring - 1);
+          L.ring[(d * kW4Ring + slot) * 64 + y] = FWD ? p : u;
+          if (FWD) L.uring[slot * 64 + y] = u;
+        }
+        const bool rs = (i & (kW4Rescale - 1)) == kW4Rescale - 1 || i == n - 1;
+        sc = 0;
+        if (rs) sc = -__builtin_amdgcn_frexp_exp(wave_sum(p));   // frexp exponent of 0 is 0
+        xb[y] = p;
+      }
+      if (dg) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stamp(tpost);
+    }
+  };
+  // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
+  phase(nA, nAi, FWD ? 0 : T - 2);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
+  phase(nB, nBi, FWD ? H : H - 1);
+  if (dg && y == 0 && w == 0) {
+    a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 0] = __builtin_readcyclecounter() - c0;
+    a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 1] = twait;
+    a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 2] = tpre;
+    a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 3] = tpost;
+  }
+}
+
+// The partner processes step i - 1 after barrier i (the ring holds the
+// filter's vectors of the last 16 steps).
+template <bool FWD>
+__device__ __forceinline__ void w4_partner(const WideArgs& a, const W4Lds& L, int y, long b, int nA, int nAi, int nB, int nBi) {
+  const int T = a.T, H = a.H;
+  const int d = FWD ? 0 : 1;
+  double* const Srow = a.S + (size_t)b * chain_scratch_row64(T) + (size_t)kW4G * 64 + y;
+  double* const Prow = (a.post && y < a.N) ? a.post + (size_t)b * a.post_bstride + a.post_off + y : nullptr;
+  const double s = a.s[y];
+  double m2 = 1.0, m1 = 1.0, zmin = 1.0;
+  int e2 = 0, e1 = 0;
+  // forward ll (nip.c:1461-1474): z2 = sum alpha_t, z1 = sum u_t s, both on
+  // the same (power-of-two) scale; mantissas and exponents kept apart
+  auto ll_step = [&](int slot) {
+    double z[2] = {L.ring[slot * 64 + y], L.uring[slot * 64 + y] * s};
+    wave_sum_n<2>(z);
+    zmin = __builtin_fmin(zmin, z[0]);
+    m2 *= __builtin_amdgcn_frexp_mant(z[0]); e2 += __builtin_amdgcn_frexp_exp(z[0]);
+    m1 *= __builtin_amdgcn_frexp_mant(z[1]); e1 += __builtin_amdgcn_frexp_exp(z[1]);
+    const int k2 = __builtin_amdgcn_frexp_exp(m2), k1 = __builtin_amdgcn_frexp_exp(m1);
+    m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+    m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+  };
+  const unsigned long long c0 = a.diag ? __builtin_readcyclecounter() : 0;
+  if (!FWD && !a.filter) Srow[(long)(T - 1) * 64] = y < a.N ? 1.0 : 0.0;   // beta_{T-1}, T-1 >= H
+  // phase A: the interface vectors to the scratch
+  for (int i = 0; i <= nAi; i++) {
+    block_barrier();
+    const int j = i - 1;
+    if (j >= 0 && j < nA) {
+      const int slot = j & (kW4Ring - 1);
+      Srow[(long)(FWD ? j : T - 2 - j) * 64] = L.ring[(d * kW4Ring + slot) * 64 + y];
+      if (FWD) ll_step(slot);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // phase B: posterior = normalise(this o other); the other direction's
+  // vectors come from the scratch one 8-step chunk ahead, ping-ponged between
+  // two register sets (no register copy of a pending load)
+  const int tB = FWD ? H : H - 1;
+  auto tof = [&](int j) { return FWD ? tB + j : tB - j; };
+  // forward_inference reads a valid dummy row instead of the scratch
+  const double* const Sld = a.filter ? a.S + y : Srow;
+  const long sstr = a.filter ? 0 : 64;
+  auto load8 = [&](double (&r)[8], int c) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) r[k] = Sld[(long)tof(8 * c + k) * sstr];   // guards cover the over-run
+  };
+  auto chunk = [&](const double (&r)[8], int c) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      block_barrier();                               // iteration 8c + k + 1: step 8c + k is in the ring
+      const int j = 8 * c + k;
+      if (j < nB) {
+        const int slot = j & (kW4Ring - 1);
+        const double pr = L.ring[(d * kW4Ring + slot) * 64 + y] * (a.filter ? 1.0 : r[k]);
+        const double q = pr * recip(wave_sum(pr));   // an all-zero row stays zero
+        if (Prow) Prow[(long)tof(j) * a.post_tstride] = q;
+        if (FWD) ll_step(slot);
+      }
+    }
+  };
+  const int nch = nBi / 8;                           // nBi: a multiple of 8 (kernel)
+  double ra[8], rb[8];
+  load8(ra, 0);
+  block_barrier();                                   // iteration 0
+  for (int c = 0; c < nch; c += 2) {
+    load8(rb, c + 1);
+    chunk(ra, c);
+    if (c + 1 >= nch) break;
+    load8(ra, c + 2);
+    chunk(rb, c + 1);
+  }
+  if (a.diag && y == 0) a.diag[blockIdx.x * 16 + (FWD ? 8 : 12)] = __builtin_readcyclecounter() - c0;
+  if (FWD && y == 0) {
+    double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+    const bool dead = zmin == 0.0;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 1u : 0u;
+  }
+}
+
+__global__ __launch_bounds__(kW4Threads, 1)
+void chain_wide4_kernel(WideArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  lds_d* sm = (lds_d*)(smem);
+  W4Lds L;
+  L.xb = sm;
+  L.pb = L.xb + 2 * kQ * 64;
+  L.ring = L.pb + 2 * 2 * kQ * 64;
+  L.uring = L.ring + 2 * kW4Ring * 64;
+  lds_d* tab = L.uring + kW4Ring * 64;
+  int rows = 0, toff[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (k < a.ncol) { toff[k] = rows * 64; rows += a.M[k] + 2; }
+  L.toff0 = toff[0]; L.toff1 = toff[1]; L.toff2 = toff[2]; L.toff3 = toff[3];
+  L.eoff = rows * 64;
+  L.tab = tab;
+  lds_u8* codes = (lds_u8*)(tab + (rows + 1) * 64);
+  L.codes = codes;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long b = blockIdx.x;
+  const int T = a.T, Tr = chain_codes_row(T);
+  L.Tr = Tr;
+  // stage the evidence tables and this sequence's codes
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (k < a.ncol)
+      for (int i = tid; i < (a.M[k] + 2) * 64; i += kW4Threads) tab[toff[k] + i] = a.tab[k][i];
+  for (int i = tid; i < 64; i += kW4Threads) tab[L.eoff + i] = a.ebase[i];
+  for (int k = 0; k < a.ncol; k++) {
+    const int M = a.M[k];
+    for (int i = tid; i < Tr; i += kW4Threads) {
+      const int t = i - kW4G;
+      int c = M;                                      // missing / guard
+      if (t >= 0 && t < T) {
+        const int o = a.obs[b * a.obs_bstride + (long)t * a.obs_tstride + a.col[k]];
+        c = o < 0 ? M : (o < M ? o : M + 1);
+      }
+      codes[k * Tr + i] = (uint8_t)c;
+    }
+  }
+  __syncthreads();
+  const int H = a.H;
+  const bool filt = a.filter != 0;
+  // per-direction steps and the block-uniform iteration counts of each phase
+  const int nAf = filt ? 0 : H, nAb = filt ? 0 : T - 1 - H;
+  const int nBf = filt ? T : T - H, nBb = filt ? 0 : H;
+  // block-uniform iteration counts, multiples of the partners' 8-step batches
+  const int nAi = ((nAf > nAb ? nAf : nAb) + 7) & ~7;
+  const int nBi = ((nBf > nBb ? nBf : nBb) + 7) & ~7;
+  if (wave < kQ) w4_filter<true>(a, L, wave, lane, nAf, nAi, nBf, nBi);
+  else if (wave < 2 * kQ) w4_filter<false>(a, L, wave - kQ, lane, nAb, nAi, nBb, nBi);
+  else if (wave == 2 * kQ) w4_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
+  else w4_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
+}
+
+}  // namespace
+
+size_t chain_wide4_lds_bytes(const WideArgs& a) {
+  int rows = 0;
+  for (int k = 0; k < a.ncol; k++) rows += a.M[k] + 2;
+  return (size_t)(2 * kQ * 64 + 2 * 2 * kQ * 64 + 2 * kW4Ring * 64 + kW4Ring * 64 + (rows + 1) * 64) *
+             sizeof(double) +
+         (size_t)(a.ncol > 0 ? a.ncol : 1) * chain_codes_row(a.T);
+}
+
+int chain_wide4_launch(const WideArgs& a, hipStream_t stream) {
+  const size_t lds = (chain_wide4_lds_bytes(a) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024) return -2;
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel), lds, lds_set)) return -1;
+  hipLaunchKernelGGL(chain_wide4_kernel, dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace nipamd

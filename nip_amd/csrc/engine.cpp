@@ -751,8 +751,29 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     w.post = dst;
     w.post_bstride = dbs; w.post_tstride = dts; w.post_off = doff;
     w.ll = d_ll; w.status = d_status;
+#ifdef NIPAMD_DIAGNOSTICS
+    static const bool wtimes = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
+    if (wtimes && P.N > 32) {
+      HIP_OK(hipMalloc(&w.diag, (size_t)B * 16 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(w.diag, 0, (size_t)B * 16 * sizeof(unsigned long long), (hipStream_t)stream));
+    }
+#endif
     if (nipamd::chain_wide_launch(w, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+#ifdef NIPAMD_DIAGNOSTICS
+    if (w.diag) {
+      std::vector<unsigned long long> h((size_t)B * 16);
+      HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+      HIP_OK(hipMemcpy(h.data(), w.diag, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      (void)hipFree(w.diag);
+      double m[16] = {0};
+      for (int b = 0; b < B; b++)
+        for (int i = 0; i < 16; i++) m[i] += (double)h[(size_t)b * 16 + i] / B;
+      std::fprintf(stderr, "[nipamd] wide4 cycles (total / wait / before / after barrier): fwd filter %.0f / %.0f / %.0f / %.0f  "
+                   "bwd filter %.0f / %.0f / %.0f / %.0f  partners %.0f %.0f\n", m[0], m[1], m[2], m[3], m[4], m[5], m[6],
+                   m[7], m[8], m[12]);
+    }
+#endif
     return 0;
   }
   if (kind != kNarrowMfma && kind != kNarrowDpp)

@@ -130,3 +130,53 @@ def test_config3_scale_properties():
         rp, rl = orc.fb(o[b], ov, [m.variable("C1")])
         assert np.abs(post[b].cpu().numpy() - rp).max() <= 1e-12
         assert abs(ll[b].item() - rl) <= 1e-11 * abs(rl)
+
+
+# 33..64 states: chain_wide4_kernel (four filter waves per direction, one
+# barrier per step, sparse rescaling, partner waves for scratch/posterior/ll)
+@pytest.mark.parametrize("card,B,T", [(48, 3, 21), (40, 2, 2), (64, 2, 9), (33, 3, 1)])
+def test_wide4_demo1_vs_oracle(card, B, T):
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(card, seed=card))
+    ov = [m.variable("A1"), m.variable("B1")]
+    obs = synth.observations(B, T, card, seed=card + T, n_obs=2)
+    obs[0, ::4, 0] = -1                               # missing values on one child
+    check_vs_oracle(m, obs, ov, [m.variable("C1")], 1e-12, 1e-11)
+
+
+def test_wide4_filter_vs_oracle():
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(50, seed=3))
+    ov = [m.variable("A1"), m.variable("B1")]
+    q = [m.variable("C1")]
+    obs = synth.observations(3, 17, 50, seed=11, n_obs=2)
+    o = torch.from_numpy(obs).cuda()
+    post, ll, st = nip_amd.forward_inference(m, o, ov, q)
+    torch.cuda.synchronize()
+    post, ll = post.cpu().numpy(), ll.cpu().numpy()
+    orc = PortOracle(m.desc())
+    for b in range(obs.shape[0]):
+        rp, rl = orc.fb(obs[b], ov, q, filter_only=True)
+        assert np.abs(post[b] - rp).max() <= 1e-12
+        assert abs(ll[b] - rl) <= 1e-11 * max(1.0, abs(rl))
+
+
+def test_wide4_matches_one_wave_kernel_config5():
+    """Config 5 at full size: the four-wave kernel against the one-wave kernel
+    (NIPAMD_WIDE_KERNEL=wave1 in a child process: the switch is read once)."""
+    import subprocess, sys, os
+    code = (
+        "import numpy as np, torch, nip_amd\n"
+        "from nip_amd import synth\n"
+        "m = nip_amd.Model.from_spec(*synth.wide_spec(64, 16))\n"
+        "obs = torch.from_numpy(synth.observations(64, 128, 16, seed=6)).cuda()\n"
+        "p, l, s = nip_amd.forward_backward_inference(m, obs, [m.variable('O1')], [m.variable('X1')])\n"
+        "torch.cuda.synchronize()\n"
+        "np.savez(sys.argv[1], p=p.cpu().numpy(), l=l.cpu().numpy())\n")
+    outs = []
+    for env in ({}, {"NIPAMD_WIDE_KERNEL": "wave1"}):
+        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "wide4_%d.npz" % len(outs))
+        r = subprocess.run([sys.executable, "-c", "import sys\n" + code, path],
+                           env=dict(os.environ, **env), timeout=300)
+        assert r.returncode == 0
+        outs.append(np.load(path))
+    assert np.abs(outs[0]["p"] - outs[1]["p"]).max() <= 1e-12
+    assert np.all(np.abs(outs[0]["l"] - outs[1]["l"]) <= 1e-11 * np.maximum(1.0, np.abs(outs[1]["l"])))
