@@ -466,6 +466,7 @@ void nipamd_model_free(nipamd_model* mm) {
   if (!mm) return;
   nipamd::generate_release(mm);
   nipamd::jt_release(mm);
+  nipamd::likelihood_release(mm);
   DevState* d = static_cast<DevState*>(mm->m.dev);
   dev_release(d);
   delete d;

@@ -83,6 +83,14 @@ __global__ __launch_bounds__(256) void likelihood_kernel(LikArgs a) {
 
 using namespace nipamd;
 
+namespace {
+struct LikCache {
+  std::vector<int> key;      // model version, device, marked mask, column variables
+  int dev = -1;
+  double* d_all = nullptr;   // tables, then u [128], then ebase [64]
+};
+}  // namespace
+
 extern "C" int nipamd_likelihood(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                                  const int* marked, int B, int T, double* d_m1, double* d_m2,
                                  double* d_ll, void* stream) {
@@ -135,14 +143,36 @@ extern "C" int nipamd_likelihood(nipamd_model* mm, const int32_t* d_obs, int n_o
   all.insert(all.end(), u.begin(), u.end());
   const long off_e = (long)all.size();
   all.insert(all.end(), ebase.begin(), ebase.end());
-  double* d_all = nullptr;
-  hipError_t e = hipMalloc(&d_all, all.size() * sizeof(double));
+  // device tables cached per model, keyed by the model version, the device
+  // and the column set (as the fb path caches its request tables): a repeat
+  // call uploads nothing and stays asynchronous on `stream`
+  int dev = -1;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return set_error(NIPAMD_ERROR_DEVICE, std::string("likelihood: ") + hipGetErrorString(e));
+  std::vector<int> key{(int)mm->version, dev, (int)a.marked};
+  key.insert(key.end(), obs_vars, obs_vars + n_obs);
+  LikCache* lc = static_cast<LikCache*>(mm->lik);
+  if (!lc) mm->lik = lc = new LikCache();
   hipStream_t st = (hipStream_t)stream;
-  if (e == hipSuccess) e = hipMemcpyAsync(d_all, all.data(), all.size() * sizeof(double), hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) {
-    (void)hipFree(d_all);
-    return set_error(NIPAMD_ERROR_DEVICE, std::string("likelihood: ") + hipGetErrorString(e));
+  if (!lc->d_all || lc->key != key) {
+    if (lc->d_all) {
+      (void)hipDeviceSynchronize();                // an earlier launch may still read them
+      (void)hipSetDevice(lc->dev);
+      (void)hipFree(lc->d_all);
+      (void)hipSetDevice(dev);
+      lc->d_all = nullptr;
+    }
+    e = hipMalloc(&lc->d_all, all.size() * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(lc->d_all, all.data(), all.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(lc->d_all);
+      lc->d_all = nullptr;
+      return set_error(NIPAMD_ERROR_DEVICE, std::string("likelihood: ") + hipGetErrorString(e));
+    }
+    lc->key = key;
+    lc->dev = dev;
   }
+  double* d_all = lc->d_all;
   a.obs = d_obs;
   a.obs_bstride = (long)T * n_obs;
   a.obs_tstride = n_obs;
@@ -158,10 +188,22 @@ extern "C" int nipamd_likelihood(nipamd_model* mm, const int32_t* d_obs, int n_o
   const long n = (long)B * T;
   hipLaunchKernelGGL(likelihood_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
   e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(st);   // the tables are freed below
-  (void)hipFree(d_all);
   if (e != hipSuccess) return set_error(NIPAMD_ERROR_DEVICE, std::string("likelihood: ") + hipGetErrorString(e));
   return NIP_NO_ERROR;
+}
+
+void nipamd::likelihood_release(nipamd_model* mm) {
+  LikCache* lc = static_cast<LikCache*>(mm->lik);
+  if (!lc) return;
+  if (lc->d_all) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(lc->dev);
+    (void)hipFree(lc->d_all);
+    if (cur >= 0) (void)hipSetDevice(cur);
+  }
+  delete lc;
+  mm->lik = nullptr;
 }
 
 extern "C" int nipamd_likelihood_host(nipamd_model* mm, const int32_t* obs, int n_obs, const int* obs_vars,

@@ -142,6 +142,7 @@ struct nipamd_model {
   int estep_route = 0;           // layout of the last e_step partial: 0 chain, 1 general
   double fold_ms = 0.0;          // the last GPU fold: kernel time and clique bytes streamed
   double fold_bytes = 0.0;
+  void* lik = nullptr;           // likelihood.hip: device tables of the last column set
 };
 
 namespace nipamd {
@@ -151,6 +152,8 @@ int chain_fold_gpu(const Model& m, int keep, std::vector<double>& out, double* m
                    std::string& err);
 // engine.cpp: complete a deferred fold (ChainPlan::fold_gpu) before host use of A64
 int ensure_fold(nipamd_model* mm);
+// likelihood.hip: drop a model's cached likelihood tables (nipamd_model_free)
+void likelihood_release(nipamd_model* mm);
 // generate.cpp: drop a model's cached generate_data tables (nipamd_model_free)
 void generate_release(const nipamd_model* mm);
 // jtree_plan.cpp: the general join-tree engine (jtree.h)

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_wide.py tests/test_gpu_fold.py tests/test_gpu_filter.py tests/test_gpu_derived.py \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_wide.py tests/test_gpu_fold.py tests/test_gpu_filter.py tests/test_gpu_derived.py tests/test_gpu_likelihood.py tests/test_gpu_compat.py \
   -x -q --timeout 300 --timeout-method thread > gpurun_out/wide4_tests.log 2>&1
 echo "tests rc=$?" >> gpurun_out/wide4_tests.log
 NIPAMD_LIB=$PWD/nip_amd/_lib/variants/libnip_amd_diag.so NIPAMD_PHASE_TIMES=1 timeout -k 10 200 python bench.py --workload config5 --steps 2 --warmup 1 --no-check --no-cpu-baseline > gpurun_out/w4_diag.txt 2>&1 || exit 1
