@@ -55,6 +55,9 @@ WORKLOADS = {
     "config5": ("config5", lambda a: synth.wide_spec(64, 16), ["O1"], "X1", 256, 128),
     "generate": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 65536, 1024),
     "em": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024),
+    # the general join-tree engine (not a BASELINE config): a factorial HMM,
+    # two 4-state chains with one 16-state observation of both (interface {X1, Y1})
+    "jtree": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024),
 }
 
 
@@ -194,7 +197,8 @@ def main():
                          "e_step (config 4 per-GPU shard: counts + ll, no posterior write); "
                          "em: config 4, one step = one em_learn iteration (m_step, e_step of "
                          "the shard, the packed all-gather over RCCL, finalize); "
-                         "config3: demo1 @ 32 states smoothing; config5: wide-clique smoothing")
+                         "config3: demo1 @ 32 states smoothing; config5: wide-clique smoothing; "
+                         "jtree: a factorial HMM on the general join-tree engine")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
     args = ap.parse_args()
@@ -318,6 +322,12 @@ def main():
         workload = "generate_data: HMM-shaped DBN, %d hidden x %d observed states, B=%d series/GPU x T=%d" % (
             N, M, B, T)
         metric = "sequence-timesteps/s generate_data (sampling), 16-state DBN"
+    elif args.workload == "jtree":
+        kname = "jt_filter_kernel + jt_post_kernel"
+        bpu = 4 + 8 * N                # I/O only: the obs read, the posterior written
+        workload = ("general join-tree engine: factorial HMM, X and Y 4 states each, O1 16 states of both, "
+                    "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
+        metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
     elif args.workload == "config3":
         workload = "config3: demo1.net structure, 5 vars x 32 states, A1 B1 observed, C1 posterior, " \
                    "B=%d seq/GPU x T=%d" % (B, T)
@@ -347,6 +357,8 @@ def main():
                          "exchange_bytes_per_rank": 8 * (model.param_size() + 2),
                          "note": "kernel_ms is the whole iteration on the launch stream "
                                  "(e_step kernels, exchange, finalize, host m_step)"}
+        if args.workload == "jtree":
+            rec["roofline"]["note"] = "bytes are the request's I/O only; the engine is latency-bound (DESIGN.md 4)"
         if world == 1 and args.workload in ("fb", "config3", "config5"):
             # PCIe-inclusive figure: the same batch from host
             # buffers through nipamd_fb_host (H2D obs, kernels, D2H posteriors)

@@ -1,0 +1,373 @@
+// chain_ckpt.hip -- forward-backward for 16-state interface chains with
+// checkpoints and recomputation instead of the scratch round trip (config 2).
+//
+// chain_fb_mfma_kernel (chain_mfma.hip) hands every phase-A message to phase
+// B through HBM: alpha_t (t < H) and beta_t (t >= H) are written once and read
+// once, 256 of its 388 bytes per sequence-step.  Here phase A keeps one
+// message in four (checkpoints), and phase B recomputes each chunk's eight
+// messages from two of them -- two independent 4-step chains, interleaved --
+// on the partner SIMDs, one chunk at a time, in step with the filter that
+// consumes them:
+//
+//   SIMD 0: wave 0 forward filter (alpha, rings, z2)        wave 4 idle
+//   SIMD 1: wave 1 backward filter (beta)                    wave 5 idle
+//   SIMD 2: wave 2 forward partner (ll; phase A alpha         wave 6 recomputes
+//           checkpoints; phase B posterior of t >= H)                beta of t >= H
+//   SIMD 3: wave 3 backward partner (phase A beta             wave 7 recomputes
+//           checkpoints; phase B posterior of t < H)                 alpha of t < H
+//
+// (a workgroup's waves go to the CU's SIMDs round robin: wave w on SIMD w % 4).
+// The filters keep their SIMD's double-precision pipe to themselves; the
+// recompute wave's matrix-core chain shares a SIMD with the partner's in-lane
+// normalisation and stores.  HBM per sequence-step: the observation (4 B),
+// the posterior (128 B), checkpoints (2 x 32 B: written once, read once).
+//
+// Phase B rescales sparsely, like phase A (the forward partner sums alpha
+// itself for the ll).  Results agree with chain_fb_mfma_kernel's to the last
+// bits (tests/test_gpu_ckpt.py) and with the oracle within DESIGN.md's
+// tolerances.
+// The same recursion as nip.c:1320-1581 (forward_backward_inference), see
+// chain_kernels.hip for the derivation.
+#include "chain_mfma_core.h"
+
+namespace nipamd {
+
+namespace {
+
+constexpr int kCThreads = 512;   // 8 waves, two per SIMD
+
+// diagnostics builds (NIPAMD_WAIT_TIMES): per-wave cycle stamps, a.diag[block][wave][4] =
+// phase A, phase-barrier wait, phase B, phase-B barrier waits
+struct CkDiag {
+  unsigned long long t0 = 0, ta = 0, tb = 0;
+  WaitAcc wb;
+  __device__ __forceinline__ void stamp(unsigned long long& t) {
+    if (NIPAMD_WAIT_TIMES) t = __builtin_readcyclecounter();
+  }
+  __device__ __forceinline__ void write(const ChainArgs& a, int wave, int lane) {
+    if (!NIPAMD_WAIT_TIMES || !a.diag || lane != 0) return;
+    unsigned long long* d = a.diag + (size_t)blockIdx.x * 32 + wave * 4;
+    d[0] = ta - t0; d[1] = tb - ta; d[2] = __builtin_readcyclecounter() - tb; d[3] = wb.cyc;
+  }
+};
+
+// Message recomputation for the other direction's phase-B chunks.
+//   BWD_FOR_F (wave 6): beta_t for the forward filter's chunk ci, t = H + 8ci + k,
+//     from the checkpoint beta_{H + 8ci + 8} (or beta_{T-1} = 1), into ring row k;
+//   else (wave 7): alpha_t for the backward filter's chunk ci, t = H - 1 - 8ci - k,
+//     from the checkpoint alpha_{H - 9 - 8ci} (or alpha_{-1} = prior), into row k.
+// Chain<FWD> is the filter's own step (same operands, same rounding).
+template <bool FWD>
+__device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx& c, const double* Sw, int lane,
+                                               int nchA, int nchB, CkDiag& dg) {
+  const int j = lane & 15, g = lane >> 4;
+  const int sj = state_of(j & 3, j >> 2);
+  const int T = a.T, H = a.H;
+  Chain<FWD> ch;
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    ch.Aop[r] = FWD ? a.A[state_of(g, r) * 16 + sj] : a.A[sj * 16 + state_of(g, r)];
+  const v4d prior = load4(a.pi + 2 * g);
+  for (int ci = 0; ci < nchA; ci++) barrier_lds();
+  dg.stamp(dg.ta);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");                         // the partners' checkpoints
+  dg.stamp(dg.tb);
+
+  const int n = FWD ? H : T - H;                 // steps of the consuming filter's phase B
+  // A chunk's rows are two independent 4-step sub-chains h (rows 4h..4h+3),
+  // each from its own checkpoint, interleaved so that one's matrix-core
+  // latency hides the other's.  Start step of sub-chain h of chunk ci:
+  // backward the checkpoint above its rows (clamped to T-1), forward the one
+  // below them (-1: the prior).
+  auto start = [&](int ci, int h) {
+    if (FWD) {
+      const int lo = H - 4 - 8 * ci - 4 * h;     // lowest row's t (rows 4h + 3)
+      return lo > 0 ? lo - 1 : -1;
+    }
+    const int ts = H + 8 * ci + 4 * h + 4;
+    return ts < T - 1 ? ts : T - 1;
+  };
+  v4d ck0 = load4(Sw + (long)start(0, 0) * kSStep);   // one chunk ahead (guard rows cover t = -1)
+  v4d ck1 = load4(Sw + (long)start(0, 1) * kSStep);
+  Chain<FWD> c2 = ch;
+  for (int ci = 0; ci < nchB; ci++) {
+    double* slot = c.out + (ci & 1) * kSlotD;
+    const v4d cur0 = ck0, cur1 = ck1;
+    const int cn = ci + 1 < nchB ? ci + 1 : ci;
+    ck0 = load4(Sw + (long)start(cn, 0) * kSStep);
+    ck1 = load4(Sw + (long)start(cn, 1) * kSStep);
+    const int rem = n - 8 * ci;                  // steps of this chunk (<= 0: none)
+    if (rem > 0) {
+      v4d e[kMChunk];
+      if (FWD) {
+        const int hiT = H - 1 - 8 * ci;          // row k <-> t = hiT - k; valid rows k < rem
+#pragma unroll
+        for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + c.codes[hiT - k] * 16);
+        // sub-chain h starts below row 4h + 3 (or below the chunk's last valid row)
+        auto init = [&](Chain<FWD>& x, int h, const v4d& cur) {
+          const int ts = start(ci, h);
+          if (ts >= 0) {
+            x.X = cur;
+            x.sc = -__builtin_amdgcn_frexp_exp(chain_sum(cur));
+          } else {
+            x.X = prior;
+            x.sc = 0;
+          }
+        };
+        init(ch, 0, cur0);
+        init(c2, 1, cur1);
+        // rows 3..0 (sub-chain 0) and 7..4 (sub-chain 1), increasing t; a
+        // full chunk branch-free so that the two chains interleave
+        if (rem >= kMChunk) {
+#pragma unroll
+          for (int q = 3; q >= 0; q--) {
+            ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
+            c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 3; q >= 0; q--) {
+            if (q < rem) ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
+            if (q + 4 < rem) c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
+          }
+        }
+      } else {
+        const int lo = H + 8 * ci;               // row k <-> t = lo + k
+#pragma unroll
+        for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + c.codes[lo + k] * 16);
+        // sub-chain h: start row ks_h = start - lo (4h + 4, or the row of t = T - 1)
+        auto init = [&](Chain<FWD>& x, int h, const v4d& cur) {
+          const int ks = start(ci, h) - lo;
+          if (ks < 4 * h + 4) {
+            *reinterpret_cast<double2*>(slot + ks * kStepD + c.wo0) = make_double2(cur.x, cur.y);
+            *reinterpret_cast<double2*>(slot + ks * kStepD + c.wo1) = make_double2(cur.z, cur.w);
+          }
+          x.X = cur * load4(c.Et + c.codes[lo + ks] * 16);   // e at the start step (LDS, not a register pick)
+          x.sc = -__builtin_amdgcn_frexp_exp(chain_sum(x.X));
+          return ks;
+        };
+        const int ks0 = init(ch, 0, cur0);
+        const int ks1 = rem > 4 ? init(c2, 1, cur1) : 0;
+        if (ks0 == 4 && ks1 == kMChunk) {          // branch-free: the two chains interleave
+#pragma unroll
+          for (int q = 3; q >= 0; q--) {
+            ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
+            c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 3; q >= 0; q--) {
+            if (q < ks0) ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
+            if (q + 4 < ks1) c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
+          }
+        }
+      }
+    }
+    barrier_lds(&dg.wb);
+  }
+}
+
+template <bool FWD>
+__device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, const double* rring, const double* zr,
+                                           double* Sblk, int lane, long b0, int nchA, int nchB, CkDiag& dg) {
+  const int T = a.T, H = a.H;
+  const int s = lane & 7, hi = lane >> 3;
+  const int c = lane & 15, kq = lane >> 4;
+  const int nA = FWD ? H : T - 1 - H, nB = FWD ? T - H : H;
+  const int tA = FWD ? 0 : T - 2, tB = FWD ? H : H - 1;
+  constexpr int dir = FWD ? 1 : -1;
+  const int kB = FWD ? hi : kMChunk - 1 - hi;
+  auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
+
+  LL ll;
+  if (FWD) ll.init(a, lane, false);
+  auto ring_vec = [&](const double* slot, int k, double (&v)[16]) {
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+      const double2 x = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(c, p));
+      v[2 * p] = x.x; v[2 * p + 1] = x.y;
+    }
+  };
+  // phase A: the forward ll (as chain_mfma.hip's partner) and the checkpoints
+  auto drainA = [&](int ci) {
+    const double* slot = out + (ci & 1) * kSlotD;
+    if (FWD) {
+      double v0[16], v1[16];
+      ring_vec(slot, kq, v0);
+      ring_vec(slot, kq + 4, v1);
+      const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
+      const double za = zs[kq * kMSeq + c], zb = zs[(kq + 4) * kMSeq + c];
+      const int i = ci * kMChunk + kq;
+      const bool all = ci * kMChunk + kMChunk > nA;
+      const bool rs0 = all || (kq & (kRescale - 1)) == kRescale - 1;
+      const bool rs1 = all || ((kq + 4) & (kRescale - 1)) == kRescale - 1;
+      const int ta = tA + i, tb = tA + i + 4;
+      ll.step(ll.dot(v0), LL::sum16(v0), za, rs0, i < nA, ta == T - 1);
+      ll.step(ll.dot(v1), LL::sum16(v1), zb, rs1, i + 4 < nA, tb == T - 1);
+      ll.renorm();
+    }
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++) {
+      const int i = ci * kMChunk + k;
+      const int t = tA + dir * i;
+      // forward: alpha_{H-5-4m} >= 0; backward: beta_{H+4+4m} <= T-2
+      const bool ck = i < nA && (FWD ? (((H - 1 - t) & 3) == 0 && t <= H - 5) : (((t - H) & 3) == 0 && t >= H + 4));
+      if (!ck) continue;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int jj = q * 8 + hi;
+        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(jj, s));
+        *reinterpret_cast<double2*>(Sblk + (long)t * kSStep + jj * 16 + 2 * s) = v;
+      }
+    }
+  };
+  for (int ci = 0; ci < nchA; ci++) {
+    if (ci > 0) drainA(ci - 1);
+    barrier_lds();
+  }
+  if (nchA > 0) drainA(nchA - 1);
+  dg.stamp(dg.ta);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  dg.stamp(dg.tb);
+
+  double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
+  // chain c, slot steps kq and kq + 4: normalise(v o o) written over the ring vector
+  auto drainV = [&](int ci) {
+    double* slot = out + (ci & 1) * kSlotD;
+    const double* rs = rring + (ci & 1) * kSlotD;
+    const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = kq + 4 * h;
+      double v[16], o[16];
+      ring_vec(slot, k, v);
+      ring_vec(rs, k, o);
+      if (FWD) {
+        // phase B rescales like phase A (full chunks every kRescale-th step,
+        // partial ones every step): z2 summed here, zf published on rescales
+        const int i = ci * kMChunk + k;
+        const bool rs = ci * kMChunk + kMChunk > nB || (k & (kRescale - 1)) == kRescale - 1;
+        ll.step(ll.dot(v), LL::sum16(v), zs[k * kMSeq + c], rs, i < nB, tB + i == T - 1);
+      }
+      double pr[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) pr[i] = v[i] * o[i];
+      double z0 = pr[0] + pr[1], z1 = pr[2] + pr[3], z2 = pr[4] + pr[5], z3 = pr[6] + pr[7];
+      z0 += pr[8] + pr[9]; z1 += pr[10] + pr[11]; z2 += pr[12] + pr[13]; z3 += pr[14] + pr[15];
+      const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
+#pragma unroll
+      for (int p = 0; p < 8; p++)
+        *reinterpret_cast<double2*>(slot + k * kStepD + piece_off(c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
+    }
+    if (FWD) ll.renorm();
+  };
+  // chain q's 8 steps as one contiguous 1 KB run per store instruction
+  auto store_pass = [&](int ci) {
+    const double* slot = out + (ci & 1) * kSlotD;
+    const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
+    const bool ok = kB < nk;
+    double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s;
+#pragma unroll
+    for (int q = 0; q < kMSeq; q++) {
+      const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
+      double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
+      *reinterpret_cast<double2*>(p) = v;
+    }
+  };
+  for (int ci = 0; ci < nchB; ci++) {
+    barrier_lds(&dg.wb);
+    drainV(ci);
+    store_pass(ci);
+  }
+  if (FWD) ll.write(a, b0, lane, 1u);
+}
+
+__global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* out = reinterpret_cast<double*>(smem);     // filter rings [2 dirs][2 slots][8][16][16]
+  double* rr = out + kOutD;                          // recomputed rings [2 dirs][2 slots][8][16][16]
+  double* zr = rr + kOutD;                           // [2 slots][8][16]
+  double* Et = zr + kZD;                             // [(M+2)][16]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * 16);   // [16][Tr]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const long b0 = (long)blockIdx.x * kMSeq;
+  const int T = a.T;
+  const int Tr = chain_codes_row(T);
+  stage_codes<kCThreads>(a, b0, tid, Et, codes, Tr, [] {});
+  __syncthreads();
+  CkDiag dg;
+  dg.stamp(dg.t0);
+
+  const int H = a.H;
+  const int nA = (H > T - 1 - H ? H : T - 1 - H);
+  const int nB = (T - H > H ? T - H : H);
+  const int nchA = (nA + kMChunk - 1) / kMChunk, nchB = (nB + kMChunk - 1) / kMChunk;
+  double* Sblk = a.S + (size_t)blockIdx.x * block_scratch(T) + kMG * kSStep;   // t = 0
+  const int role = wave & 3;
+  const bool fwd = (wave & 1) == 0;
+  double* ring = out + (fwd ? 0 : 2 * kSlotD);      // the filter's ring of this side
+  // recomputed ring consumed with it: the forward side's beta (wave 6), the backward side's alpha (wave 7)
+  double* rring = rr + (fwd ? 0 : 2 * kSlotD);
+  if (wave == 4 || wave == 5) {                      // idle on the filters' SIMDs: barriers only
+    for (int ci = 0; ci < nchA; ci++) barrier_lds();
+    dg.stamp(dg.ta);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    dg.stamp(dg.tb);
+    for (int ci = 0; ci < nchB; ci++) barrier_lds(&dg.wb);
+    dg.write(a, wave, lane);
+    return;
+  }
+  if (role >= 2 && wave < 4) {
+    if (fwd) ck_partner<true>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
+    else ck_partner<false>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
+    dg.write(a, wave, lane);
+    return;
+  }
+  WaveCtx c;
+  c.Et = Et + 2 * g;
+  c.codes = codes + j * Tr + kMG;
+  c.zr = zr;
+  c.scr = nullptr;
+  c.wo0 = piece_off(j, g);
+  c.wo1 = piece_off(j, 4 + g);
+  double* Sw = Sblk + j * 16 + 2 * g;
+  if (wave >= 6) {
+    c.out = rring;
+    c.zw = false;
+    if (fwd) recompute_wave<false>(a, c, Sw, lane, nchA, nchB, dg);   // wave 6: beta for the forward side
+    else recompute_wave<true>(a, c, Sw, lane, nchA, nchB, dg);        // wave 7: alpha for the backward side
+    dg.write(a, wave, lane);
+    return;
+  }
+  c.out = ring;
+  c.zw = g == 0;
+  if (fwd) filter_wave<true, false, true>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
+  else filter_wave<false, false, true>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
+  dg.tb = dg.ta = dg.t0;                             // the filters: total only (slot 2)
+  dg.write(a, wave, lane);
+}
+
+}  // namespace
+
+size_t chain_fb_ckpt_lds_bytes(int M, int T) {
+  return (size_t)(2 * kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * 16 * sizeof(double) +
+         (size_t)kMSeq * chain_codes_row(T);
+}
+
+int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream) {
+  const size_t lds = (chain_fb_ckpt_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
+  const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
+                    ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
+  if (lds > 160 * 1024 || !pvec || a.T < 2) return -2;
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel), lds, lds_set)) return -1;
+  const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
+  hipLaunchKernelGGL(chain_fb_ckpt_kernel, dim3(blocks), dim3(kCThreads), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace nipamd

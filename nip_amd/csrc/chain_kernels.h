@@ -201,9 +201,13 @@ int rand_window_launch(int B, const uint32_t* qd_base, uint32_t* win, hipStream_
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
-// matrix-core variant (chain_mfma.hip): 16 sequences per 2-wave block
+// matrix-core variant (chain_mfma.hip): 16 sequences per 4-wave block
 size_t chain_mfma_lds_bytes(int M, int T);
 int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream);
+// checkpoint + recompute variant (chain_ckpt.hip, 8-wave block, N = 16
+// posterior rows); -2 when the request does not fit it
+size_t chain_fb_ckpt_lds_bytes(int M, int T);
+int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core e_step (N, M <= 16): one slab row per 16-sequence block (the
 // sums over its sequences); -2 when the request does not fit the kernel
 size_t chain_estep_mfma_lds_bytes(int M, int T);

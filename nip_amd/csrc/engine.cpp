@@ -801,6 +801,9 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     HIP_OK(hipMalloc(&stamps, (size_t)nblk * 24 * sizeof(unsigned long long)));
     HIP_OK(hipMemsetAsync(stamps, 0, (size_t)nblk * 24 * sizeof(unsigned long long), (hipStream_t)stream));
     a.counts = reinterpret_cast<double*>(stamps);
+    // chain_ckpt.hip's per-wave stamps [block][8 waves][4]
+    HIP_OK(hipMalloc(&a.diag, (size_t)nblk * 32 * sizeof(unsigned long long)));
+    HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 32 * sizeof(unsigned long long), (hipStream_t)stream));
   }
 #endif
   const int rc = kind == kNarrowMfma ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
@@ -812,6 +815,21 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     HIP_OK(hipMemcpy(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     (void)hipFree(stamps);
     phase_report(h.data(), nblk);
+    std::vector<unsigned long long> w((size_t)nblk * 32);
+    HIP_OK(hipMemcpy(w.data(), a.diag, w.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    (void)hipFree(a.diag);
+    double m[32] = {0};
+    for (int k = 0; k < nblk; k++)
+      for (int i = 0; i < 32; i++) m[i] += (double)w[(size_t)k * 32 + i] / nblk;
+    if (m[2] > 0) {
+      std::fprintf(stderr, "[nipamd] ckpt kernel cycles per wave (phase A / phase-barrier wait / phase B / "
+                   "phase-B barrier waits):\n");
+      static const char* names[8] = {"fwd filter", "bwd filter", "fwd partner", "bwd partner", "idle 4", "idle 5",
+                                     "beta recompute", "alpha recompute"};
+      for (int v = 0; v < 8; v++)
+        std::fprintf(stderr, "[nipamd]   %-16s %9.0f %9.0f %9.0f %9.0f\n", names[v], m[v * 4], m[v * 4 + 1],
+                     m[v * 4 + 2], m[v * 4 + 3]);
+    }
   }
 #endif
   if (rc)
