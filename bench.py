@@ -296,8 +296,10 @@ def main():
         kname = "chain_mfma_wide_kernel<%d>" % (1 if N <= 16 else 2)
     elif not narrow:
         kname = "chain_wide_kernel<%d>" % (16 if N <= 16 else 32 if N <= 32 else 64)
-    elif os.environ.get("NIPAMD_FB_KERNEL") != "dpp":
+    elif os.environ.get("NIPAMD_FB_KERNEL") == "scratch":
         kname = "chain_fb_mfma_kernel"
+    elif os.environ.get("NIPAMD_FB_KERNEL") != "dpp":
+        kname = "chain_fb_ckpt_kernel"     # 16-state posteriors (config 2); else chain_fb_mfma_kernel
     else:
         kname = "chain_kernel<false>"
     metric = METRIC

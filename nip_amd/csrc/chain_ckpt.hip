@@ -35,38 +35,67 @@ namespace nipamd {
 namespace {
 
 constexpr int kCThreads = 512;   // 8 waves, two per SIMD
+// Evidence rows 144 B apart: row r starts at bank 36r mod 64, so sixteen
+// chains reading sixteen different rows (16 B per lane) hit distinct banks
+// (a 128-B stride maps every row to bank 0 or 32: up to 4-way conflicts)
+constexpr int kEtStride = 18;
 
-// diagnostics builds (NIPAMD_WAIT_TIMES): per-wave cycle stamps, a.diag[block][wave][4] =
-// phase A, phase-barrier wait, phase B, phase-B barrier waits
+// Ring layout (one step = 16 chains x 16 states): chain j of row k at
+// position j ^ (k & 1), its eight 16-byte pieces XOR-swizzled by j >> 1.
+// Every access pattern of this kernel is then free of LDS bank conflicts
+// (filter and recompute row writes, the partner's per-chain reads and writes,
+// the store pass's per-step reads, the checkpoint reads), where chain_mfma.hip's
+// (j & 7) swizzle leaves the partner's reads 2-way.
+__device__ __forceinline__ int ck_off(int k, int j, int p) {
+  return k * kStepD + ((j ^ (k & 1)) << 4) + ((p ^ ((j >> 1) & 7)) << 1);
+}
+
+// diagnostics builds (NIPAMD_WAIT_TIMES): per-wave cycle stamps, a.diag[block][wave][5] =
+// phase A, phase-barrier wait, phase B, phase-B barrier waits, SIMD id (HW_ID[5:4])
 struct CkDiag {
   unsigned long long t0 = 0, ta = 0, tb = 0;
+  unsigned long long x1 = 0, x2 = 0, tx = 0;   // recompute waves: chunk set-up / steps cycles
+  bool rc = false;
   WaitAcc wb;
+  __device__ __forceinline__ void lap(unsigned long long* acc) {
+    if (!NIPAMD_WAIT_TIMES) return;
+    const unsigned long long t = __builtin_readcyclecounter();
+    if (acc) *acc += t - tx;
+    tx = t;
+  }
   __device__ __forceinline__ void stamp(unsigned long long& t) {
     if (NIPAMD_WAIT_TIMES) t = __builtin_readcyclecounter();
   }
   __device__ __forceinline__ void write(const ChainArgs& a, int wave, int lane) {
     if (!NIPAMD_WAIT_TIMES || !a.diag || lane != 0) return;
-    unsigned long long* d = a.diag + (size_t)blockIdx.x * 32 + wave * 4;
-    d[0] = ta - t0; d[1] = tb - ta; d[2] = __builtin_readcyclecounter() - tb; d[3] = wb.cyc;
+    unsigned long long* d = a.diag + (size_t)blockIdx.x * 40 + wave * 5;
+    d[0] = rc ? x1 : ta - t0; d[1] = rc ? x2 : tb - ta; d[2] = __builtin_readcyclecounter() - tb; d[3] = wb.cyc;
+    d[4] = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3;   // hwreg(HW_REG_HW_ID)
   }
 };
 
 // Message recomputation for the other direction's phase-B chunks.
-//   BWD_FOR_F (wave 6): beta_t for the forward filter's chunk ci, t = H + 8ci + k,
-//     from the checkpoint beta_{H + 8ci + 8} (or beta_{T-1} = 1), into ring row k;
-//   else (wave 7): alpha_t for the backward filter's chunk ci, t = H - 1 - 8ci - k,
-//     from the checkpoint alpha_{H - 9 - 8ci} (or alpha_{-1} = prior), into row k.
-// Chain<FWD> is the filter's own step (same operands, same rounding).
+//   !FWD (wave 6): beta_t for the forward filter's chunk ci, t = H + 8ci + k, into
+//     ring row k; sub-chain h (rows 4h..4h+3) from beta_{H+8ci+4h+4} (a
+//     checkpoint, or beta_{T-1} = 1 written by the backward filter);
+//   FWD (wave 7): alpha_t for the backward filter's chunk ci, t = H - 1 - 8ci - k,
+//     into row k; sub-chain h from alpha_{H-5-8ci-4h} (a checkpoint, or the
+//     prior alpha_{-1}).
+// The two sub-chains of a chunk are independent: interleaved, one's
+// matrix-core latency hides the other's.  Each starts from a vector rescaled
+// to sum ~1 and runs at most four steps without rescaling (the bound phase A's
+// sparse rescaling already relies on); the posterior normalisation removes
+// the scale.  The next chunk's evidence vectors and the checkpoints two
+// chunks ahead are loaded while a chunk runs.
 template <bool FWD>
 __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx& c, const double* Sw, int lane,
                                                int nchA, int nchB, CkDiag& dg) {
   const int j = lane & 15, g = lane >> 4;
   const int sj = state_of(j & 3, j >> 2);
   const int T = a.T, H = a.H;
-  Chain<FWD> ch;
+  double Aop[4];
 #pragma unroll
-  for (int r = 0; r < 4; r++)
-    ch.Aop[r] = FWD ? a.A[state_of(g, r) * 16 + sj] : a.A[sj * 16 + state_of(g, r)];
+  for (int r = 0; r < 4; r++) Aop[r] = FWD ? a.A[state_of(g, r) * 16 + sj] : a.A[sj * 16 + state_of(g, r)];
   const v4d prior = load4(a.pi + 2 * g);
   for (int ci = 0; ci < nchA; ci++) barrier_lds();
   dg.stamp(dg.ta);
@@ -75,96 +104,109 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
   dg.stamp(dg.tb);
 
   const int n = FWD ? H : T - H;                 // steps of the consuming filter's phase B
-  // A chunk's rows are two independent 4-step sub-chains h (rows 4h..4h+3),
-  // each from its own checkpoint, interleaved so that one's matrix-core
-  // latency hides the other's.  Start step of sub-chain h of chunk ci:
-  // backward the checkpoint above its rows (clamped to T-1), forward the one
-  // below them (-1: the prior).
+  auto tof = [&](int ci, int k) { return FWD ? H - 1 - 8 * ci - k : H + 8 * ci + k; };   // t of row k
+  // start step of sub-chain h: backward above its rows (clamped to T-1),
+  // forward below them (-1: the prior)
   auto start = [&](int ci, int h) {
     if (FWD) {
-      const int lo = H - 4 - 8 * ci - 4 * h;     // lowest row's t (rows 4h + 3)
+      const int lo = H - 4 - 8 * ci - 4 * h;
       return lo > 0 ? lo - 1 : -1;
     }
     const int ts = H + 8 * ci + 4 * h + 4;
     return ts < T - 1 ? ts : T - 1;
   };
-  v4d ck0 = load4(Sw + (long)start(0, 0) * kSStep);   // one chunk ahead (guard rows cover t = -1)
-  v4d ck1 = load4(Sw + (long)start(0, 1) * kSStep);
-  Chain<FWD> c2 = ch;
-  for (int ci = 0; ci < nchB; ci++) {
+  auto ld = [&](int ci, int h) { return load4(Sw + (long)start(ci < nchB ? ci : nchB - 1, h) * kSStep); };
+  auto ldE = [&](int ci, v4d (&E)[kMChunk]) {
+    const int cc = ci < nchB ? ci : nchB - 1;
+#pragma unroll
+    for (int k = 0; k < kMChunk; k++) E[k] = load4(c.Et + c.codes[tof(cc, k)] * c.es);
+  };
+  auto row = [&](double* slot, int k, const v4d& v) {
+    double* L = slot + k * kStepD + ((k & 1) ? c.wodd : 0);
+    *reinterpret_cast<double2*>(L + c.wo0) = make_double2(v.x, v.y);
+    *reinterpret_cast<double2*>(L + c.wo1) = make_double2(v.z, v.w);
+  };
+  // one step of a sub-chain: X -> the row's vector, X <- the next input
+  auto step = [&](v4d& X, int sc, double* slot, int k, const v4d& e) {
+    const v4d u = ldexp4(matvec(Aop, X), sc);
+    const v4d p = u * e;
+    row(slot, k, FWD ? p : u);
+    X = p;
+  };
+  auto norm_exp = [](const v4d& v) { return -__builtin_amdgcn_frexp_exp(chain_sum(v)); };
+
+  v4d P0 = ld(0, 0), P1 = ld(0, 1), Q0 = ld(1, 0), Q1 = ld(1, 1);
+  v4d Ea[kMChunk], Eb[kMChunk];
+  ldE(0, Ea);
+  dg.rc = true;
+  auto chunk = [&](int ci, v4d& R0, v4d& R1, const v4d (&E)[kMChunk], v4d (&En)[kMChunk]) {
+    dg.lap(nullptr);
     double* slot = c.out + (ci & 1) * kSlotD;
-    const v4d cur0 = ck0, cur1 = ck1;
-    const int cn = ci + 1 < nchB ? ci + 1 : ci;
-    ck0 = load4(Sw + (long)start(cn, 0) * kSStep);
-    ck1 = load4(Sw + (long)start(cn, 1) * kSStep);
-    const int rem = n - 8 * ci;                  // steps of this chunk (<= 0: none)
-    if (rem > 0) {
-      v4d e[kMChunk];
-      if (FWD) {
-        const int hiT = H - 1 - 8 * ci;          // row k <-> t = hiT - k; valid rows k < rem
+    const v4d cur0 = R0, cur1 = R1;
+    R0 = ld(ci + 2, 0);
+    R1 = ld(ci + 2, 1);
+    ldE(ci + 1, En);
+    const int rem = n - 8 * ci;                  // rows of this chunk (<= 0: none)
+    if (FWD && rem >= kMChunk) {
+      // rows 3..0 (sub-chain 0) and 7..4 (sub-chain 1) in increasing t
+      v4d X0 = start(ci, 0) >= 0 ? cur0 : prior, X1 = start(ci, 1) >= 0 ? cur1 : prior;
+      const int s0 = start(ci, 0) >= 0 ? norm_exp(cur0) : 0, s1 = start(ci, 1) >= 0 ? norm_exp(cur1) : 0;
+      dg.lap(&dg.x1);
+      step(X0, s0, slot, 3, E[3]);
+      step(X1, s1, slot, 7, E[7]);
 #pragma unroll
-        for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + c.codes[hiT - k] * 16);
-        // sub-chain h starts below row 4h + 3 (or below the chunk's last valid row)
-        auto init = [&](Chain<FWD>& x, int h, const v4d& cur) {
-          const int ts = start(ci, h);
-          if (ts >= 0) {
-            x.X = cur;
-            x.sc = -__builtin_amdgcn_frexp_exp(chain_sum(cur));
-          } else {
-            x.X = prior;
-            x.sc = 0;
-          }
-        };
-        init(ch, 0, cur0);
-        init(c2, 1, cur1);
-        // rows 3..0 (sub-chain 0) and 7..4 (sub-chain 1), increasing t; a
-        // full chunk branch-free so that the two chains interleave
-        if (rem >= kMChunk) {
+      for (int q = 2; q >= 0; q--) {
+        step(X0, 0, slot, q, E[q]);
+        step(X1, 0, slot, q + 4, E[q + 4]);
+      }
+    } else if (!FWD && rem > kMChunk) {
+      // start rows 4 and 8 (= the next chunk's row 0); rows 3..0 and 7..4 in decreasing t
+      v4d X0 = cur0 * E[4], X1 = cur1 * En[0];
+      const int s0 = norm_exp(X0), s1 = norm_exp(X1);
+      dg.lap(&dg.x1);
 #pragma unroll
-          for (int q = 3; q >= 0; q--) {
-            ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
-            c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
-          }
-        } else {
+      for (int q = 3; q >= 0; q--) {
+        step(X0, q == 3 ? s0 : 0, slot, q, E[q]);
+        step(X1, q == 3 ? s1 : 0, slot, q + 4, E[q + 4]);
+      }
+    } else if (rem > 0) {
+      // the phase's last chunk: short, or reaching t = T - 1 (rare; plain loops)
 #pragma unroll
-          for (int q = 3; q >= 0; q--) {
-            if (q < rem) ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
-            if (q + 4 < rem) c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
-          }
-        }
-      } else {
-        const int lo = H + 8 * ci;               // row k <-> t = lo + k
-#pragma unroll
-        for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + c.codes[lo + k] * 16);
-        // sub-chain h: start row ks_h = start - lo (4h + 4, or the row of t = T - 1)
-        auto init = [&](Chain<FWD>& x, int h, const v4d& cur) {
-          const int ks = start(ci, h) - lo;
-          if (ks < 4 * h + 4) {
-            *reinterpret_cast<double2*>(slot + ks * kStepD + c.wo0) = make_double2(cur.x, cur.y);
-            *reinterpret_cast<double2*>(slot + ks * kStepD + c.wo1) = make_double2(cur.z, cur.w);
-          }
-          x.X = cur * load4(c.Et + c.codes[lo + ks] * 16);   // e at the start step (LDS, not a register pick)
-          x.sc = -__builtin_amdgcn_frexp_exp(chain_sum(x.X));
-          return ks;
-        };
-        const int ks0 = init(ch, 0, cur0);
-        const int ks1 = rem > 4 ? init(c2, 1, cur1) : 0;
-        if (ks0 == 4 && ks1 == kMChunk) {          // branch-free: the two chains interleave
-#pragma unroll
-          for (int q = 3; q >= 0; q--) {
-            ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
-            c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
+      for (int h = 0; h < 2; h++) {
+        const int ts = start(ci, h);
+        const v4d cur = h ? cur1 : cur0;
+        if (FWD) {
+          const int hiT = H - 1 - 8 * ci;
+          if (hiT - 4 * h < 0) continue;          // no valid row
+          v4d X = ts >= 0 ? cur : prior;
+          int sc = ts >= 0 ? norm_exp(cur) : 0;
+          for (int t = ts + 1; t <= hiT - 4 * h; t++) {
+            const int k = hiT - t;
+            step(X, sc, slot, k, load4(c.Et + c.codes[t] * c.es));
+            sc = 0;
           }
         } else {
-#pragma unroll
-          for (int q = 3; q >= 0; q--) {
-            if (q < ks0) ch.step(c, slot + q * kStepD, nullptr, nullptr, e[q]);
-            if (q + 4 < ks1) c2.step(c, slot + (q + 4) * kStepD, nullptr, nullptr, e[q + 4]);
+          const int lo = H + 8 * ci + 4 * h;
+          if (lo > T - 1) continue;               // no valid row
+          const int ks = ts - (H + 8 * ci);
+          if (ts < lo + 4) row(slot, ks, cur);    // beta_{T-1} inside the chunk
+          v4d X = cur * load4(c.Et + c.codes[ts] * c.es);
+          int sc = norm_exp(X);
+          for (int t = ts - 1; t >= lo; t--) {
+            step(X, sc, slot, t - (H + 8 * ci), load4(c.Et + c.codes[t] * c.es));
+            sc = 0;
           }
         }
       }
     }
+    if (NIPAMD_WAIT_TIMES) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    dg.lap(&dg.x2);
     barrier_lds(&dg.wb);
+  };
+  for (int ci = 0; ci < nchB; ci += 2) {
+    chunk(ci, P0, P1, Ea, Eb);
+    if (ci + 1 >= nchB) break;
+    chunk(ci + 1, Q0, Q1, Eb, Ea);
   }
 }
 
@@ -185,7 +227,7 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
   auto ring_vec = [&](const double* slot, int k, double (&v)[16]) {
 #pragma unroll
     for (int p = 0; p < 8; p++) {
-      const double2 x = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(c, p));
+      const double2 x = *reinterpret_cast<const double2*>(slot + ck_off(k, c, p));
       v[2 * p] = x.x; v[2 * p + 1] = x.y;
     }
   };
@@ -217,7 +259,7 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const int jj = q * 8 + hi;
-        const double2 v = *reinterpret_cast<const double2*>(slot + k * kStepD + piece_off(jj, s));
+        const double2 v = *reinterpret_cast<const double2*>(slot + ck_off(k, jj, s));
         *reinterpret_cast<double2*>(Sblk + (long)t * kSStep + jj * 16 + 2 * s) = v;
       }
     }
@@ -258,7 +300,7 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
       const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
 #pragma unroll
       for (int p = 0; p < 8; p++)
-        *reinterpret_cast<double2*>(slot + k * kStepD + piece_off(c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
+        *reinterpret_cast<double2*>(slot + ck_off(k, c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
     }
     if (FWD) ll.renorm();
   };
@@ -270,7 +312,7 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
     double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s;
 #pragma unroll
     for (int q = 0; q < kMSeq; q++) {
-      const double2 v = *reinterpret_cast<const double2*>(slot + kB * kStepD + piece_off(q, s));
+      const double2 v = *reinterpret_cast<const double2*>(slot + ck_off(kB, q, s));
       double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
       *reinterpret_cast<double2*>(p) = v;
     }
@@ -288,15 +330,16 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   double* out = reinterpret_cast<double*>(smem);     // filter rings [2 dirs][2 slots][8][16][16]
   double* rr = out + kOutD;                          // recomputed rings [2 dirs][2 slots][8][16][16]
   double* zr = rr + kOutD;                           // [2 slots][8][16]
-  double* Et = zr + kZD;                             // [(M+2)][16]
-  uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * 16);   // [16][Tr]
+  double* Et = zr + kZD;                             // [(M+2)][kEtStride]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * kEtStride);   // [16][Tr]
+  auto nozero = [] {};
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * kMSeq;
   const int T = a.T;
   const int Tr = chain_codes_row(T);
-  stage_codes<kCThreads>(a, b0, tid, Et, codes, Tr, [] {});
+  stage_codes<kCThreads, decltype(nozero), kEtStride>(a, b0, tid, Et, codes, Tr, nozero);
   __syncthreads();
   CkDiag dg;
   dg.stamp(dg.t0);
@@ -328,11 +371,13 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   }
   WaveCtx c;
   c.Et = Et + 2 * g;
+  c.es = kEtStride;
   c.codes = codes + j * Tr + kMG;
   c.zr = zr;
   c.scr = nullptr;
-  c.wo0 = piece_off(j, g);
-  c.wo1 = piece_off(j, 4 + g);
+  c.wo0 = ck_off(0, j, g);
+  c.wo1 = ck_off(0, j, 4 + g);
+  c.wodd = ck_off(1, j, g) - kStepD - c.wo0;     // = (j & 1) ? -16 : 16, for both pieces
   double* Sw = Sblk + j * 16 + 2 * g;
   if (wave >= 6) {
     c.out = rring;
@@ -344,8 +389,8 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   }
   c.out = ring;
   c.zw = g == 0;
-  if (fwd) filter_wave<true, false, true>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
-  else filter_wave<false, false, true>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
+  if (fwd) filter_wave<true, false, true, 1>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
+  else filter_wave<false, false, true, 1>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
   dg.tb = dg.ta = dg.t0;                             // the filters: total only (slot 2)
   dg.write(a, wave, lane);
 }
@@ -353,7 +398,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
 }  // namespace
 
 size_t chain_fb_ckpt_lds_bytes(int M, int T) {
-  return (size_t)(2 * kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * 16 * sizeof(double) +
+  return (size_t)(2 * kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * kEtStride * sizeof(double) +
          (size_t)kMSeq * chain_codes_row(T);
 }
 

@@ -215,16 +215,20 @@ __device__ __forceinline__ void diag_stamp(const ChainArgs& a, int k, int lane) 
 }
 
 struct WaveCtx {
-  const double* Et;         // LDS evidence table + 2g (row stride 16)
+  const double* Et;         // LDS evidence table + 2g (row stride es)
   const uint8_t* codes;     // LDS codes of chain j, index t in [-kMG, T + kMG)
   double* out;              // this direction's LDS ring [2][kMChunk][kStepD]
   double* zr;               // forward: LDS ring of step masses z2 [2][kMChunk][16], else null
   int* scr;                 // e_step: LDS ring of applied scale exponents [2][kMChunk][16], else null
   int wo0, wo1;             // this lane's two piece offsets within a step
   bool zw;                  // this lane writes its chain's z2 (lane group 0)
+  int es = 16;              // evidence row stride (doubles)
+  int wodd = 0;             // chain-swap layouts (Chain<..., SW = 1>): offset added on odd rows
 };
 
-template <bool FWD, bool ES = false>
+// SW = 1: the chain-swap ring layout of chain_ckpt.hip (odd rows hold chain
+// j at position j ^ 1: row pointer + c.wodd for this lane)
+template <bool FWD, bool ES = false, int SW = 0>
 struct Chain {
   double Aop[4];
   v4d X;          // next mat-vec input (fwd: alpha_{t-1}; bwd: e_{t+1} o beta_{t+1})
@@ -257,7 +261,7 @@ struct Chain {
 #pragma unroll
     for (int k = 0; k < kMChunk; k++) code[k] = c.codes[t0 + dir * (base + k)];   // guards cover over-run
 #pragma unroll
-    for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + code[k] * 16);
+    for (int k = 0; k < kMChunk; k++) e[k] = load4(c.Et + code[k] * c.es);
   }
 
   template <bool SPARSE>
@@ -272,14 +276,15 @@ struct Chain {
 #pragma unroll
       for (int k = 0; k < kMChunk; k++) {
         if (!SPARSE || (k & (kRescale - 1)) == kRescale - 1)
-          step<true>(c, slot + k * kStepD, zs + k * kMSeq, ss + k * kMSeq, e[k]);
+          step<true>(c, slot + k * kStepD + ((SW && (k & 1)) ? c.wodd : 0), zs + k * kMSeq, ss + k * kMSeq, e[k]);
         else
-          step<false>(c, slot + k * kStepD, zs + k * kMSeq, ss + k * kMSeq, e[k]);
+          step<false>(c, slot + k * kStepD + ((SW && (k & 1)) ? c.wodd : 0), zs + k * kMSeq, ss + k * kMSeq, e[k]);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < kMChunk; k++)
-        if (base + k < n) step(c, slot + k * kStepD, zs + k * kMSeq, ss + k * kMSeq, e[k]);
+        if (base + k < n)
+          step(c, slot + k * kStepD + ((SW && (k & 1)) ? c.wodd : 0), zs + k * kMSeq, ss + k * kMSeq, e[k]);
     }
     barrier_lds(w);
   }
@@ -303,14 +308,14 @@ struct Chain {
   }
 };
 
-template <bool FWD, bool ES = false, bool SPARSE_B = false>
+template <bool FWD, bool ES = false, bool SPARSE_B = false, int SW = 0>
 __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c, const double* Et,
                                             double* Sw, int lane, bool active, long b,
                                             int nchA, int nchB, unsigned long long* stamps) {
   const int j = lane & 15, g = lane >> 4;
   const int sj = state_of(j & 3, j >> 2);       // actual state of D row j
   const int T = a.T, H = a.H;
-  Chain<FWD, ES> ch;
+  Chain<FWD, ES, SW> ch;
 #pragma unroll
   for (int r = 0; r < 4; r++)
     ch.Aop[r] = FWD ? a.A[state_of(g, r) * 16 + sj] : a.A[sj * 16 + state_of(g, r)];
@@ -330,7 +335,7 @@ __device__ __forceinline__ void filter_wave(const ChainArgs& a, const WaveCtx& c
       *reinterpret_cast<double2*>(q) = make_double2(beta.x, beta.y);
       *reinterpret_cast<double2*>(q + 8) = make_double2(beta.z, beta.w);
     }
-    ch.X = load4(c.Et + c.codes[T - 1] * 16) * beta;
+    ch.X = load4(c.Et + c.codes[T - 1] * c.es) * beta;
     ch.sc = -__builtin_amdgcn_frexp_exp(chain_sum(ch.X));
   }
   WaitAcc wa, wb;
@@ -450,9 +455,10 @@ struct LL {
 // observation codes into LDS (codes row Tr per chain, guard bytes = missing).
 // zero() runs while the first loads are in flight (block-specific LDS init).
 // The caller synchronises the block afterwards.
-template <int NT, typename Z>
+template <int NT, typename Z, int ESTR = 16>
 __device__ __forceinline__ void stage_codes(const ChainArgs& a, long b0, int tid, double* Et, uint8_t* codes,
                                             int Tr, Z zero) {
+  auto put_et = [&](int i) { Et[(i >> 4) * ESTR + (i & 15)] = a.Etab[i]; };   // row stride ESTR
   const int T = a.T;
   const int nseq = (int)((a.B - b0) < kMSeq ? (a.B - b0) : kMSeq);
   auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
@@ -482,7 +488,7 @@ __device__ __forceinline__ void stage_codes(const ChainArgs& a, long b0, int tid
       }
     };
     load(tid);
-    for (int i = tid; i < (a.M + 2) * 16; i += NT) Et[i] = a.Etab[i];
+    for (int i = tid; i < (a.M + 2) * 16; i += NT) put_et(i);
     const int gw = kMG / 4, tw = (Tr - kMG - T) / 4;             // guard words before / after
     for (int i = tid; i < kMSeq * (gw + tw); i += NT) {
       const int cq = i / (gw + tw), w = i - cq * (gw + tw);
@@ -496,7 +502,7 @@ __device__ __forceinline__ void stage_codes(const ChainArgs& a, long b0, int tid
       put(i0);
     }
   } else {
-    for (int i = tid; i < (a.M + 2) * 16; i += NT) Et[i] = a.Etab[i];
+    for (int i = tid; i < (a.M + 2) * 16; i += NT) put_et(i);
     for (int i = tid; i < kMSeq * Tr / 4; i += NT)
       reinterpret_cast<uint32_t*>(codes)[i] = 0x01010101u * (uint32_t)a.M;   // missing / guard
     zero();

@@ -340,7 +340,8 @@ int reduce_rows(const double* in, long n, int S, double* tA, double* tB, double*
   return nipamd::tree_reduce_launch(cur, n, S, out, st);
 }
 
-// fb kernel choice: the matrix-core kernel unless NIPAMD_FB_KERNEL=dpp
+// fb kernel choice: the matrix-core kernels (chain_fb_ckpt_kernel for 16-wide
+// posterior rows, NIPAMD_FB_KERNEL=scratch for chain_fb_mfma_kernel) unless NIPAMD_FB_KERNEL=dpp
 // (the 16-lane DPP kernel, kept for the e_step and for A/B measurements)
 bool use_mfma() {
   static const bool v = [] {
@@ -801,9 +802,9 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     HIP_OK(hipMalloc(&stamps, (size_t)nblk * 24 * sizeof(unsigned long long)));
     HIP_OK(hipMemsetAsync(stamps, 0, (size_t)nblk * 24 * sizeof(unsigned long long), (hipStream_t)stream));
     a.counts = reinterpret_cast<double*>(stamps);
-    // chain_ckpt.hip's per-wave stamps [block][8 waves][4]
-    HIP_OK(hipMalloc(&a.diag, (size_t)nblk * 32 * sizeof(unsigned long long)));
-    HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 32 * sizeof(unsigned long long), (hipStream_t)stream));
+    // chain_ckpt.hip's per-wave stamps [block][8 waves][5]
+    HIP_OK(hipMalloc(&a.diag, (size_t)nblk * 40 * sizeof(unsigned long long)));
+    HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 40 * sizeof(unsigned long long), (hipStream_t)stream));
   }
 #endif
   const int rc = kind == kNarrowMfma ? nipamd::chain_fb_mfma_launch(a, (hipStream_t)stream)
@@ -815,20 +816,20 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     HIP_OK(hipMemcpy(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     (void)hipFree(stamps);
     phase_report(h.data(), nblk);
-    std::vector<unsigned long long> w((size_t)nblk * 32);
+    std::vector<unsigned long long> w((size_t)nblk * 40);
     HIP_OK(hipMemcpy(w.data(), a.diag, w.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     (void)hipFree(a.diag);
-    double m[32] = {0};
+    double m[40] = {0};
     for (int k = 0; k < nblk; k++)
-      for (int i = 0; i < 32; i++) m[i] += (double)w[(size_t)k * 32 + i] / nblk;
+      for (int i = 0; i < 40; i++) m[i] += (double)w[(size_t)k * 40 + i] / nblk;
     if (m[2] > 0) {
       std::fprintf(stderr, "[nipamd] ckpt kernel cycles per wave (phase A / phase-barrier wait / phase B / "
-                   "phase-B barrier waits):\n");
+                   "phase-B barrier waits / mean SIMD id; block 0's SIMD ids):\n");
       static const char* names[8] = {"fwd filter", "bwd filter", "fwd partner", "bwd partner", "idle 4", "idle 5",
                                      "beta recompute", "alpha recompute"};
       for (int v = 0; v < 8; v++)
-        std::fprintf(stderr, "[nipamd]   %-16s %9.0f %9.0f %9.0f %9.0f\n", names[v], m[v * 4], m[v * 4 + 1],
-                     m[v * 4 + 2], m[v * 4 + 3]);
+        std::fprintf(stderr, "[nipamd]   %-16s %9.0f %9.0f %9.0f %9.0f %5.2f %llu\n", names[v], m[v * 5], m[v * 5 + 1],
+                     m[v * 5 + 2], m[v * 5 + 3], m[v * 5 + 4], w[v * 5 + 4]);
     }
   }
 #endif

@@ -1,8 +1,8 @@
 """The checkpoint + recompute forward-backward kernel (chain_ckpt.hip).
 
-NIPAMD_FB_KERNEL selects the 16-state fb kernel once per process, so the
-checkpoint kernel's outputs come from a worker process (tests/_fb_worker.py)
-run with NIPAMD_FB_KERNEL=ckpt, and this process keeps the scratch-round-trip
+NIPAMD_FB_KERNEL selects the 16-state fb kernel once per process: this
+process runs the default (the checkpoint kernel), a worker process
+(tests/_fb_worker.py) run with NIPAMD_FB_KERNEL=scratch the scratch-round-trip
 kernel (chain_mfma.hip).  Both are checked against the oracle (1e-12, as
 tests/test_gpu_parity.py) and against each other: the recomputed messages and
 the sparse phase-B rescaling change only the powers of two the vectors carry
@@ -31,10 +31,10 @@ DBL_MAX = np.finfo(np.float64).max
 
 
 @pytest.fixture(scope="module")
-def ckpt_results():
+def scratch_results():
     with tempfile.TemporaryDirectory() as d:
-        out = os.path.join(d, "ckpt.npz")
-        env = dict(os.environ, NIPAMD_FB_KERNEL="ckpt", NIPAMD_REPORT_KERNEL="1")
+        out = os.path.join(d, "scratch.npz")
+        env = dict(os.environ, NIPAMD_FB_KERNEL="scratch")
         r = subprocess.run([sys.executable, os.path.join(HERE, "_fb_worker.py"), out], env=env,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
@@ -43,10 +43,10 @@ def ckpt_results():
 
 
 @pytest.mark.parametrize("name", list(_fb_worker.CASES))
-def test_ckpt_bit_identical_and_oracle(name, ckpt_results):
+def test_ckpt_vs_scratch_and_oracle(name, scratch_results):
     m, obs, ov, q = _fb_worker.build_case(name)
-    post, ll, st = _fb_worker.run(m, obs, ov, q)
-    cp, cl, cs = ckpt_results[name + "/post"], ckpt_results[name + "/ll"], ckpt_results[name + "/st"]
+    cp, cl, cs = _fb_worker.run(m, obs, ov, q)      # checkpoint kernel (this process)
+    post, ll, st = scratch_results[name + "/post"], scratch_results[name + "/ll"], scratch_results[name + "/st"]
     orc = PortOracle(m.desc())
     idx = range(obs.shape[0]) if obs.shape[0] <= 32 else (0, 1, obs.shape[0] // 2, obs.shape[0] - 1)
     for b in idx:
