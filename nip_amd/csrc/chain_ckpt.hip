@@ -36,8 +36,9 @@ namespace {
 
 constexpr int kCThreads = 512;   // 8 waves, two per SIMD
 // Evidence rows 144 B apart: row r starts at bank 36r mod 64, so sixteen
-// chains reading sixteen different rows (16 B per lane) hit distinct banks
-// (a 128-B stride maps every row to bank 0 or 32: up to 4-way conflicts)
+// chains reading sixteen different rows (16 B per lane) conflict at most
+// 2-way (a 128-B stride maps every row to bank 0 or 32: 4-way;
+// profiles/r02/ck_banks.py)
 constexpr int kEtStride = 18;
 
 // Ring layout (one step = 16 chains x 16 states): chain j of row k at
