@@ -117,10 +117,19 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
     return ts < T - 1 ? ts : T - 1;
   };
   auto ld = [&](int ci, int h) { return load4(Sw + (long)start(ci < nchB ? ci : nchB - 1, h) * kSStep); };
-  auto ldE = [&](int ci, v4d (&E)[kMChunk]) {
+  // a chunk's evidence rows; backward also row 8 (the next chunk's row 0,
+  // sub-chain 1's start), so that no start waits on a load just issued
+  constexpr int kE = FWD ? kMChunk : kMChunk + 1;
+  // codes two chunks ahead, evidence rows one chunk ahead: no load waits on
+  // another load issued in the same chunk
+  auto ldC = [&](int ci, int (&C)[kE]) {
     const int cc = ci < nchB ? ci : nchB - 1;
 #pragma unroll
-    for (int k = 0; k < kMChunk; k++) E[k] = load4(c.Et + c.codes[tof(cc, k)] * c.es);
+    for (int k = 0; k < kE; k++) C[k] = c.codes[tof(cc, k)];
+  };
+  auto ldE = [&](const int (&C)[kE], v4d (&E)[kE]) {
+#pragma unroll
+    for (int k = 0; k < kE; k++) E[k] = load4(c.Et + C[k] * c.es);
   };
   auto row = [&](double* slot, int k, const v4d& v) {
     double* L = slot + k * kStepD + ((k & 1) ? c.wodd : 0);
@@ -137,24 +146,29 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
   auto norm_exp = [](const v4d& v) { return -__builtin_amdgcn_frexp_exp(chain_sum(v)); };
 
   v4d P0 = ld(0, 0), P1 = ld(0, 1), Q0 = ld(1, 0), Q1 = ld(1, 1);
-  v4d Ea[kMChunk], Eb[kMChunk];
-  ldE(0, Ea);
+  v4d Ea[kE], Eb[kE];
+  int Ca[kE], Cb[kE];
+  ldC(0, Ca);
+  ldE(Ca, Ea);
+  ldC(1, Ca);                                      // chunk 1's codes (Cb: chunk 2's, loaded in chunk 0)
   dg.rc = true;
-  auto chunk = [&](int ci, v4d& R0, v4d& R1, const v4d (&E)[kMChunk], v4d (&En)[kMChunk]) {
+  auto chunk = [&](int ci, v4d& R0, v4d& R1, const v4d (&E)[kE], v4d (&En)[kE], const int (&Cn)[kE],
+                   int (&Cnn)[kE]) {
     dg.lap(nullptr);
     double* slot = c.out + (ci & 1) * kSlotD;
     const v4d cur0 = R0, cur1 = R1;
     R0 = ld(ci + 2, 0);
     R1 = ld(ci + 2, 1);
-    ldE(ci + 1, En);
+    ldE(Cn, En);                                   // chunk ci + 1's evidence
+    ldC(ci + 2, Cnn);                              // chunk ci + 2's codes
     const int rem = n - 8 * ci;                  // rows of this chunk (<= 0: none)
     if (FWD && rem >= kMChunk) {
       // rows 3..0 (sub-chain 0) and 7..4 (sub-chain 1) in increasing t
+      // the checkpoints (and the prior) sum to ~1: no rescale at the start
       v4d X0 = start(ci, 0) >= 0 ? cur0 : prior, X1 = start(ci, 1) >= 0 ? cur1 : prior;
-      const int s0 = start(ci, 0) >= 0 ? norm_exp(cur0) : 0, s1 = start(ci, 1) >= 0 ? norm_exp(cur1) : 0;
       dg.lap(&dg.x1);
-      step(X0, s0, slot, 3, E[3]);
-      step(X1, s1, slot, 7, E[7]);
+      step(X0, 0, slot, 3, E[3]);
+      step(X1, 0, slot, 7, E[7]);
 #pragma unroll
       for (int q = 2; q >= 0; q--) {
         step(X0, 0, slot, q, E[q]);
@@ -162,13 +176,14 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
       }
     } else if (!FWD && rem > kMChunk) {
       // start rows 4 and 8 (= the next chunk's row 0); rows 3..0 and 7..4 in decreasing t
-      v4d X0 = cur0 * E[4], X1 = cur1 * En[0];
-      const int s0 = norm_exp(X0), s1 = norm_exp(X1);
+      // checkpoints sum to ~1 (beta_{T-1} = 1 to N): four evidence factors
+      // per sub-chain at most, no rescale
+      v4d X0 = cur0 * E[4], X1 = cur1 * E[kE - 1];
       dg.lap(&dg.x1);
 #pragma unroll
       for (int q = 3; q >= 0; q--) {
-        step(X0, q == 3 ? s0 : 0, slot, q, E[q]);
-        step(X1, q == 3 ? s1 : 0, slot, q + 4, E[q + 4]);
+        step(X0, 0, slot, q, E[q]);
+        step(X1, 0, slot, q + 4, E[q + 4]);
       }
     } else if (rem > 0) {
       // the phase's last chunk: short, or reaching t = T - 1 (rare; plain loops)
@@ -205,15 +220,16 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
     barrier_lds(&dg.wb);
   };
   for (int ci = 0; ci < nchB; ci += 2) {
-    chunk(ci, P0, P1, Ea, Eb);
+    chunk(ci, P0, P1, Ea, Eb, Ca, Cb);
     if (ci + 1 >= nchB) break;
-    chunk(ci + 1, Q0, Q1, Eb, Ea);
+    chunk(ci + 1, Q0, Q1, Eb, Ea, Cb, Ca);
   }
 }
 
 template <bool FWD>
-__device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, const double* rring, const double* zr,
-                                           double* Sblk, int lane, long b0, int nchA, int nchB, CkDiag& dg) {
+__device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, double* rring, const double* zr,
+                                           double* Sblk, int lane, long b0, int nchA, int nchB, CkDiag& dg,
+                                           const double* llx) {
   const int T = a.T, H = a.H;
   const int s = lane & 7, hi = lane >> 3;
   const int c = lane & 15, kq = lane >> 4;
@@ -257,11 +273,21 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
       // forward: alpha_{H-5-4m} >= 0; backward: beta_{H+4+4m} <= T-2
       const bool ck = i < nA && (FWD ? (((H - 1 - t) & 3) == 0 && t <= H - 5) : (((t - H) & 3) == 0 && t >= H + 4));
       if (!ck) continue;
+      // stored rescaled to sum ~1 (the chain's 16 states are the 8 lanes of
+      // an aligned DPP row group): a recompute chain starts from it as is
+      double2 v[2];
+      double z[2];
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const int jj = q * 8 + hi;
-        const double2 v = *reinterpret_cast<const double2*>(slot + ck_off(k, jj, s));
-        *reinterpret_cast<double2*>(Sblk + (long)t * kSStep + jj * 16 + 2 * s) = v;
+        v[q] = *reinterpret_cast<const double2*>(slot + ck_off(k, q * 8 + hi, s));
+        z[q] = v[q].x + v[q].y;
+      }
+      sum8_n(z);
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int e = -__builtin_amdgcn_frexp_exp(z[q]);
+        *reinterpret_cast<double2*>(Sblk + (long)t * kSStep + (q * 8 + hi) * 16 + 2 * s) =
+            make_double2(__builtin_ldexp(v[q].x, e), __builtin_ldexp(v[q].y, e));
       }
     }
   };
@@ -270,29 +296,31 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
     barrier_lds();
   }
   if (nchA > 0) drainA(nchA - 1);
+  // forward: phase A's ll, reduced over the chain's lanes now (ll_wave keeps
+  // phase B's); only the five per-chain totals stay live
+  double E2a = 0.0, E1a = 0.0;
+  if (FWD) {
+    ll.renorm();
+    ll.reduce(E2a, E1a);
+  }
   dg.stamp(dg.ta);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   dg.stamp(dg.tb);
 
   double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
   // chain c, slot steps kq and kq + 4: normalise(v o o) written over the ring vector
+  // chain c, slot steps kq and kq + 4: normalise(v o o) written over the
+  // recomputed vector o (the forward side's phase-B ll reads v meanwhile,
+  // ll_wave); the store pass then reads the recomputed ring
   auto drainV = [&](int ci) {
-    double* slot = out + (ci & 1) * kSlotD;
-    const double* rs = rring + (ci & 1) * kSlotD;
-    const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
+    const double* slot = out + (ci & 1) * kSlotD;
+    double* rs = rring + (ci & 1) * kSlotD;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int k = kq + 4 * h;
       double v[16], o[16];
       ring_vec(slot, k, v);
       ring_vec(rs, k, o);
-      if (FWD) {
-        // phase B rescales like phase A (full chunks every kRescale-th step,
-        // partial ones every step): z2 summed here, zf published on rescales
-        const int i = ci * kMChunk + k;
-        const bool rs = ci * kMChunk + kMChunk > nB || (k & (kRescale - 1)) == kRescale - 1;
-        ll.step(ll.dot(v), LL::sum16(v), zs[k * kMSeq + c], rs, i < nB, tB + i == T - 1);
-      }
       double pr[16];
 #pragma unroll
       for (int i = 0; i < 16; i++) pr[i] = v[i] * o[i];
@@ -301,13 +329,12 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
       const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
 #pragma unroll
       for (int p = 0; p < 8; p++)
-        *reinterpret_cast<double2*>(slot + ck_off(k, c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
+        *reinterpret_cast<double2*>(rs + ck_off(k, c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
     }
-    if (FWD) ll.renorm();
   };
   // chain q's 8 steps as one contiguous 1 KB run per store instruction
   auto store_pass = [&](int ci) {
-    const double* slot = out + (ci & 1) * kSlotD;
+    const double* slot = rring + (ci & 1) * kSlotD;
     const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
     const bool ok = kB < nk;
     double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s;
@@ -323,7 +350,60 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, cons
     drainV(ci);
     store_pass(ci);
   }
-  if (FWD) ll.write(a, b0, lane, 1u);
+  barrier_lds();                                     // the ll wave's partial products are in llx
+  if (FWD) {
+    // ll = phase A's products (here) x phase B's (ll_wave), per chain
+    const double* x = llx + c * 5;
+    ll.m2 *= x[0]; ll.m1 *= x[1]; ll.zmin = __builtin_fmin(ll.zmin, x[2]);
+    ll.finish(a, b0, lane, E2a + x[3], E1a + x[4], 1u);
+  }
+}
+
+// Wave 4 (the forward filter's SIMD, idle otherwise): the forward side's
+// phase-B log-likelihood (nip.c:1461-1474, LL above), from the filter's ring
+// vectors and published masses, as the partner does in phase A.  Its per-chain
+// partial products go to llx for the forward partner to combine.
+__device__ __forceinline__ void ll_wave(const ChainArgs& a, const double* out, const double* zr, int lane,
+                                        int nchA, int nchB, CkDiag& dg, double* llx) {
+  const int T = a.T, H = a.H;
+  const int c = lane & 15, kq = lane >> 4;
+  const int nB = T - H, tB = H;
+  for (int ci = 0; ci < nchA; ci++) barrier_lds();
+  dg.stamp(dg.ta);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  dg.stamp(dg.tb);
+  LL ll;
+#pragma unroll
+  for (int i = 0; i < 16; i++) ll.w[i] = a.ts[i];
+  ll.m2 = 1.0; ll.m1 = 1.0; ll.zmin = 1.0; ll.e2 = 0; ll.e1 = 0;
+  for (int ci = 0; ci < nchB; ci++) {
+    barrier_lds(&dg.wb);
+    const double* slot = out + (ci & 1) * kSlotD;
+    const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = kq + 4 * h;
+      double v[16];
+#pragma unroll
+      for (int p = 0; p < 8; p++) {
+        const double2 x = *reinterpret_cast<const double2*>(slot + ck_off(k, c, p));
+        v[2 * p] = x.x; v[2 * p + 1] = x.y;
+      }
+      // phase B rescales like phase A (full chunks every kRescale-th step,
+      // partial ones every step): z2 summed here, zf published on rescales
+      const int i = ci * kMChunk + k;
+      const bool rs = ci * kMChunk + kMChunk > nB || (k & (kRescale - 1)) == kRescale - 1;
+      ll.step(ll.dot(v), LL::sum16(v), zs[k * kMSeq + c], rs, i < nB, tB + i == T - 1);
+    }
+    ll.renorm();
+  }
+  double E2, E1;
+  ll.reduce(E2, E1);
+  if (lane < kMSeq) {
+    double* x = llx + lane * 5;
+    x[0] = ll.m2; x[1] = ll.m1; x[2] = ll.zmin; x[3] = E2; x[4] = E1;
+  }
+  barrier_lds();                                     // llx complete
 }
 
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
@@ -333,6 +413,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   double* zr = rr + kOutD;                           // [2 slots][8][16]
   double* Et = zr + kZD;                             // [(M+2)][kEtStride]
   uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * kEtStride);   // [16][Tr]
+  double* llx = reinterpret_cast<double*>(codes + kMSeq * chain_codes_row(a.T));   // [16 chains][5]
   auto nozero = [] {};
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -355,18 +436,25 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   double* ring = out + (fwd ? 0 : 2 * kSlotD);      // the filter's ring of this side
   // recomputed ring consumed with it: the forward side's beta (wave 6), the backward side's alpha (wave 7)
   double* rring = rr + (fwd ? 0 : 2 * kSlotD);
-  if (wave == 4 || wave == 5) {                      // idle on the filters' SIMDs: barriers only
+  // every wave ends with one more barrier: the forward ll's two halves meet in llx
+  if (wave == 4) {
+    ll_wave(a, out, zr, lane, nchA, nchB, dg, llx);
+    dg.write(a, wave, lane);
+    return;
+  }
+  if (wave == 5) {                                   // idle on the backward filter's SIMD: barriers only
     for (int ci = 0; ci < nchA; ci++) barrier_lds();
     dg.stamp(dg.ta);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     dg.stamp(dg.tb);
     for (int ci = 0; ci < nchB; ci++) barrier_lds(&dg.wb);
+    barrier_lds();
     dg.write(a, wave, lane);
     return;
   }
   if (role >= 2 && wave < 4) {
-    if (fwd) ck_partner<true>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
-    else ck_partner<false>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
+    if (fwd) ck_partner<true>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg, llx);
+    else ck_partner<false>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg, llx);
     dg.write(a, wave, lane);
     return;
   }
@@ -385,6 +473,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
     c.zw = false;
     if (fwd) recompute_wave<false>(a, c, Sw, lane, nchA, nchB, dg);   // wave 6: beta for the forward side
     else recompute_wave<true>(a, c, Sw, lane, nchA, nchB, dg);        // wave 7: alpha for the backward side
+    barrier_lds();
     dg.write(a, wave, lane);
     return;
   }
@@ -392,6 +481,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   c.zw = g == 0;
   if (fwd) filter_wave<true, false, true, 1>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
   else filter_wave<false, false, true, 1>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
+  barrier_lds();
   dg.tb = dg.ta = dg.t0;                             // the filters: total only (slot 2)
   dg.write(a, wave, lane);
 }
@@ -400,7 +490,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
 
 size_t chain_fb_ckpt_lds_bytes(int M, int T) {
   return (size_t)(2 * kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * kEtStride * sizeof(double) +
-         (size_t)kMSeq * chain_codes_row(T);
+         (size_t)kMSeq * chain_codes_row(T) + (size_t)kMSeq * 5 * sizeof(double);
 }
 
 int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream) {

@@ -415,10 +415,9 @@ struct LL {
     const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
     const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
   }
-  __device__ __forceinline__ void write(const ChainArgs& a, long b0, int lane, unsigned dead_status = 1u) {
-    renorm();
-    // combine the chain's four lanes (l, l ^ 32, l ^ 16); every operation is
-    // symmetric, so both lanes of a pair hold identical bits
+  // combine the chain's four lanes (l, l ^ 32, l ^ 16) after renorm(); every
+  // operation is symmetric, so all four lanes hold identical bits
+  __device__ __forceinline__ void reduce(double& E2, double& E1) {
     auto pair32 = [](double x, auto f) {
       const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
       const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
@@ -434,12 +433,16 @@ struct LL {
     auto mul = [](double x, double y) { return x * y; };
     auto mn = [](double x, double y) { return __builtin_fmin(x, y); };
     auto add = [](double x, double y) { return x + y; };
-    double E2 = (double)e2, E1 = (double)e1;     // small integers: exact in a double
+    E2 = (double)e2; E1 = (double)e1;             // small integers: exact in a double
     m2 = pair16(pair32(m2, mul), mul);
     m1 = pair16(pair32(m1, mul), mul);
     zmin = pair16(pair32(zmin, mn), mn);
     E2 = pair16(pair32(E2, add), add);
     E1 = pair16(pair32(E1, add), add);
+  }
+  // lanes 0..15 (chain = lane) write the sequence's ll and status
+  __device__ __forceinline__ void finish(const ChainArgs& a, long b0, int lane, double E2, double E1,
+                                         unsigned dead_status) const {
     if (lane >= kMSeq) return;
     const long b = b0 + lane;
     if (b >= a.B) return;
@@ -448,6 +451,12 @@ struct LL {
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
     if (a.status) a.status[b] = dead ? dead_status : 0u;
+  }
+  __device__ __forceinline__ void write(const ChainArgs& a, long b0, int lane, unsigned dead_status = 1u) {
+    renorm();
+    double E2, E1;
+    reduce(E2, E1);
+    finish(a, b0, lane, E2, E1, dead_status);
   }
 };
 
