@@ -129,15 +129,21 @@ __device__ __forceinline__ double div_by(double x, double c) {
   return x * r;
 }
 
-constexpr int kChunk = 8;   // steps per unrolled chunk; prefetch distance = 1 chunk
+#ifndef NIPAMD_ESTEP_CHUNK
+#define NIPAMD_ESTEP_CHUNK 8
+#endif
+#ifndef NIPAMD_ESTEP_WAVES
+#define NIPAMD_ESTEP_WAVES 2        // e_step: waves per SIMD the register budget is sized for
+#endif
 
 // Per-chunk prefetch registers: evidence values from LDS and (phase B) the
 // other direction's interface vector from HBM, issued one chunk ahead so no
-// step waits on a fresh load.
+// step waits on a fresh load.  KC steps per unrolled chunk.
+template <int KC>
 struct Prefetch {
-  double e[kChunk];
-  double s[kChunk];
-  int c[kChunk];       // observation codes (E-step: M1 count row)
+  double e[KC];
+  double s[KC];
+  int c[KC];           // observation codes (E-step: M1 count row)
 };
 
 }  // namespace
@@ -167,36 +173,37 @@ struct ChainCtx {
 // Prefetch kChunk steps of this row starting at t0 in direction dir.  The
 // guard steps make every index in [-kGuard, T + kGuard) readable, so the tail
 // of a phase needs no clamping (its values are never used).
-__device__ __forceinline__ void load_chunk(const ChainCtx& c, Prefetch& p, int t0, int dir,
+template <int KC>
+__device__ __forceinline__ void load_chunk(const ChainCtx& c, Prefetch<KC>& p, int t0, int dir,
                                            bool with_s) {
-  int code[kChunk];
+  int code[KC];
 #pragma unroll
-  for (int j = 0; j < kChunk; j++) {
+  for (int j = 0; j < KC; j++) {
     const int t = t0 + dir * j;
     code[j] = c.codes[t];
     if (with_s) p.s[j] = c.Sload[(long)t * 16];
   }
 #pragma unroll
-  for (int j = 0; j < kChunk; j++) { p.e[j] = c.Et[code[j] * 16]; p.c[j] = code[j]; }
+  for (int j = 0; j < KC; j++) { p.e[j] = c.Et[code[j] * 16]; p.c[j] = code[j]; }
 }
 
 // n wave-uniform steps with one-chunk-ahead ping-pong prefetch.
-template <typename Step>
+template <int KC, typename Step>
 __device__ __forceinline__ void run_phase(const ChainCtx& c, int n, int t0, int dir,
                                           bool with_s, Step&& step) {
-  Prefetch pa, pb;
+  Prefetch<KC> pa, pb;
   if (n <= 0) return;
   load_chunk(c, pa, t0, dir, with_s);
-  for (int base = 0; base < n; base += 2 * kChunk) {
-    load_chunk(c, pb, t0 + dir * (base + kChunk), dir, with_s);
+  for (int base = 0; base < n; base += 2 * KC) {
+    load_chunk(c, pb, t0 + dir * (base + KC), dir, with_s);
 #pragma unroll
-    for (int j = 0; j < kChunk; j++)
+    for (int j = 0; j < KC; j++)
       if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], pa.c[j], j);
-    if (base + kChunk >= n) break;
-    load_chunk(c, pa, t0 + dir * (base + 2 * kChunk), dir, with_s);
+    if (base + KC >= n) break;
+    load_chunk(c, pa, t0 + dir * (base + 2 * KC), dir, with_s);
 #pragma unroll
-    for (int j = 0; j < kChunk; j++)
-      if (base + kChunk + j < n) step(t0 + dir * (base + kChunk + j), pb.e[j], pb.s[j], pb.c[j], j);
+    for (int j = 0; j < KC; j++)
+      if (base + KC + j < n) step(t0 + dir * (base + KC + j), pb.e[j], pb.s[j], pb.c[j], j);
   }
 }
 
@@ -206,8 +213,10 @@ __device__ __forceinline__ void run_phase(const ChainCtx& c, int n, int t0, int 
 // ESTEP = true:  e_step (nip.c:1708-2007): the same two filters; phase B
 // accumulates the expected counts of every family (see chain_estep_slab).
 template <bool ESTEP>
-__global__ __launch_bounds__(kThreads, 2)
+__global__ __launch_bounds__(kThreads, ESTEP ? NIPAMD_ESTEP_WAVES : 2)
 void chain_kernel(ChainArgs a) {
+  constexpr int KC = ESTEP ? NIPAMD_ESTEP_CHUNK : 8;   // steps per unrolled chunk
+  static_assert(KC % 4 == 0, "the ll products renormalise every 4th step of a chunk");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* Et = reinterpret_cast<double*>(smem);                       // [(M+2)][16]
   uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);    // [8][Tr]
@@ -364,7 +373,7 @@ void chain_kernel(ChainArgs a) {
   {
     const int nf = H, nb = T - 1 - H, n = nf < nb ? nf : nb;
     const int t0 = fwd ? 0 : T - 2;
-    run_phase(cx, n, t0, dir, false, [&](int t, double e, double o, int c, int j) { step(t, e, o, c, false, j); });
+    run_phase<KC>(cx, n, t0, dir, false, [&](int t, double e, double o, int c, int j) { step(t, e, o, c, false, j); });
     if (nf != nb && (fwd ? nf : nb) > n) {             // peeled tail: rows with one more step
       const int t = t0 + dir * n;
       step(t, cx.Et[cx.codes[t] * 16], 0.0, cx.codes[t], false, 3);
@@ -376,7 +385,7 @@ void chain_kernel(ChainArgs a) {
   {
     const int nf = T - H, nb = H, n = nf < nb ? nf : nb;
     const int t0 = fwd ? H : H - 1;
-    run_phase(cx, n, t0, dir, true, [&](int t, double e, double o, int c, int j) { step(t, e, o, c, true, j); });
+    run_phase<KC>(cx, n, t0, dir, true, [&](int t, double e, double o, int c, int j) { step(t, e, o, c, true, j); });
     if (nf != nb && (fwd ? nf : nb) > n) {
       const int t = t0 + dir * n;
       step(t, cx.Et[cx.codes[t] * 16], cx.Sload[(long)t * 16], cx.codes[t], true, 3);
