@@ -9,12 +9,14 @@
 // on the partner SIMDs, one chunk at a time, in step with the filter that
 // consumes them:
 //
-//   SIMD 0: wave 0 forward filter (alpha, rings, z2)        wave 4 idle
-//   SIMD 1: wave 1 backward filter (beta)                    wave 5 idle
-//   SIMD 2: wave 2 forward partner (ll; phase A alpha         wave 6 recomputes
-//           checkpoints; phase B posterior of t >= H)                beta of t >= H
-//   SIMD 3: wave 3 backward partner (phase A beta             wave 7 recomputes
-//           checkpoints; phase B posterior of t < H)                 alpha of t < H
+//   SIMD 0: wave 0 forward filter (alpha, rings, z2)        wave 4 backward posteriors,
+//                                                                    chains 8-15
+//   SIMD 1: wave 1 backward filter (beta)                    wave 5 forward posteriors,
+//                                                                    chains 8-15
+//   SIMD 2: wave 2 forward partner (ll; alpha checkpoints    wave 6 recomputes
+//           in phase A; posteriors t >= H, chains 0-7)               beta of t >= H
+//   SIMD 3: wave 3 backward partner (beta checkpoints         wave 7 recomputes
+//           in phase A; posteriors t < H, chains 0-7)                alpha of t < H
 //
 // (a workgroup's waves go to the CU's SIMDs round robin: wave w on SIMD w % 4).
 // The filters keep their SIMD's double-precision pipe to themselves; the
@@ -226,10 +228,58 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
   }
 }
 
+// Phase B, one side's chunk ci, chains 8 part .. 8 part + 7 (the side's
+// partner takes part 0, a wave on a filter SIMD part 1): normalise(v o o)
+// with v from the filter's ring slot and o from the recomputed ring slot
+// (lane L: chain 8 part + (L & 7), slot step L >> 3), written over o; then
+// each chain's 8 steps leave as one contiguous 1 KB run per store
+// instruction (lane L: step L >> 3 in address order, piece L & 7).
+template <bool FWD>
+__device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fslot, double* rslot, int part,
+                                           int lane, long b0, int ci, double* sink) {
+  const int T = a.T, H = a.H;
+  const int nB = FWD ? T - H : H, tB = FWD ? H : H - 1;
+  {
+    const int c = 8 * part + (lane & 7), k = lane >> 3;
+    double v[16], o[16];
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+      const double2 x = *reinterpret_cast<const double2*>(fslot + ck_off(k, c, p));
+      v[2 * p] = x.x; v[2 * p + 1] = x.y;
+      const double2 y = *reinterpret_cast<const double2*>(rslot + ck_off(k, c, p));
+      o[2 * p] = y.x; o[2 * p + 1] = y.y;
+    }
+    double pr[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) pr[i] = v[i] * o[i];
+    double z0 = pr[0] + pr[1], z1 = pr[2] + pr[3], z2 = pr[4] + pr[5], z3 = pr[6] + pr[7];
+    z0 += pr[8] + pr[9]; z1 += pr[10] + pr[11]; z2 += pr[12] + pr[13]; z3 += pr[14] + pr[15];
+    const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
+#pragma unroll
+    for (int p = 0; p < 8; p++)
+      *reinterpret_cast<double2*>(rslot + ck_off(k, c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
+  }
+  const int s = lane & 7, hi = lane >> 3;
+  const int kB = FWD ? hi : kMChunk - 1 - hi;
+  const int tlow = FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1);
+  const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
+  const bool ok = kB < nk;
+  double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow + hi) * 16 + a.post_off + 2 * s;
+#ifndef NIPAMD_CKPT_NO_STORES
+#define NIPAMD_CKPT_NO_STORES 0    // timing-only builds: posteriors not written (wrong results)
+#endif
+#pragma unroll
+  for (int q = 8 * part; q < 8 * part + 8; q++) {
+    const double2 v = *reinterpret_cast<const double2*>(rslot + ck_off(kB, q, s));
+    double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
+    if (NIPAMD_CKPT_NO_STORES && v.x != 12345.0) continue;
+    *reinterpret_cast<double2*>(p) = v;
+  }
+}
+
 template <bool FWD>
 __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, double* rring, const double* zr,
-                                           double* Sblk, int lane, long b0, int nchA, int nchB, CkDiag& dg,
-                                           const double* llx) {
+                                           double* Sblk, int lane, long b0, int nchA, int nchB, CkDiag& dg) {
   const int T = a.T, H = a.H;
   const int s = lane & 7, hi = lane >> 3;
   const int c = lane & 15, kq = lane >> 4;
@@ -296,114 +346,35 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
     barrier_lds();
   }
   if (nchA > 0) drainA(nchA - 1);
-  // forward: phase A's ll, reduced over the chain's lanes now (ll_wave keeps
-  // phase B's); only the five per-chain totals stay live
-  double E2a = 0.0, E1a = 0.0;
-  if (FWD) {
-    ll.renorm();
-    ll.reduce(E2a, E1a);
-  }
   dg.stamp(dg.ta);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   dg.stamp(dg.tb);
 
   double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * s;
-  // chain c, slot steps kq and kq + 4: normalise(v o o) written over the ring vector
-  // chain c, slot steps kq and kq + 4: normalise(v o o) written over the
-  // recomputed vector o (the forward side's phase-B ll reads v meanwhile,
-  // ll_wave); the store pass then reads the recomputed ring
-  auto drainV = [&](int ci) {
-    const double* slot = out + (ci & 1) * kSlotD;
-    double* rs = rring + (ci & 1) * kSlotD;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int k = kq + 4 * h;
-      double v[16], o[16];
-      ring_vec(slot, k, v);
-      ring_vec(rs, k, o);
-      double pr[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) pr[i] = v[i] * o[i];
-      double z0 = pr[0] + pr[1], z1 = pr[2] + pr[3], z2 = pr[4] + pr[5], z3 = pr[6] + pr[7];
-      z0 += pr[8] + pr[9]; z1 += pr[10] + pr[11]; z2 += pr[12] + pr[13]; z3 += pr[14] + pr[15];
-      const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
-#pragma unroll
-      for (int p = 0; p < 8; p++)
-        *reinterpret_cast<double2*>(rs + ck_off(k, c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
-    }
-  };
-  // chain q's 8 steps as one contiguous 1 KB run per store instruction
-  auto store_pass = [&](int ci) {
-    const double* slot = rring + (ci & 1) * kSlotD;
-    const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
-    const bool ok = kB < nk;
-    double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow(ci) + hi) * 16 + a.post_off + 2 * s;
-#pragma unroll
-    for (int q = 0; q < kMSeq; q++) {
-      const double2 v = *reinterpret_cast<const double2*>(slot + ck_off(kB, q, s));
-      double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
-      *reinterpret_cast<double2*>(p) = v;
-    }
-  };
+  // phase B: the forward ll from the filter's ring (phase B rescales like
+  // phase A: z2 summed here, zf published on rescales); posteriors of chains
+  // 0-7 of each chunk here, 8-15 on a filter SIMD's spare wave (wave 5
+  // forward, wave 4 backward)
   for (int ci = 0; ci < nchB; ci++) {
     barrier_lds(&dg.wb);
-    drainV(ci);
-    store_pass(ci);
-  }
-  barrier_lds();                                     // the ll wave's partial products are in llx
-  if (FWD) {
-    // ll = phase A's products (here) x phase B's (ll_wave), per chain
-    const double* x = llx + c * 5;
-    ll.m2 *= x[0]; ll.m1 *= x[1]; ll.zmin = __builtin_fmin(ll.zmin, x[2]);
-    ll.finish(a, b0, lane, E2a + x[3], E1a + x[4], 1u);
-  }
-}
-
-// Wave 4 (the forward filter's SIMD, idle otherwise): the forward side's
-// phase-B log-likelihood (nip.c:1461-1474, LL above), from the filter's ring
-// vectors and published masses, as the partner does in phase A.  Its per-chain
-// partial products go to llx for the forward partner to combine.
-__device__ __forceinline__ void ll_wave(const ChainArgs& a, const double* out, const double* zr, int lane,
-                                        int nchA, int nchB, CkDiag& dg, double* llx) {
-  const int T = a.T, H = a.H;
-  const int c = lane & 15, kq = lane >> 4;
-  const int nB = T - H, tB = H;
-  for (int ci = 0; ci < nchA; ci++) barrier_lds();
-  dg.stamp(dg.ta);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
-  dg.stamp(dg.tb);
-  LL ll;
+    if (FWD) {
+      const double* slot = out + (ci & 1) * kSlotD;
+      const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
 #pragma unroll
-  for (int i = 0; i < 16; i++) ll.w[i] = a.ts[i];
-  ll.m2 = 1.0; ll.m1 = 1.0; ll.zmin = 1.0; ll.e2 = 0; ll.e1 = 0;
-  for (int ci = 0; ci < nchB; ci++) {
-    barrier_lds(&dg.wb);
-    const double* slot = out + (ci & 1) * kSlotD;
-    const double* zs = zr + (ci & 1) * kMChunk * kMSeq;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int k = kq + 4 * h;
-      double v[16];
-#pragma unroll
-      for (int p = 0; p < 8; p++) {
-        const double2 x = *reinterpret_cast<const double2*>(slot + ck_off(k, c, p));
-        v[2 * p] = x.x; v[2 * p + 1] = x.y;
+      for (int h = 0; h < 2; h++) {
+        const int k = kq + 4 * h;
+        double v[16];
+        ring_vec(slot, k, v);
+        const int i = ci * kMChunk + k;
+        const bool rs = ci * kMChunk + kMChunk > nB || (k & (kRescale - 1)) == kRescale - 1;
+        ll.step(ll.dot(v), LL::sum16(v), zs[k * kMSeq + c], rs, i < nB, tB + i == T - 1);
       }
-      // phase B rescales like phase A (full chunks every kRescale-th step,
-      // partial ones every step): z2 summed here, zf published on rescales
-      const int i = ci * kMChunk + k;
-      const bool rs = ci * kMChunk + kMChunk > nB || (k & (kRescale - 1)) == kRescale - 1;
-      ll.step(ll.dot(v), LL::sum16(v), zs[k * kMSeq + c], rs, i < nB, tB + i == T - 1);
+      ll.renorm();
     }
-    ll.renorm();
+    norm_store<FWD>(a, out + (ci & 1) * kSlotD, rring + (ci & 1) * kSlotD, 0, lane, b0, ci, sink);
   }
-  double E2, E1;
-  ll.reduce(E2, E1);
-  if (lane < kMSeq) {
-    double* x = llx + lane * 5;
-    x[0] = ll.m2; x[1] = ll.m1; x[2] = ll.zmin; x[3] = E2; x[4] = E1;
-  }
-  barrier_lds();                                     // llx complete
+  if (FWD) ll.write(a, b0, lane, 1u);
+  barrier_lds();                                     // the block's closing barrier
 }
 
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
@@ -413,7 +384,6 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   double* zr = rr + kOutD;                           // [2 slots][8][16]
   double* Et = zr + kZD;                             // [(M+2)][kEtStride]
   uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * kEtStride);   // [16][Tr]
-  double* llx = reinterpret_cast<double*>(codes + kMSeq * chain_codes_row(a.T));   // [16 chains][5]
   auto nozero = [] {};
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -436,25 +406,28 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   double* ring = out + (fwd ? 0 : 2 * kSlotD);      // the filter's ring of this side
   // recomputed ring consumed with it: the forward side's beta (wave 6), the backward side's alpha (wave 7)
   double* rring = rr + (fwd ? 0 : 2 * kSlotD);
-  // every wave ends with one more barrier: the forward ll's two halves meet in llx
-  if (wave == 4) {
-    ll_wave(a, out, zr, lane, nchA, nchB, dg, llx);
-    dg.write(a, wave, lane);
-    return;
-  }
-  if (wave == 5) {                                   // idle on the backward filter's SIMD: barriers only
+  // waves 4 and 5 (the filters' SIMDs): chains 8-15 of the other side's
+  // posteriors -- wave 4 the backward side's, wave 5 the forward side's
+  double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * (lane & 7);
+  if (wave == 4 || wave == 5) {
+    const bool f = wave == 5;
     for (int ci = 0; ci < nchA; ci++) barrier_lds();
     dg.stamp(dg.ta);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     dg.stamp(dg.tb);
-    for (int ci = 0; ci < nchB; ci++) barrier_lds(&dg.wb);
+    const int side = f ? 0 : 2 * kSlotD;
+    for (int ci = 0; ci < nchB; ci++) {
+      barrier_lds(&dg.wb);
+      if (f) norm_store<true>(a, out + side + (ci & 1) * kSlotD, rr + side + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
+      else norm_store<false>(a, out + side + (ci & 1) * kSlotD, rr + side + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
+    }
     barrier_lds();
     dg.write(a, wave, lane);
     return;
   }
   if (role >= 2 && wave < 4) {
-    if (fwd) ck_partner<true>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg, llx);
-    else ck_partner<false>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg, llx);
+    if (fwd) ck_partner<true>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
+    else ck_partner<false>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
     dg.write(a, wave, lane);
     return;
   }
@@ -490,7 +463,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
 
 size_t chain_fb_ckpt_lds_bytes(int M, int T) {
   return (size_t)(2 * kOutD + kZD) * sizeof(double) + (size_t)(M + 2) * kEtStride * sizeof(double) +
-         (size_t)kMSeq * chain_codes_row(T) + (size_t)kMSeq * 5 * sizeof(double);
+         (size_t)kMSeq * chain_codes_row(T);
 }
 
 int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream) {
