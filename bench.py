@@ -295,7 +295,8 @@ def main():
     if not narrow and N <= 32 and os.environ.get("NIPAMD_FB_KERNEL") != "wide":
         kname = "chain_mfma_wide_kernel<%d>" % (1 if N <= 16 else 2)
     elif not narrow:
-        kname = "chain_wide_kernel<%d>" % (16 if N <= 16 else 32 if N <= 32 else 64)
+        kname = ("chain_wide4_kernel" if N > 32 and os.environ.get("NIPAMD_WIDE_KERNEL") != "wave1"
+                 else "chain_wide_kernel<%d>" % (16 if N <= 16 else 32 if N <= 32 else 64))
     elif os.environ.get("NIPAMD_FB_KERNEL") == "scratch":
         kname = "chain_fb_mfma_kernel"
     elif os.environ.get("NIPAMD_FB_KERNEL") != "dpp":
