@@ -108,6 +108,7 @@ __device__ __forceinline__ void estep_phase_b(const ChainArgs& a, double* out, c
   const int nact = (int)(a.B - b0 < kMSeq ? a.B - b0 : kMSeq);    // sequences present in this block
   const v4d zero4 = {0.0, 0.0, 0.0, 0.0};
   v4d dx0 = zero4, dx1 = zero4;
+  v4d hc0 = zero4, hc1 = zero4;                          // M1 count accumulators (D rows = codes)
   double miss = 0.0, p0 = 0.0;
   const uint8_t* cdl = es.codes + c * es.Tr + kMG;       // in-lane pass: chain c's codes
   const int last = nchB > 0 ? nchB - 1 : 0;
@@ -219,7 +220,12 @@ __device__ __forceinline__ void estep_phase_b(const ChainArgs& a, double* out, c
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     tick(3);
-    // 4. M1 counts, missing, P0
+    // 4. M1 counts on the matrix cores: H[m][y] += sum over (chain, step) of
+    //    [code == m] q(y), one v_mfma_f64_16x16x4 per chain and 4-step half
+    //    (K = the half's four steps; A = the one-hot code rows, lane (m = L &
+    //    15, step kq); B = the posteriors, lane (step kq, state y)); a fixed
+    //    accumulation order, no atomics.  Missing observations summed apart
+    //    (row M, split by finalize); P0 = posterior at t = -1 (backward).
 #pragma unroll 4
     for (int cc = 0; cc < kMSeq; cc++) {
       const uint8_t* cd = es.codes + cc * es.Tr + kMG;
@@ -230,13 +236,11 @@ __device__ __forceinline__ void estep_phase_b(const ChainArgs& a, double* out, c
         const int t = FWD ? tB + i : tB - i;
         const double qv = obb[cc * kOBRow + (FWD ? k : kMChunk - 1 - k) * 16 + y];
         const int code = cd[t];
-        const bool obs = t >= 0 && code < M;
         miss += (t >= 0 && code == M) ? qv : 0.0;
         if (!FWD) p0 += t == -1 ? qv : 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-          if (kq == r && obs)
-            __hip_atomic_fetch_add(es.H + code * 16 + y, qv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const double oh = (t >= 0 && code == y && code < M) ? 1.0 : 0.0;
+        if (h == 0) hc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(oh, qv, hc0, 0, 0, 0);
+        else hc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(oh, qv, hc1, 0, 0, 0);
       }
     }
     tick(4);
@@ -254,7 +258,12 @@ __device__ __forceinline__ void estep_phase_b(const ChainArgs& a, double* out, c
     const int x = (lane >> 4) + 4 * r;                   // D row: the previous state
     slab[(FWD ? kSlabKf : kSlabKb) + x * 16 + y] = dx[r];
   }
-  for (int p = lane; p < M * 16; p += 64) slab[hoff + p] = es.H[p];
+  const v4d hc = hc0 + hc1;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int m = (lane >> 4) + 4 * r;                   // D row: the observation code
+    if (m < M) slab[hoff + m * 16 + y] = hc[r];
+  }
   miss = sum_lanes16(sum_lanes32(miss));                  // the four steps kq of state y
   if (!FWD) p0 = sum_lanes16(sum_lanes32(p0));
   if (lane < 16) {
