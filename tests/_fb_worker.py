@@ -40,6 +40,11 @@ CASES = {
     "peaked": (12, 19, 77, "peaked"),
     "config2_slice": (13, 512, 1024, "plain"),
 }
+# every T around the chunk (8) and checkpoint (4) boundaries, odd batch sizes,
+# and lengths across the LDS budget of the checkpoint kernel (it falls back to
+# the scratch kernel beyond it)
+for _T in list(range(4, 41)) + [63, 64, 65, 127, 129, 255, 257, 511, 513, 1023, 1025, 1500, 1601]:
+    CASES["sweep_T%d" % _T] = (100 + _T, 17 if _T < 100 else 9, _T, "missing" if _T % 3 == 0 else "plain")
 
 
 def build_case(name):

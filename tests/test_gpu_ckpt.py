@@ -49,6 +49,8 @@ def test_ckpt_vs_scratch_and_oracle(name, scratch_results):
     post, ll, st = scratch_results[name + "/post"], scratch_results[name + "/ll"], scratch_results[name + "/st"]
     orc = PortOracle(m.desc())
     idx = range(obs.shape[0]) if obs.shape[0] <= 32 else (0, 1, obs.shape[0] // 2, obs.shape[0] - 1)
+    if obs.shape[1] > 300:                     # long sweeps: the scratch kernel is the reference, oracle spot check
+        idx = (0, obs.shape[0] - 1)
     for b in idx:
         rp, rl = orc.fb(obs[b], ov, q)
         assert np.abs(cp[b] - rp).max() <= 1e-12
