@@ -161,8 +161,12 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
     const v4d cur0 = R0, cur1 = R1;
     R0 = ld(ci + 2, 0);
     R1 = ld(ci + 2, 1);
-    ldE(Cn, En);                                   // chunk ci + 1's evidence
-    ldC(ci + 2, Cnn);                              // chunk ci + 2's codes
+    // chunk ci + 1's evidence and chunk ci + 2's codes, issued after the
+    // first step pair so that no step waits behind them
+    auto issue = [&] {
+      ldE(Cn, En);
+      ldC(ci + 2, Cnn);
+    };
     const int rem = n - 8 * ci;                  // rows of this chunk (<= 0: none)
     if (FWD && rem >= kMChunk) {
       // rows 3..0 (sub-chain 0) and 7..4 (sub-chain 1) in increasing t
@@ -171,6 +175,7 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
       dg.lap(&dg.x1);
       step(X0, 0, slot, 3, E[3]);
       step(X1, 0, slot, 7, E[7]);
+      issue();
 #pragma unroll
       for (int q = 2; q >= 0; q--) {
         step(X0, 0, slot, q, E[q]);
@@ -182,12 +187,16 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
       // per sub-chain at most, no rescale
       v4d X0 = cur0 * E[4], X1 = cur1 * E[kE - 1];
       dg.lap(&dg.x1);
+      step(X0, 0, slot, 3, E[3]);
+      step(X1, 0, slot, 7, E[7]);
+      issue();
 #pragma unroll
-      for (int q = 3; q >= 0; q--) {
+      for (int q = 2; q >= 0; q--) {
         step(X0, 0, slot, q, E[q]);
         step(X1, 0, slot, q + 4, E[q + 4]);
       }
     } else if (rem > 0) {
+      issue();
       // the phase's last chunk: short, or reaching t = T - 1 (rare; plain loops)
 #pragma unroll
       for (int h = 0; h < 2; h++) {
@@ -216,6 +225,8 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
           }
         }
       }
+    } else {
+      issue();
     }
     if (NIPAMD_WAIT_TIMES) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     dg.lap(&dg.x2);
