@@ -326,7 +326,10 @@ int ensure_work(nipamd_model* mm, size_t bytes) {
 // Sequences per E-step launch: bounds the slab + scratch memory.  A power of
 // two times 64^k, so chunk trees are subtrees of the one binary tree over the
 // batch (see tree64_kernel).
-constexpr long kEstepChunk = 16384;
+#ifndef NIPAMD_ESTEP_SEQS
+#define NIPAMD_ESTEP_SEQS 16384
+#endif
+constexpr long kEstepChunk = NIPAMD_ESTEP_SEQS;
 
 // rows [n][S] -> out [S] by repeated radix-64 tree levels (ping-pong tA/tB)
 int reduce_rows(const double* in, long n, int S, double* tA, double* tB, double* out, hipStream_t st) {
