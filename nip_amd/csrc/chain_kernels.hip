@@ -112,6 +112,34 @@ __device__ __forceinline__ double row_sum(double x) {
   return x;
 }
 
+#ifndef NIPAMD_ESTEP_SWZ
+#define NIPAMD_ESTEP_SWZ 0          // e_step: off-critical-path sums on ds_swizzle (A/B build)
+#endif
+
+// The same sum with the lane exchanges done by ds_swizzle (xor 8, 4, 2, 1
+// inside the 32-lane swizzle group) on the LDS pipe instead of VALU DPP
+// moves: 4 VALU instructions instead of 12, at LDS latency.  Lane i adds
+// lane i ^ k where row_sum adds lane (i + k) mod 16; the partial sums are
+// periodic at every level, so both pair the same values and the bits are
+// identical.  Used for sums off the recursion's critical path.
+template <int K>
+__device__ __forceinline__ double swz_xor(double v) {
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x1F | (K << 10));
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x1F | (K << 10));
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double row_sum_swz(double x) {
+#if NIPAMD_ESTEP_SWZ
+  x += swz_xor<8>(x);
+  x += swz_xor<4>(x);
+  x += swz_xor<2>(x);
+  x += swz_xor<1>(x);
+  return x;
+#else
+  return row_sum(x);
+#endif
+}
 
 // exponent e such that x = m * 2^e, m in [0.5, 1); 0 for x == 0
 __device__ __forceinline__ int exp2_of(double x) {
@@ -327,7 +355,7 @@ void chain_kernel(ChainArgs a) {
 #ifdef NIPAMD_ABLATE_NO_LL
     const double z1 = 0.0;
 #else
-    const double z1 = row_sum(u * s_y);              // fwd: m1
+    const double z1 = ESTEP ? row_sum_swz(u * s_y) : row_sum(u * s_y);   // fwd: m1
 #endif
 #ifdef NIPAMD_ABLATE_NO_STORE     // timing-only ablation build (wrong results)
     if (0) {
@@ -349,7 +377,7 @@ void chain_kernel(ChainArgs a) {
       //   P1:  xi_t(x,y) = alpha_{t-1}(x) A(x,y) e_t(y) beta_t(y) / c_t   (fwd, t >= H)
       //        xi_{t+1}(x,y) = alpha_t(x) A(x,y) g_{t+1}(y) / c_t        (bwd, t+1 < H)
       const double pr = keep * other;
-      const double c = row_sum(pr);
+      const double c = row_sum_swz(pr);
       const double q = div_by(pr, c);
       Hrow[code * 16] += q;
       const double rc = c != 0.0 ? __builtin_ldexp(div_by(1.0, c), sc) : 0.0;
