@@ -131,6 +131,10 @@ __device__ __forceinline__ double swz_xor(double v) {
 
 __device__ __forceinline__ double row_sum_swz(double x) {
 #if NIPAMD_ESTEP_SWZ
+  // x is often a fresh product: keep the compiler from contracting it into
+  // the first add (an fma would round differently from row_sum of the same
+  // product, and e_step's missing steps rely on z2 == z1 to the bit)
+  asm volatile("" : "+v"(x));
   x += swz_xor<8>(x);
   x += swz_xor<4>(x);
   x += swz_xor<2>(x);
@@ -349,7 +353,12 @@ void chain_kernel(ChainArgs a) {
   // scaled; p = e o u.  fwd: alpha_t = p;  bwd: beta_t = u, next input p.
   auto step = [&](int t, double e, double other, int code, bool combine, int j) {
     const double u = __builtin_ldexp(dot_bcast(x, C), sc);
+#if NIPAMD_ESTEP_SWZ
+    double p = u * e;
+    if (ESTEP) asm volatile("" : "+v"(p));           // the same rounded product as z1's (see row_sum_swz)
+#else
     const double p = u * e;
+#endif
     const double keep = fwd ? p : u;                 // interface vector at time t
     const double z2 = row_sum(p);                    // fwd: m2 ; bwd: scale
 #ifdef NIPAMD_ABLATE_NO_LL

@@ -90,16 +90,7 @@ struct JtPlanDev {
   int pi_off, w_off;      // dp: prior of the previous interface (t = 0), m1 weights
   int ws_alpha, ws_beta, ws_out, ws_slab;   // workspace slots (ws_slab: e_step counts)
   int slab;               // e_step slab size (param_size), 0 otherwise
-  int nip, ndp;           // pool sizes (ints, doubles)
-  int stage;              // 1: the kernels copy both pools into LDS first (jt_pool_lds_bytes)
 };
-
-// LDS bytes of a staged plan: the double pool, then the int pool
-inline size_t jt_pool_lds_bytes(const JtPlanDev& p) {
-  return ((size_t)p.ndp * sizeof(double) + (size_t)p.nip * sizeof(int) + 15) & ~(size_t)15;
-}
-// LDS budget of one single-wave block (workspace + staged pools)
-constexpr size_t kJtLdsBudget = 64 * 1024;
 
 struct JtRun {
   JtPlanDev p;

@@ -130,25 +130,6 @@ __device__ __forceinline__ double* unit_ws(const JtRun& r, double* lds, int u, i
   return r.wsg + ((long)blockIdx.x * U + u) * r.p.ws;
 }
 
-// The plan as the kernel reads it: both pools copied into LDS after the
-// workspace when the host marked them stageable (JtPlanDev::stage), else the
-// HBM pools.  Every table lookup of a step (index maps, pre-images, base
-// tables, the visit lists) is then an LDS round trip.
-template <bool LDS>
-__device__ JtPlanDev stage_plan(const JtRun& r, double* lds, int U) {
-  JtPlanDev P = r.p;
-  if (P.stage) {
-    double* d = lds + (LDS ? (long)U * P.ws : 0);
-    int* ip = reinterpret_cast<int*>(d + P.ndp);
-    for (int i = threadIdx.x; i < P.ndp; i += blockDim.x) d[i] = P.dp[i];
-    for (int i = threadIdx.x; i < P.nip; i += blockDim.x) ip[i] = P.ip[i];
-    __syncthreads();
-    P.dp = d;
-    P.ip = ip;
-  }
-  return P;
-}
-
 // any evidence entered at this step (a step without any contributes exactly 0
 // to ll; DESIGN.md 6, the missing-value note)
 __device__ __forceinline__ bool row_has_evidence(const int32_t* orow, int nobs) {
@@ -164,7 +145,7 @@ __global__ __launch_bounds__(64) void jt_filter_kernel(JtRun r, int dir_base) {
   constexpr int U = 64 / L;
   const int u = threadIdx.x / L, sub = threadIdx.x % L;
   const int dir = dir_base + (int)blockIdx.y;
-  const JtPlanDev P = stage_plan<LDS>(r, lds, U);
+  const JtPlanDev& P = r.p;
   double* ws = unit_ws<LDS>(r, lds, u, U);
   const int K = P.K;
   const JtVisit* V = reinterpret_cast<const JtVisit*>(P.ip + (dir == 0 ? P.fwd : P.bwd));
@@ -257,7 +238,7 @@ __global__ __launch_bounds__(64) void jt_post_kernel(JtRun r) {
   extern __shared__ double lds[];
   constexpr int U = 64 / L;
   const int u = threadIdx.x / L, sub = threadIdx.x % L;
-  const JtPlanDev P = stage_plan<LDS>(r, lds, U);
+  const JtPlanDev& P = r.p;
   double* ws = unit_ws<LDS>(r, lds, u, U);
   const int K = P.K;
   const JtVisit* V = reinterpret_cast<const JtVisit*>(P.ip + P.post);
@@ -345,8 +326,7 @@ int filter_launch(const JtRun& r, int dirs, hipStream_t st) {
   constexpr int U = 64 / L;
   long blocks = (r.B + U - 1) / U;
   if (!LDS && blocks > kJtGlobalUnits / U) blocks = kJtGlobalUnits / U;
-  const size_t shm = (LDS ? (size_t)U * r.p.ws * sizeof(double) : 0) +
-                     (r.p.stage ? jt_pool_lds_bytes(r.p) : 0);
+  const size_t shm = LDS ? (size_t)U * r.p.ws * sizeof(double) : 0;
   const int dir_base = dirs == 2 ? 0 : (dirs == 0 ? 0 : 1);   // dirs: 0 fwd only, 1 bwd only, 2 both
   hipLaunchKernelGGL((jt_filter_kernel<L, LDS>), dim3((unsigned)blocks, dirs == 2 ? 2 : 1), dim3(64),
                      shm, st, r, dir_base);
@@ -359,8 +339,7 @@ int post_launch(const JtRun& r, hipStream_t st) {
   const long nch = (r.T + r.chunk - 1) / r.chunk;
   long blocks = (r.B * nch + U - 1) / U;
   if (!LDS && blocks > kJtGlobalUnits / U) blocks = kJtGlobalUnits / U;
-  const size_t shm = (LDS ? (size_t)U * r.p.ws * sizeof(double) : 0) +
-                     (r.p.stage ? jt_pool_lds_bytes(r.p) : 0);
+  const size_t shm = LDS ? (size_t)U * r.p.ws * sizeof(double) : 0;
   hipLaunchKernelGGL((jt_post_kernel<L, LDS>), dim3((unsigned)blocks), dim3(64), shm, st, r);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

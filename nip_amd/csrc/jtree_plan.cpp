@@ -390,15 +390,11 @@ static int build_plan(const nipamd_model* mm, int n_obs, const int* obs_vars, in
   if (I.size() > (size_t)0x7fffffff) { why = "schedule too large"; return NIPAMD_ERROR_UNSUPPORTED; }
 
   P.L = maxc <= 64 && K <= 64 && maxout <= 64 ? 16 : 64;
-  const size_t ws_lds = (size_t)(64 / P.L) * p.ws * sizeof(double);
-  P.lds = ws_lds <= kJtLdsBudget;
-  // the schedule and tables are read every step by every unit, mostly along
-  // dependent chains (map -> table, pre-image -> table): staged in LDS when
-  // they fit next to the workspace, so no step waits on an L2 round trip
-  p.nip = (int)I.size();
-  p.ndp = (int)B.dp.size();
-  p.stage = (P.lds ? ws_lds : 0) + jt_pool_lds_bytes(p) <= kJtLdsBudget ? 1 : 0;
-  if (const char* e = std::getenv("NIPAMD_JT_STAGE")) p.stage = p.stage && std::atoi(e) != 0;   // A/B: 0 = global pools
+  if (const char* e = std::getenv("NIPAMD_JT_L")) {       // A/B: lanes per unit (16 or 64)
+    const int l = std::atoi(e);
+    if (l == 16 || l == 64) P.L = l;
+  }
+  P.lds = (size_t)(64 / P.L) * p.ws * sizeof(double) <= 64 * 1024;
   P.hI = std::move(I);
   P.hD = std::move(B.dp);
   return 0;
