@@ -114,7 +114,7 @@ struct JtRun {
   int chunk;              // posterior: time steps per unit
 };
 
-// launches (jtree.hip); L = lanes per sequence unit (16 or 64)
+// launches (jtree.hip); L = lanes per sequence unit (16, 32 or 64)
 int jt_w_launch(const JtRun& r, double* w_out, int L, hipStream_t st);
 int jt_filter_launch(const JtRun& r, int L, bool lds, int dirs, hipStream_t st);
 int jt_post_launch(const JtRun& r, int L, bool lds, hipStream_t st);

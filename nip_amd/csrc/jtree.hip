@@ -348,11 +348,13 @@ int post_launch(const JtRun& r, hipStream_t st) {
 
 int jt_filter_launch(const JtRun& r, int L, bool lds, int dirs, hipStream_t st) {
   if (L == 16) return lds ? filter_launch<16, true>(r, dirs, st) : filter_launch<16, false>(r, dirs, st);
+  if (L == 32) return lds ? filter_launch<32, true>(r, dirs, st) : filter_launch<32, false>(r, dirs, st);
   return lds ? filter_launch<64, true>(r, dirs, st) : filter_launch<64, false>(r, dirs, st);
 }
 
 int jt_post_launch(const JtRun& r, int L, bool lds, hipStream_t st) {
   if (L == 16) return lds ? post_launch<16, true>(r, st) : post_launch<16, false>(r, st);
+  if (L == 32) return lds ? post_launch<32, true>(r, st) : post_launch<32, false>(r, st);
   return lds ? post_launch<64, true>(r, st) : post_launch<64, false>(r, st);
 }
 
@@ -360,6 +362,8 @@ int jt_w_launch(const JtRun& r, double* w_out, int L, hipStream_t st) {
   // one block; its workspace is the first global slot
   if (L == 16)
     hipLaunchKernelGGL((jt_w_kernel<16, false>), dim3(1), dim3(64), 0, st, r, w_out);
+  else if (L == 32)
+    hipLaunchKernelGGL((jt_w_kernel<32, false>), dim3(1), dim3(64), 0, st, r, w_out);
   else
     hipLaunchKernelGGL((jt_w_kernel<64, false>), dim3(1), dim3(64), 0, st, r, w_out);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -390,9 +390,9 @@ static int build_plan(const nipamd_model* mm, int n_obs, const int* obs_vars, in
   if (I.size() > (size_t)0x7fffffff) { why = "schedule too large"; return NIPAMD_ERROR_UNSUPPORTED; }
 
   P.L = maxc <= 64 && K <= 64 && maxout <= 64 ? 16 : 64;
-  if (const char* e = std::getenv("NIPAMD_JT_L")) {       // A/B: lanes per unit (16 or 64)
+  if (const char* e = std::getenv("NIPAMD_JT_L")) {       // A/B: lanes per unit (16, 32 or 64)
     const int l = std::atoi(e);
-    if (l == 16 || l == 64) P.L = l;
+    if (l == 16 || l == 32 || l == 64) P.L = l;
   }
   P.lds = (size_t)(64 / P.L) * p.ws * sizeof(double) <= 64 * 1024;
   P.hI = std::move(I);
