@@ -58,6 +58,9 @@ WORKLOADS = {
     # the general join-tree engine (not a BASELINE config): a factorial HMM,
     # two 4-state chains with one 16-state observation of both (interface {X1, Y1})
     "jtree": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024),
+    # the same slice as a joint-interface chain (16 joint states) on the
+    # matrix-core chain kernels -- what the automatic engine choice runs
+    "joint": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024),
 }
 
 
@@ -198,7 +201,8 @@ def main():
                          "em: config 4, one step = one em_learn iteration (m_step, e_step of "
                          "the shard, the packed all-gather over RCCL, finalize); "
                          "config3: demo1 @ 32 states smoothing; config5: wide-clique smoothing; "
-                         "jtree: a factorial HMM on the general join-tree engine")
+                         "jtree: a factorial HMM on the general join-tree engine; "
+                         "joint: the same slice as a joint-interface chain")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
     args = ap.parse_args()
@@ -221,6 +225,8 @@ def main():
     nodes, pots = spec(args)
     model = nip_amd.Model.from_spec(nodes, pots)
     ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
+    if args.workload == "jtree":
+        model.set_engine(nip_amd.ENGINE_JTREE)     # the joint-interface chain would take it otherwise
     N, M = model.card(q), model.card(ov[0])
     obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
                              for i, v in enumerate(ov)], axis=2)
@@ -331,6 +337,15 @@ def main():
         workload = ("general join-tree engine: factorial HMM, X and Y 4 states each, O1 16 states of both, "
                     "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
         metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
+    elif args.workload == "joint":
+        K = 16                         # joint interface states (X1, Y1)
+        kname = "chain_fb_ckpt_kernel + derive_kernel"
+        # the chain kernel's bytes at K states, then the derive pass: the joint
+        # posterior read back, X1's marginal written
+        bpu = algorithmic_bytes_per_seq_step(K, len(ov), True) + 8 * K + 8 * N
+        workload = ("joint-interface chain: factorial HMM, X and Y 4 states each, O1 16 states of both, "
+                    "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
+        metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (joint-interface chain kernels)"
     elif args.workload == "config3":
         workload = "config3: demo1.net structure, 5 vars x 32 states, A1 B1 observed, C1 posterior, " \
                    "B=%d seq/GPU x T=%d" % (B, T)

@@ -164,6 +164,8 @@ struct DeriveArgs {
   const double* child_E; // [(M+1)][64]: E, then the row sums
   int hid_card;          // kDeriveHidden
   const double* G;       // [card][64][64]
+  int prev_stride;       // kDerivePrev of a joint interface: the variable's digit of the
+  int prev_card;         // joint state (state / stride % card); prev_card 0: the whole interface
 };
 int derive_launch(const DeriveArgs& a, hipStream_t stream);
 

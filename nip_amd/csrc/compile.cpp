@@ -19,6 +19,7 @@
 #include "nip_amd.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -592,9 +593,18 @@ long clique_index(const Model& m, int c, const std::vector<int>& val_of_var) {
   for (int v : m.cliques[c].vars) { idx += val_of_var[v] * stride; stride *= m.vars[v].card; }
   return idx;
 }
+
+void build_single_chain_plan(Model& m);
+void build_joint_chain_plan(Model& m);
 }  // namespace
 
 void build_chain_plan(Model& m) {
+  build_single_chain_plan(m);
+  if (!m.chain.valid) build_joint_chain_plan(m);
+}
+
+namespace {
+void build_single_chain_plan(Model& m) {
   ChainPlan& P = m.chain;
   P = ChainPlan();
   if (m.outgoing.size() != 1 || m.previous_outgoing.size() != 1) return;
@@ -705,6 +715,169 @@ void build_chain_plan(Model& m) {
   P.hmm = hidden.empty() && P.emits.size() == 1 && V.size() == 3 && N <= 16;
   P.valid = true;
 }
+
+// Several interface variables (a factorial HMM, coupled chains): the slice is
+// still an interface chain over the JOINT interface state when its
+// distribution over (previous interface x, interface y, observation
+// candidates o_k) factorises as A[x][y] prod_k E_k[y][o_k].  x and y index the
+// joint states as the general engine's interface messages do (dimension 0
+// fastest over previous_outgoing / outgoing, paired by position), the other
+// variables of the slice are summed out, and the factorisation is checked
+// numerically on the slice's joint -- the product of the clique tables the
+// reference propagates (orig_p, nip_global_retraction, src/nipjointree.c:791-817)
+// and the priors use_priors enters every slice (src/nip.c:88-119) -- so a
+// slice that does not factorise keeps the general engine.  Candidates are
+// leaf variables whose parents are all interface variables; each interface
+// variable is a pseudo-child with an indicator table, so its marginal is
+// derived from the joint posterior (derive.hip, kDeriveChild) and evidence on
+// it is an indicator row.
+bool every_slice_prior(const Var& v) {
+  if (!v.parents.empty() || !v.has_prior || (v.ifs & IF_OLD_OUTGOING)) return false;
+  for (double x : v.prior) if (x > 0) return true;            // nip_enter_prior rejects a zero vector
+  return false;
+}
+
+void build_joint_chain_plan(Model& m) {
+  ChainPlan& P = m.chain;
+  P = ChainPlan();
+  const auto& V = m.vars;
+  const int nv = (int)V.size();
+  const auto &prev = m.previous_outgoing, &cur = m.outgoing;
+  if (cur.size() < 2 || cur.size() != prev.size()) return;
+  long K = 1;
+  for (size_t i = 0; i < cur.size(); i++) {
+    if (V[cur[i]].card != V[prev[i]].card || !V[prev[i]].parents.empty()) return;
+    K *= V[cur[i]].card;
+    if (K > 64) return;
+  }
+  std::vector<int> role(nv, 3);                               // 0 prev, 1 cur, 2 candidate, 3 summed
+  for (int v : prev) role[v] = 0;
+  for (int v : cur) role[v] = 1;
+  std::vector<char> has_child(nv, 0);
+  for (int v = 0; v < nv; v++) for (int q : V[v].parents) has_child[q] = 1;
+  std::vector<int> cand;
+  long C = 1;
+  for (int v = 0; v < nv; v++) {
+    if (role[v] != 3 || has_child[v] || V[v].parents.empty() || V[v].card > 253) continue;
+    bool ok = true;
+    for (int q : V[v].parents) ok &= role[q] == 1;
+    if (!ok) continue;
+    role[v] = 2;
+    cand.push_back(v);
+    C *= V[v].card;
+    if (K * K * C > (1L << 22)) return;
+  }
+  long total = 1;
+  for (int v = 0; v < nv; v++) { total *= V[v].card; if (total > (1L << 20)) return; }
+  // F[(x * K + y) * C + c]: the slice joint with everything else summed out
+  std::vector<double> F((size_t)(K * K * C), 0.0);
+  std::vector<int> val(nv, 0);
+  for (long i = 0; i < total; i++) {
+    double w = 1.0;
+    for (size_t c = 0; c < m.cliques.size() && w != 0.0; c++) {
+      const auto& o = m.cliques[c].original;
+      const long k = clique_index(m, (int)c, val);
+      w *= k < (long)o.size() ? o[k] : 1.0;
+    }
+    for (int v = 0; v < nv && w != 0.0; v++) if (every_slice_prior(V[v])) w *= V[v].prior[val[v]];
+    long x = 0, y = 0, cc = 0, sx = 1, sc = 1;
+    for (size_t k = 0; k < cur.size(); k++) {
+      x += val[prev[k]] * sx; y += val[cur[k]] * sx; sx *= V[cur[k]].card;
+    }
+    for (int v : cand) { cc += val[v] * sc; sc *= V[v].card; }
+    F[(size_t)((x * K + y) * C + cc)] += w;
+    for (int v = 0; v < nv; v++) {                              // odometer, variable 0 fastest
+      if (++val[v] < V[v].card) break;
+      val[v] = 0;
+    }
+  }
+  // A and the candidates' tables, then the factorisation check
+  std::vector<double> A((size_t)(K * K), 0.0);
+  double fmax = 0.0;
+  for (long xy = 0; xy < K * K; xy++)
+    for (long c = 0; c < C; c++) { A[xy] += F[xy * C + c]; fmax = std::max(fmax, F[xy * C + c]); }
+  std::vector<std::vector<double>> E(cand.size());
+  for (size_t k = 0; k < cand.size(); k++) {
+    const int M = V[cand[k]].card;
+    long stride = 1;
+    for (size_t j = 0; j < k; j++) stride *= V[cand[j]].card;
+    E[k].assign((size_t)M * 64, 0.0);
+    for (long y = 0; y < K; y++) {
+      long xb = -1;
+      for (long x = 0; x < K; x++) if (A[x * K + y] > 0 && (xb < 0 || A[x * K + y] > A[xb * K + y])) xb = x;
+      if (xb < 0) continue;                                      // y unreachable: its evidence never matters
+      for (long c = 0; c < C; c++)
+        E[k][(size_t)((c / stride) % M) * 64 + y] += F[(xb * K + y) * C + c];
+      for (int mm = 0; mm < M; mm++) E[k][(size_t)mm * 64 + y] /= A[xb * K + y];
+    }
+  }
+  for (long x = 0; x < K; x++)
+    for (long y = 0; y < K; y++)
+      for (long c = 0; c < C; c++) {
+        double f = A[x * K + y];
+        long r = c;
+        for (size_t k = 0; k < cand.size(); k++) {
+          const int M = V[cand[k]].card;
+          f *= E[k][(size_t)(r % M) * 64 + y];
+          r /= M;
+        }
+        if (std::fabs(f - F[(x * K + y) * C + c]) > 1e-13 * fmax) return;   // does not factorise
+      }
+  P.N = (int)K;
+  P.A64.assign(64 * 64, 0.0);
+  for (long x = 0; x < K; x++)
+    for (long y = 0; y < K; y++) P.A64[x * 64 + y] = A[x * K + y];
+  P.pi64.assign(64, 0.0);
+  for (long x = 0; x < K; x++) {
+    double p = 1.0;
+    long r = x;
+    for (int v : prev) {
+      const int d = (int)(r % V[v].card);
+      r /= V[v].card;
+      bool entered = V[v].has_prior;
+      if (entered) { entered = false; for (double q : V[v].prior) entered |= q > 0; }
+      if (entered) p *= V[v].prior[d];
+    }
+    P.pi64[x] = p;
+  }
+  for (size_t k = 0; k < cand.size(); k++) {
+    ChainEmit em;
+    em.var = cand[k]; em.clique = V[cand[k]].family; em.M = V[cand[k]].card;
+    em.E = std::move(E[k]);
+    em.s.assign(64, 0.0);
+    for (long y = 0; y < K; y++)
+      for (int mm = 0; mm < em.M; mm++) em.s[y] += em.E[(size_t)mm * 64 + y];
+    P.emits.push_back(std::move(em));
+  }
+  long sx = 1;
+  for (size_t i = 0; i < cur.size(); i++) {                   // the interface variables: indicator pseudo-children
+    ChainEmit em;
+    em.var = cur[i]; em.clique = V[cur[i]].family; em.M = V[cur[i]].card;
+    em.E.assign((size_t)em.M * 64, 0.0);
+    em.s.assign(64, 0.0);
+    for (long y = 0; y < K; y++) { em.E[(size_t)((y / sx) % em.M) * 64 + y] = 1.0; em.s[y] = 1.0; }
+    sx *= em.M;
+    P.emits.push_back(std::move(em));
+  }
+  P.s_all64.assign(64, 0.0);
+  for (long y = 0; y < K; y++) {
+    double s = 1.0;
+    for (const auto& em : P.emits) s *= em.s[y];
+    P.s_all64[y] = s;
+  }
+  if (K <= 16) {
+    P.A.assign(256, 0.0);
+    P.pi.assign(16, 0.0);
+    for (long x = 0; x < K; x++) {
+      P.pi[x] = P.pi64[x];
+      for (long y = 0; y < K; y++) P.A[x * 16 + y] = P.A64[x * 64 + y];
+    }
+  }
+  P.jprev = prev;
+  P.joint = true;
+  P.valid = true;
+}
+}  // namespace
 
 void hidden_table(const Model& m, int j, std::vector<double>& G) {
   const ChainPlan& P = m.chain;

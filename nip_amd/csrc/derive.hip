@@ -50,6 +50,14 @@ __device__ __forceinline__ double evidence(const DeriveArgs& a, long b, int t, i
   return e;
 }
 
+// one variable's marginal from a joint interface vector: out[k] = sum of v[x]
+// over the joint states x whose digit (x / stride % card) is k
+__device__ __forceinline__ int project_digit(const double* v, int N, int stride, int card, double* out) {
+  for (int k = 0; k < card; k++) out[k] = 0.0;
+  for (int x = 0; x < N; x++) out[(x / stride) % card] += v[x];
+  return card;
+}
+
 __global__ __launch_bounds__(256)
 void derive_kernel(DeriveArgs a) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -78,7 +86,8 @@ void derive_kernel(DeriveArgs a) {
   } else if (a.kind == kDerivePrev && !a.filter && t > 0) {
     n = N;
     const double* q = pc - a.cur_tstride;
-    for (int x = 0; x < N; x++) out[x] = q[x];
+    if (a.prev_card > 0) n = project_digit(q, N, a.prev_stride, a.prev_card, out);
+    else for (int x = 0; x < N; x++) out[x] = q[x];
   } else {
     // a_t and lambda_t
     double av[kMaxN], lam[kMaxN];
@@ -95,11 +104,14 @@ void derive_kernel(DeriveArgs a) {
     }
     if (a.kind == kDerivePrev) {
       n = N;
+      double pj[kMaxN];
       for (int x = 0; x < N; x++) {
         double acc = 0.0;
         for (int y = 0; y < N; y++) acc += a.A[x * 64 + y] * lam[y];
-        out[x] = av[x] * acc;
+        pj[x] = av[x] * acc;
       }
+      if (a.prev_card > 0) n = project_digit(pj, N, a.prev_stride, a.prev_card, out);
+      else for (int x = 0; x < N; x++) out[x] = pj[x];
     } else {
       n = a.hid_card;
       for (int d = 0; d < n; d++) {

@@ -355,11 +355,15 @@ bool use_mfma() {
 }
 
 // Role of a query variable in the chain plan: 0 the interface variable, 1 its
-// previous-slice copy, 2 + k leaf child k, 1000 + j hidden parent j; -1 none.
-// Every variable of a valid plan has one (build_chain_plan accounts for all).
+// previous-slice copy, 2 + k leaf child k, 500 + i previous-slice interface
+// variable i of a joint interface, 1000 + j hidden parent j; -1 none.
+// Every variable of a single-variable plan has one (build_chain_plan accounts
+// for all); a joint plan covers the interface variables, their previous-slice
+// copies and the leaf children it factorises.
 int query_kind(const nipamd::ChainPlan& P, int v) {
   if (v == P.v_cur) return 0;
   if (v == P.v_prev) return 1;
+  for (size_t i = 0; i < P.jprev.size(); i++) if (P.jprev[i] == v) return 500 + (int)i;
   for (size_t k = 0; k < P.emits.size(); k++) if (P.emits[k].var == v) return 2 + (int)k;
   for (size_t j = 0; j < P.hidden.size(); j++) if (P.hidden[j] == v) return 1000 + (int)j;
   return -1;
@@ -524,7 +528,7 @@ int nipamd_jt_plan_dump(const nipamd_model* mm, int n_obs, const int* obs_vars, 
 int nipamd_model_fold(nipamd_model* mm, int keep, double* out, long cap, double* kernel_ms, double* bytes) {
   if (!mm || !out) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   const auto& P = mm->m.chain;
-  if (!P.valid) return fail(NIPAMD_ERROR_UNSUPPORTED, "the model has no interface-chain plan");
+  if (!P.valid || P.joint) return fail(NIPAMD_ERROR_UNSUPPORTED, "the model has no single-variable interface-chain plan");
   if (keep < -1 || keep >= (int)P.hidden.size()) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad hidden parent");
   const long need = (keep < 0 ? 1L : (long)mm->m.vars[P.hidden[keep]].card) * 64 * 64;
   if (cap < need) return fail(NIP_ERROR_INVALID_ARGUMENT, "output buffer too small");
@@ -938,6 +942,14 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     g.child_col = -1;
     if (kind[i] == 1) {
       g.kind = nipamd::kDerivePrev;
+    } else if (kind[i] >= 500 && kind[i] < 1000) {
+      // a joint interface's previous-slice variable: its digit of the joint
+      // previous-interface marginal
+      const int k = kind[i] - 500;
+      g.kind = nipamd::kDerivePrev;
+      g.prev_stride = 1;
+      for (int j = 0; j < k; j++) g.prev_stride *= mm->m.vars[P.jprev[j]].card;
+      g.prev_card = mm->m.vars[P.jprev[k]].card;
     } else if (kind[i] < 1000) {
       const int k = kind[i] - 2;
       g.kind = nipamd::kDeriveChild;

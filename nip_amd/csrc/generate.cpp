@@ -162,7 +162,7 @@ int build_tables(const nipamd_model* mm, GenCache& g) {
   const Model& m = mm->m;
   const ChainPlan& P = m.chain;
   const auto& V = m.vars;
-  if (!P.valid) return set_error(NIPAMD_ERROR_UNSUPPORTED, "generate: the model has no interface-chain plan");
+  if (!P.valid || P.joint) return set_error(NIPAMD_ERROR_UNSUPPORTED, "generate: the model has no single-variable interface-chain plan");
   if (P.hidden.size() + 2 > (size_t)kGenMaxCtx || V.size() > (size_t)kGenMaxVars)
     return set_error(NIP_ERROR_INVALID_ARGUMENT, "generate: too many variables in the slice");
   const int N = P.N, vp = P.v_prev, vc = P.v_cur, cin = P.c_trans;

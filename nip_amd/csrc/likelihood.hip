@@ -98,7 +98,7 @@ extern "C" int nipamd_likelihood(nipamd_model* mm, const int32_t* d_obs, int n_o
       (B > 0 && T > 0 && (!d_m1 || !d_m2 || !d_ll || (n_obs && !d_obs))))
     return set_error(NIP_ERROR_INVALID_ARGUMENT, "likelihood: bad arguments");
   const ChainPlan& P = mm->m.chain;
-  if (!P.valid) return set_error(NIPAMD_ERROR_UNSUPPORTED, "likelihood: the model has no interface-chain plan");
+  if (!P.valid || P.joint) return set_error(NIPAMD_ERROR_UNSUPPORTED, "likelihood: the model has no single-variable interface-chain plan");
   if (int rc = ensure_fold(mm)) return rc;
   const int N = P.N;
   LikArgs a{};

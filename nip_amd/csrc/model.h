@@ -93,6 +93,12 @@ struct ChainPlan {
   // the GPU when the engine first needs them (fold.hip), not here
   bool fold_gpu = false;
   bool folded = false;
+  // joint interface chain (several interface variables, compile.cpp
+  // build_joint_chain_plan): N = the joint interface's states, v_prev = v_cur =
+  // -1, no hidden parents, emits = the observation candidates followed by one
+  // indicator pseudo-child per interface variable; fb / filter only
+  bool joint = false;
+  std::vector<int> jprev;           // joint: previous_outgoing (their marginals: derive.hip kDerivePrev, projected)
 };
 constexpr long kGpuFoldMin = 1L << 22;
 struct Model {

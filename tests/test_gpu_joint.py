@@ -1,0 +1,133 @@
+"""Joint-interface chains (compile.cpp build_joint_chain_plan): slices with
+several interface variables -- factorial and coupled HMMs -- run as interface
+chains over the joint interface state on the matrix-core chain kernels, with
+the interface variables' marginals derived from the joint posterior.
+
+Checked against the general join-tree engine (NIPAMD_ENGINE_JTREE, itself
+pinned to the reference's own code by test_gpu_jtree.py) on the same inputs,
+and against the oracle on a few sequences.  Tolerances as every fb kernel
+(DESIGN.md 6): posteriors abs 1e-12, ll rel 1e-12 or both -DBL_MAX."""
+import numpy as np
+import pytest
+import torch
+
+import nip_amd
+from nip_amd import synth
+from oracle.bind import PortOracle
+
+pytestmark = pytest.mark.gpu
+
+DBL_MAX = np.finfo(np.float64).max
+POST_TOL = 1e-12
+LL_RTOL = 1e-12
+
+
+def close_ll(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    both_min = (a == -DBL_MAX) & (b == -DBL_MAX)
+    return bool(np.all(both_min | (np.abs(a - b) <= LL_RTOL * np.maximum(1.0, np.abs(b)))))
+
+
+def run(model, obs, ov, q, filt=False):
+    o = torch.from_numpy(np.ascontiguousarray(obs, np.int32)).cuda()
+    fn = nip_amd.forward_inference if filt else nip_amd.forward_backward_inference
+    post, ll, st = fn(model, o, ov, q)
+    torch.cuda.synchronize()
+    return post.cpu().numpy(), ll.cpu().numpy(), st.cpu().numpy()
+
+
+def both_engines(model, obs, ov, q, filt=False):
+    model.set_engine(nip_amd.ENGINE_CHAIN)
+    assert model.gpu_supported(ov, q), "expected a joint-interface chain plan"
+    a = run(model, obs, ov, q, filt)
+    model.set_engine(nip_amd.ENGINE_JTREE)
+    b = run(model, obs, ov, q, filt)
+    model.set_engine(nip_amd.ENGINE_AUTO)
+    return a, b
+
+
+def make_obs(rng, B, T, cards, missing=0.2, invalid=0.0):
+    cols = []
+    for M in cards:
+        o = rng.integers(0, M, size=(B, T, 1)).astype(np.int32)
+        o[rng.random(o.shape) < missing] = -1
+        o[rng.random(o.shape) < invalid] = M          # out of range: zero evidence
+        cols.append(o)
+    return np.concatenate(cols, axis=2)
+
+
+CASES = [
+    # name, spec, observed, queried
+    ("factorial4x4", synth.factorial_spec(4, 4, 16), ["O1"], ["X1"]),
+    ("factorial4x3", synth.factorial_spec(4, 3, 5), ["O1"], ["X1", "Y1", "Y0", "X0"]),
+    ("coupled", synth.coupled_spec(), ["A1", "B1"], ["Y1", "X1", "A1", "X0"]),
+    ("coupled_one_obs", synth.coupled_spec(), ["B1"], ["X1", "A1"]),
+    ("factorial_obs_iface", synth.factorial_spec(4, 3, 5), ["O1", "X1"], ["X1", "Y1"]),
+    ("factorial8x8", synth.factorial_spec(8, 8, 6), ["O1"], ["Y1"]),
+]
+
+
+@pytest.mark.parametrize("name,spec,osyms,qsyms", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("T", [1, 2, 37, 300])
+def test_joint_chain_equals_general_engine(name, spec, osyms, qsyms, T):
+    m = nip_amd.Model.from_spec(*spec)
+    ov, q = [m.variable(v) for v in osyms], [m.variable(v) for v in qsyms]
+    rng = np.random.default_rng(T * 31 + len(name))
+    obs = make_obs(rng, 19, T, [m.card(v) for v in ov])
+    for filt in (False, True):
+        (pa, la, sa), (pb, lb, sb) = both_engines(m, obs, ov, q, filt)
+        assert np.abs(pa - pb).max() <= POST_TOL, (filt, np.abs(pa - pb).max())
+        assert close_ll(la, lb)
+        assert np.array_equal(sa != 0, sb != 0)
+
+
+@pytest.mark.parametrize("name,spec,osyms,qsyms", CASES[:3], ids=[c[0] for c in CASES[:3]])
+def test_joint_chain_vs_oracle(name, spec, osyms, qsyms):
+    m = nip_amd.Model.from_spec(*spec)
+    ov, q = [m.variable(v) for v in osyms], [m.variable(v) for v in qsyms]
+    rng = np.random.default_rng(7)
+    obs = make_obs(rng, 6, 45, [m.card(v) for v in ov])
+    obs[0] = -1                                       # a fully missing sequence
+    post, ll, st = run(m, obs, ov, q)
+    assert not st.any()
+    assert ll[0] == 0.0
+    orc = PortOracle(m.desc())
+    for b in range(obs.shape[0]):
+        rp, rl = orc.fb(obs[b], ov, q)
+        assert np.abs(post[b] - rp).max() <= POST_TOL
+        assert close_ll([ll[b]], [rl])
+
+
+def test_joint_chain_zero_mass_and_ragged_batch():
+    """Out-of-range codes (an all-zero likelihood) kill a sequence exactly as
+    on the general engine; B not a multiple of the kernels' 16-sequence
+    blocks and above one launch wave."""
+    m = nip_amd.Model.from_spec(*synth.factorial_spec(4, 4, 16))
+    ov, q = [m.variable("O1")], [m.variable("X1"), m.variable("Y1")]
+    rng = np.random.default_rng(3)
+    obs = make_obs(rng, 1000 + 13, 64, [16], missing=0.1, invalid=0.002)
+    (pa, la, sa), (pb, lb, sb) = both_engines(m, obs, ov, q)
+    assert (sa != 0).any() and (sa == 0).any()
+    assert np.array_equal(sa != 0, sb != 0)
+    assert close_ll(la, lb)
+    assert np.abs(pa - pb).max() <= POST_TOL
+
+
+def test_joint_chain_scale_properties():
+    """The bench slice at a launch-filling batch: normalisation, filter ll ==
+    smoothing ll, last filtered step == last smoothed step, spot oracle parity."""
+    m = nip_amd.Model.from_spec(*synth.factorial_spec(4, 4, 16))
+    ov, q = [m.variable("O1")], [m.variable("X1")]
+    B, T = 4096, 256
+    obs = synth.observations(B, T, 16, seed=5)
+    post, ll, st = run(m, obs, ov, q)
+    fpost, fll, _ = run(m, obs, ov, q, filt=True)
+    assert not st.any()
+    assert np.abs(post.sum(-1) - 1).max() < 1e-12
+    assert close_ll(fll, ll)
+    assert np.abs(post[:, -1] - fpost[:, -1]).max() < 1e-12
+    orc = PortOracle(m.desc())
+    for b in (0, 2049, 4095):
+        rp, rl = orc.fb(obs[b], ov, q)
+        assert np.abs(post[b] - rp).max() <= POST_TOL
+        assert close_ll([ll[b]], [rl])

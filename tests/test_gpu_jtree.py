@@ -69,6 +69,23 @@ def test_general_slice_matches_reference(path):
 
 
 @pytest.mark.parametrize("path", GEN, ids=[os.path.basename(p) for p in GEN])
+def test_general_slice_matches_reference_on_general_engine(path):
+    """The same fixtures with the general engine forced: slices with several
+    interface variables otherwise run as joint-interface chains
+    (test_gpu_joint.py), so this keeps the general engine's own coverage."""
+    z = np.load(path)
+    m = gen_model(z)
+    m.set_engine(nip_amd.ENGINE_JTREE)
+    ov, q = list(z["obs_vars"]), list(z["query"])
+    post, ll, st = run(m, z["obs"], ov, q)
+    assert np.abs(post - z["post"]).max() <= POST_TOL
+    assert close_ll(ll, z["ll"])
+    fpost, fll, _ = run(m, z["obs"], ov, q, filt=True)
+    assert np.abs(fpost - z["fpost"]).max() <= POST_TOL
+    assert close_ll(fll, z["fll"])
+
+
+@pytest.mark.parametrize("path", GEN, ids=[os.path.basename(p) for p in GEN])
 def test_general_estep_matches_reference(path):
     z = np.load(path)
     m = gen_model(z)
