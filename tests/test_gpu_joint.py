@@ -90,7 +90,9 @@ def test_joint_chain_vs_oracle(name, spec, osyms, qsyms):
     obs[0] = -1                                       # a fully missing sequence
     post, ll, st = run(m, obs, ov, q)
     assert not st.any()
-    assert ll[0] == 0.0
+    # no evidence anywhere: ll = 0 up to rounding (the matrix-core kernel's m1
+    # is alpha . (A s), m2 the sum of alpha's successor -- equal in exact arithmetic)
+    assert abs(ll[0]) <= 1e-12
     orc = PortOracle(m.desc())
     for b in range(obs.shape[0]):
         rp, rl = orc.fb(obs[b], ov, q)
