@@ -133,7 +133,9 @@ int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, bool filter_only, hipS
 
 // marginals of the chain's other variables from the interface variable's
 // (derive.hip): the previous-slice copy, a hidden parent, a leaf child
-enum : int { kDerivePrev = 0, kDeriveChild = 1, kDeriveHidden = 2 };
+// kDeriveProject: a joint interface's variable, the digit (prev_stride,
+// prev_card) of the joint posterior
+enum : int { kDerivePrev = 0, kDeriveChild = 1, kDeriveHidden = 2, kDeriveProject = 3 };
 struct DeriveArgs {
   int kind;
   int filter;            // 1: forward_inference marginals (cur = filtered)
@@ -164,8 +166,8 @@ struct DeriveArgs {
   const double* child_E; // [(M+1)][64]: E, then the row sums
   int hid_card;          // kDeriveHidden
   const double* G;       // [card][64][64]
-  int prev_stride;       // kDerivePrev of a joint interface: the variable's digit of the
-  int prev_card;         // joint state (state / stride % card); prev_card 0: the whole interface
+  int prev_stride;       // kDerivePrev of a joint interface / kDeriveProject: the variable's digit
+  int prev_card;         // of the joint state (state / stride % card); prev_card 0: the whole interface
 };
 int derive_launch(const DeriveArgs& a, hipStream_t stream);
 

@@ -874,6 +874,7 @@ void build_joint_chain_plan(Model& m) {
     }
   }
   P.jprev = prev;
+  P.jcur = cur;
   P.joint = true;
   P.valid = true;
 }

@@ -52,9 +52,14 @@ __device__ __forceinline__ double evidence(const DeriveArgs& a, long b, int t, i
 
 // one variable's marginal from a joint interface vector: out[k] = sum of v[x]
 // over the joint states x whose digit (x / stride % card) is k
+// (states in increasing order; each output written once)
 __device__ __forceinline__ int project_digit(const double* v, int N, int stride, int card, double* out) {
-  for (int k = 0; k < card; k++) out[k] = 0.0;
-  for (int x = 0; x < N; x++) out[(x / stride) % card] += v[x];
+  for (int k = 0; k < card; k++) {
+    double s = 0.0;
+    for (int hi = k * stride; hi < N; hi += stride * card)
+      for (int lo = 0; lo < stride; lo++) s += v[hi + lo];
+    out[k] = s;
+  }
   return card;
 }
 
@@ -68,7 +73,9 @@ void derive_kernel(DeriveArgs a) {
   const double* pc = a.cur + b * a.cur_bstride + (long)t * a.cur_tstride;
   double* out = a.out + b * a.out_bstride + (long)t * a.out_tstride + a.out_off;
   int n = 0;
-  if (a.kind == kDeriveChild) {
+  if (a.kind == kDeriveProject) {
+    n = project_digit(pc, N, a.prev_stride, a.prev_card, out);
+  } else if (a.kind == kDeriveChild) {
     const int M = a.child_M;
     n = M;
     const int o = a.child_col >= 0 ? a.obs[b * a.obs_bstride + (long)t * a.obs_tstride + a.child_col] : -1;

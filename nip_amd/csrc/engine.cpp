@@ -355,8 +355,9 @@ bool use_mfma() {
 }
 
 // Role of a query variable in the chain plan: 0 the interface variable, 1 its
-// previous-slice copy, 2 + k leaf child k, 500 + i previous-slice interface
-// variable i of a joint interface, 1000 + j hidden parent j; -1 none.
+// previous-slice copy, 2 + k leaf child k, 500 + i / 700 + i previous-slice /
+// current interface variable i of a joint interface, 1000 + j hidden parent j;
+// -1 none.
 // Every variable of a single-variable plan has one (build_chain_plan accounts
 // for all); a joint plan covers the interface variables, their previous-slice
 // copies and the leaf children it factorises.
@@ -364,6 +365,7 @@ int query_kind(const nipamd::ChainPlan& P, int v) {
   if (v == P.v_cur) return 0;
   if (v == P.v_prev) return 1;
   for (size_t i = 0; i < P.jprev.size(); i++) if (P.jprev[i] == v) return 500 + (int)i;
+  for (size_t i = 0; i < P.jcur.size(); i++) if (P.jcur[i] == v) return 700 + (int)i;
   for (size_t k = 0; k < P.emits.size(); k++) if (P.emits[k].var == v) return 2 + (int)k;
   for (size_t j = 0; j < P.hidden.size(); j++) if (P.hidden[j] == v) return 1000 + (int)j;
   return -1;
@@ -943,13 +945,15 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     if (kind[i] == 1) {
       g.kind = nipamd::kDerivePrev;
     } else if (kind[i] >= 500 && kind[i] < 1000) {
-      // a joint interface's previous-slice variable: its digit of the joint
-      // previous-interface marginal
-      const int k = kind[i] - 500;
-      g.kind = nipamd::kDerivePrev;
+      // a joint interface's variable: its digit of the joint interface
+      // marginal (current slice), or of the derived previous-interface one
+      const bool is_prev = kind[i] < 700;
+      const int k = kind[i] - (is_prev ? 500 : 700);
+      const auto& vs = is_prev ? P.jprev : P.jcur;
+      g.kind = is_prev ? nipamd::kDerivePrev : nipamd::kDeriveProject;
       g.prev_stride = 1;
-      for (int j = 0; j < k; j++) g.prev_stride *= mm->m.vars[P.jprev[j]].card;
-      g.prev_card = mm->m.vars[P.jprev[k]].card;
+      for (int j = 0; j < k; j++) g.prev_stride *= mm->m.vars[vs[j]].card;
+      g.prev_card = mm->m.vars[vs[k]].card;
     } else if (kind[i] < 1000) {
       const int k = kind[i] - 2;
       g.kind = nipamd::kDeriveChild;

@@ -99,6 +99,7 @@ struct ChainPlan {
   // indicator pseudo-child per interface variable; fb / filter only
   bool joint = false;
   std::vector<int> jprev;           // joint: previous_outgoing (their marginals: derive.hip kDerivePrev, projected)
+  std::vector<int> jcur;            // joint: outgoing (their marginals: derive.hip kDeriveProject)
 };
 constexpr long kGpuFoldMin = 1L << 22;
 struct Model {
