@@ -142,11 +142,52 @@ void derive_kernel(DeriveArgs a) {
   }
 }
 
+// kDeriveProject over a dense [B][T][N] joint posterior (the engine's work
+// buffer): a block's rows (256, fewer past 31 states: 64 KB of LDS) are
+// staged in LDS by coalesced loads (rows
+// padded to N + 1 doubles, so a wave's per-thread row reads spread over the
+// banks), then each thread projects and normalises its row as derive_kernel
+// does -- same sums in the same order, so the same bits.
+__host__ __device__ inline int project_rows(int N) {
+  const int r = 65536 / (8 * (N + 1));
+  return r < 256 ? r : 256;
+}
+
+__global__ __launch_bounds__(256)
+void project_kernel(DeriveArgs a) {
+  extern __shared__ double rows[];
+  const int N = a.N, P = N + 1, R = project_rows(N);
+  const long total = a.B * (long)a.T;
+  const long r0 = (long)blockIdx.x * R;
+  const int nr = (int)(total - r0 < R ? total - r0 : R);
+  const double* src = a.cur + r0 * N;
+  for (int i = threadIdx.x; i < nr * N; i += 256) rows[(i / N) * P + (i % N)] = src[i];
+  __syncthreads();
+  if ((int)threadIdx.x >= nr) return;
+  const long i = r0 + threadIdx.x;
+  const long b = i / a.T;
+  const int t = (int)(i - b * a.T);
+  double* out = a.out + b * a.out_bstride + (long)t * a.out_tstride + a.out_off;
+  const int n = project_digit(rows + threadIdx.x * P, N, a.prev_stride, a.prev_card, out);
+  double z = 0.0;
+  for (int k = 0; k < n; k++) z += out[k];
+  if (z != 0.0) {
+    const double r = 1.0 / z;
+    for (int k = 0; k < n; k++) out[k] *= r;
+  }
+}
+
 }  // namespace
 
 int derive_launch(const DeriveArgs& a, hipStream_t stream) {
   const long n = a.B * (long)a.T;
   if (n == 0) return 0;
+  if (a.kind == kDeriveProject && a.cur_tstride == a.N && a.cur_bstride == (long)a.T * a.N) {
+    const int R = project_rows(a.N);
+    const size_t lds = (size_t)R * (a.N + 1) * sizeof(double);        // <= 64 KB
+    hipLaunchKernelGGL(project_kernel, dim3((unsigned)((n + R - 1) / R)), dim3(256), lds, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   hipLaunchKernelGGL(derive_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
