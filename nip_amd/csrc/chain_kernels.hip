@@ -534,6 +534,25 @@ void estep_finalize_kernel(const double* __restrict__ R, ChainFinalize f, double
   }
 }
 
+__global__ __launch_bounds__(256)
+void estep_map_finalize_kernel(const double* __restrict__ R, int n, const int* __restrict__ ptr,
+                               const int* __restrict__ idx, const double* __restrict__ coef,
+                               double* __restrict__ counts) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  double acc = 0.0;
+  for (int j = ptr[p]; j < ptr[p + 1]; j++) acc += coef[j] * R[idx[j]];
+  counts[p] += acc;
+}
+
+int estep_map_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef,
+                              double* counts, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(estep_map_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, R, n, ptr, idx,
+                     coef, counts);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream) {
   hipLaunchKernelGGL(estep_finalize_kernel, dim3(1), dim3(256), 0, stream, R, f, counts);
   return hipGetLastError() == hipSuccess ? 0 : -1;

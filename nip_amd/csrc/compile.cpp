@@ -875,6 +875,9 @@ void build_joint_chain_plan(Model& m) {
   }
   P.jprev = prev;
   P.jcur = cur;
+  bool summed = false;
+  for (int v = 0; v < nv; v++) summed |= role[v] == 3;
+  P.jhmm = !summed && cand.size() == 1 && K <= 16;
   P.joint = true;
   P.valid = true;
 }

@@ -74,6 +74,11 @@ struct DevState {
   size_t Q_bytes = 0;
   std::vector<double*> childE;   // per leaf child [(M+1)][64]: E, then the row sums
   std::vector<double*> G;        // per hidden parent [card][64][64], built on first use
+  // joint-interface e_step finalize: the slab -> em_learn layout map (CSR)
+  int* jm_ptr = nullptr;
+  int* jm_idx = nullptr;
+  double* jm_coef = nullptr;
+  int jm_n = 0;
 };
 
 DevState* dev_of(nipamd_model* mm) {
@@ -94,6 +99,8 @@ void free_tables(DevState* d) {
   for (double* p : d->G) (void)hipFree(p);
   d->childE.clear();
   d->G.clear();
+  (void)hipFree(d->jm_ptr); (void)hipFree(d->jm_idx); (void)hipFree(d->jm_coef);
+  d->jm_ptr = nullptr; d->jm_idx = nullptr; d->jm_coef = nullptr; d->jm_n = 0;
 }
 
 void dev_release(DevState* d) {
@@ -1034,7 +1041,7 @@ int nipamd_filter_host(nipamd_model* mm, const int32_t* obs, int n_obs, const in
 int nipamd_estep_partial_size(const nipamd_model* mm) {
   if (!mm) return -1;
   const int ps = nipamd::param_size(mm->m);
-  if (mm->engine != NIPAMD_ENGINE_JTREE && mm->m.chain.valid && mm->m.chain.hmm)
+  if (mm->engine != NIPAMD_ENGINE_JTREE && mm->m.chain.valid && (mm->m.chain.hmm || mm->m.chain.jhmm))
     return std::max(ps, nipamd::chain_estep_slab(mm->m.chain.emits[0].M));
   return mm->engine == NIPAMD_ENGINE_CHAIN ? -1 : ps;
 }
@@ -1057,7 +1064,8 @@ static int chain_estep_kernel(const nipamd_model* mm, int T) {
 
 static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r) {
   std::string why;
-  if (mm->engine == NIPAMD_ENGINE_JTREE || !mm->m.chain.valid || !mm->m.chain.hmm) return false;
+  if (mm->engine == NIPAMD_ENGINE_JTREE || !mm->m.chain.valid || !(mm->m.chain.hmm || mm->m.chain.jhmm))
+    return false;
   if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why)) return false;
   if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0)) return false;   // evidence on the child only
   return chain_estep_kernel(mm, T) != 0;
@@ -1163,17 +1171,119 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   return 0;
 }
 
+// A joint interface's e_step counts (the HMM e_step kernel's slab over the
+// joint states: xi sums Kf / Kb without the A factor, M1 tables of the
+// observation, the t = 0 posterior P0) projected onto every family of the
+// em_learn layout (child first, then its parents, nip.c:2101-2128): the
+// family's value at a joint (x, y) is its variables' digits, previous-slice
+// variables from x and interface variables from y.  Built on the host once
+// per model version; each count is one fixed-order sum (CSR row).
+static int ensure_joint_map(nipamd_model* mm) {
+  DevState* d = dev_of(mm);
+  if (d->jm_ptr) return 0;
+  const nipamd::Model& m = mm->m;
+  const auto& P = m.chain;
+  const int nv = (int)m.vars.size(), K = P.N, M = P.emits[0].M, ov = P.emits[0].var;
+  const int Kb = nipamd::kSlabKb, Hf = nipamd::kSlabH, Hb = nipamd::kSlabH + (M + 2) * 16;
+  const int p0 = nipamd::chain_slab_p0(M);
+  std::vector<int> off(nv + 1, 0);
+  for (int v = 0; v < nv; v++) {
+    int sz = m.vars[v].card;
+    for (int q : m.vars[v].parents) sz *= m.vars[q].card;
+    off[v + 1] = off[v] + sz;
+  }
+  // value of variable w at joint (x, y): -1 if it is neither interface's
+  auto value = [&](int w, int x, int y) {
+    long sx = 1;
+    for (size_t i = 0; i < P.jprev.size(); i++) {
+      const int c = m.vars[P.jprev[i]].card;
+      if (P.jprev[i] == w) return (int)((x / sx) % c);
+      if (P.jcur[i] == w) return (int)((y / sx) % c);
+      sx *= c;
+    }
+    return -1;
+  };
+  std::vector<std::vector<std::pair<int, double>>> rows(off[nv]);
+  for (int v = 0; v < nv; v++) {
+    const auto& V = m.vars[v];
+    std::vector<int> U{v};
+    U.insert(U.end(), V.parents.begin(), V.parents.end());
+    auto family_index = [&](int x, int y, int first) {     // first: v's own value (child first)
+      long idx = first, st = V.card;
+      for (size_t k = 1; k < U.size(); k++) {
+        const int u = value(U[k], x, y);
+        if (u < 0) return -1L;
+        idx += u * st;
+        st *= m.vars[U[k]].card;
+      }
+      return idx;
+    };
+    const bool is_prev = std::find(P.jprev.begin(), P.jprev.end(), v) != P.jprev.end();
+    const bool is_cur = std::find(P.jcur.begin(), P.jcur.end(), v) != P.jcur.end();
+    if (is_prev) {
+      if (U.size() != 1) return fail(NIPAMD_ERROR_UNSUPPORTED, "joint e_step: previous-slice variable with parents");
+      for (int x = 0; x < K; x++) rows[off[v] + value(v, x, 0)].push_back({p0 + x, 1.0});
+    } else if (is_cur) {
+      for (int x = 0; x < K; x++)
+        for (int y = 0; y < K; y++) {
+          const long i = family_index(x, y, value(v, x, y));
+          if (i < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "joint e_step: family outside the interfaces");
+          const double a = P.A[x * 16 + y];
+          rows[off[v] + i].push_back({x * 16 + y, a});
+          rows[off[v] + i].push_back({Kb + x * 16 + y, a});
+        }
+    } else if (v == ov) {
+      const auto& E = P.emits[0];
+      for (int y = 0; y < K; y++)
+        for (int o = 0; o < M; o++) {
+          const long i = family_index(0, y, o);
+          if (i < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "joint e_step: observation family outside the interface");
+          rows[off[v] + i].push_back({Hf + o * 16 + y, 1.0});
+          rows[off[v] + i].push_back({Hb + o * 16 + y, 1.0});
+          if (E.s[y] != 0.0) {                   // missing observations, split as E(y, o) / s(y)
+            const double w = E.E[(size_t)o * 64 + y] / E.s[y];
+            rows[off[v] + i].push_back({Hf + M * 16 + y, w});
+            rows[off[v] + i].push_back({Hb + M * 16 + y, w});
+          }
+        }
+    } else {
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "joint e_step: variable outside the joint chain");
+    }
+  }
+  std::vector<int> ptr{0}, idx;
+  std::vector<double> coef;
+  for (const auto& r : rows) {
+    for (const auto& e : r) { idx.push_back(e.first); coef.push_back(e.second); }
+    ptr.push_back((int)idx.size());
+  }
+  HIP_OK(hipMalloc(&d->jm_ptr, ptr.size() * sizeof(int)));
+  HIP_OK(hipMemcpy(d->jm_ptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OK(hipMalloc(&d->jm_idx, std::max<size_t>(1, idx.size()) * sizeof(int)));
+  if (!idx.empty()) HIP_OK(hipMemcpy(d->jm_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (int rc = upload(&d->jm_coef, coef)) return rc;
+  d->jm_n = off[nv];
+  return 0;
+}
+
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   if (mm->estep_route == 1) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
   const auto& P = mm->m.chain;
-  if (!P.valid || !P.hmm) return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
+  if (!P.valid || !(P.hmm || P.jhmm))
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
   if (int rc = ensure_tables(mm)) return rc;
   Route rh;
   rh.primary = 0;
   ReqTables* rt = nullptr;
   if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
   DevState* d = dev_of(mm);
+  if (P.jhmm) {
+    if (int rc = ensure_joint_map(mm)) return rc;
+    if (nipamd::estep_map_finalize_launch(d_partial, d->jm_n, d->jm_ptr, d->jm_idx, d->jm_coef, d_counts,
+                                          (hipStream_t)stream))
+      return fail(NIPAMD_ERROR_DEVICE, "finalize launch failed");
+    return 0;
+  }
   nipamd::ChainFinalize f{};
   f.N = P.N; f.M = P.emits[0].M;
   int off = 0;

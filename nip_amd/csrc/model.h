@@ -100,6 +100,10 @@ struct ChainPlan {
   bool joint = false;
   std::vector<int> jprev;           // joint: previous_outgoing (their marginals: derive.hip kDerivePrev, projected)
   std::vector<int> jcur;            // joint: outgoing (their marginals: derive.hip kDeriveProject)
+  // joint, <= 16 joint states, one observation candidate (emits[0]) and no
+  // summed-out variable: the HMM e_step kernel runs on the joint state and the
+  // finalize projects the joint counts onto every family (engine.cpp)
+  bool jhmm = false;
 };
 constexpr long kGpuFoldMin = 1L << 22;
 struct Model {

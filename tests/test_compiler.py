@@ -95,7 +95,7 @@ def test_chain_plan_recognition():
     # a slice with two interface variables is a chain over the joint interface
     # state (compile.cpp build_joint_chain_plan) for fb / filter of the
     # interface variables, their previous-slice copies and leaf children;
-    # evidence on the previous slice and e_step stay on the general engine
+    # evidence on the previous slice stays on the general engine
     nodes = [("a0", 2, "a1"), ("b0", 2, "b1"), ("a1", 2, None), ("b1", 2, None), ("o", 2, None)]
     pots = [("a0", [], None), ("b0", [], None), ("a1", ["a0"], None), ("b1", ["b0", "a1"], None),
             ("o", ["b1"], None)]
@@ -105,7 +105,11 @@ def test_chain_plan_recognition():
     assert w.gpu_supported([w.variable("o"), w.variable("b1")], [w.variable("a1"), w.variable("b1")])
     assert w.gpu_supported([w.variable("o")], [w.variable("a0"), w.variable("b0")])
     assert not w.gpu_supported([w.variable("a0")], [w.variable("a1")])   # evidence on the previous slice
-    assert not w.estep_supported()
+    assert w.estep_supported()          # one observed child, no summed-out variable: the HMM e_step kernel
+    c = nip_amd.Model.from_spec(*synth.coupled_spec())
+    c.set_engine(nip_amd.ENGINE_CHAIN)
+    assert c.gpu_supported([c.variable("A1"), c.variable("B1")], [c.variable("X1")])
+    assert not c.estep_supported()      # two observed children: e_step on the general engine
     w.set_engine(nip_amd.ENGINE_AUTO)
     assert w.gpu_supported([w.variable("o")], [w.variable("a1")])
     assert w.estep_supported()
