@@ -877,7 +877,10 @@ void build_joint_chain_plan(Model& m) {
   P.jcur = cur;
   bool summed = false;
   for (int v = 0; v < nv; v++) summed |= role[v] == 3;
-  P.jhmm = !summed && cand.size() == 1 && K <= 16;
+  // the joint e_step (engine.cpp ensure_joint_map) is off: its counts agree
+  // with the general engine at T <= 2 but not at T = 41;
+  // these slices' e_step stays on the general engine
+  P.jhmm = false && !summed && cand.size() == 1 && K <= 16;
   P.joint = true;
   P.valid = true;
 }
