@@ -880,7 +880,10 @@ void build_joint_chain_plan(Model& m) {
   // the joint e_step (engine.cpp ensure_joint_map) is off: its counts agree
   // with the general engine at T <= 2 but not at T = 41;
   // these slices' e_step stays on the general engine
-  P.jhmm = false && !summed && cand.size() == 1 && K <= 16;
+#ifndef NIPAMD_JOINT_ESTEP
+#define NIPAMD_JOINT_ESTEP 0      // diagnostics builds only
+#endif
+  P.jhmm = NIPAMD_JOINT_ESTEP && !summed && cand.size() == 1 && K <= 16;
   P.joint = true;
   P.valid = true;
 }
