@@ -149,8 +149,8 @@ ESTEP_CASES = [
 ]
 
 
-@pytest.mark.skip(reason="joint e_step disabled: its counts match the general engine at T <= 2 but "
-                         "not at T = 41 (r02q, max abs diff 0.058); DESIGN.md 10")
+@pytest.mark.skip(reason="joint e_step route off: wrong with missing values across several blocks "
+                         "(B=23, T=41: 0.058 from the oracle; the general engine 1.3e-13); DESIGN.md 10")
 @pytest.mark.parametrize("name,spec,osym", ESTEP_CASES, ids=[c[0] for c in ESTEP_CASES])
 @pytest.mark.parametrize("T", [1, 2, 41])
 def test_joint_estep_equals_general_engine(name, spec, osym, T):
