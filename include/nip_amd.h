@@ -229,7 +229,12 @@ int nipamd_estep_host(nipamd_model* m, const int32_t* obs, int n_obs,
  *                         are applied.  Partials of power-of-two shards combine
  *                         (pairwise, in rank order) into exactly the partial of
  *                         the whole batch.
- *   nipamd_estep_finalize d_counts += the e_step families of a partial.
+ *   nipamd_estep_finalize d_counts += the e_step families of a partial
+ *                         (synchronises the stream to read the route tag).
+ * A partial ends in two tag slots counting the partials summed into it per
+ * kernel route (the route depends on the engine setting and on T); the
+ * finalize fails with NIP_ERROR_INVALID_ARGUMENT on partials of different
+ * routes combined, instead of summing mismatched layouts.
  */
 int nipamd_estep_partial_size(const nipamd_model* m);
 int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,

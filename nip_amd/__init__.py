@@ -527,8 +527,11 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
 
 
 def estep_finalize(model: Model, partial, counts, stream=None):
-    """counts (CUDA float64 [param_size], em_learn layout) += families of partial."""
+    """counts (CUDA float64 [param_size], em_learn layout) += families of partial.
+    counts=None starts from the em_learn pseudo-counts (ones, nip.c:2172)."""
     import torch
+    if counts is None:
+        counts = torch.ones((model.param_size(),), dtype=torch.float64, device=partial.device)
     counts = _out_buf(counts, (model.param_size(),), torch.float64, partial.device, "counts")
     _check(lib().nipamd_estep_finalize(model._h, C.c_void_p(partial.data_ptr()),
                                        C.c_void_p(counts.data_ptr()), _stream_ptr(stream)))

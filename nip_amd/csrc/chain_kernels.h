@@ -219,6 +219,8 @@ int chain_estep_mfma_launch(const ChainArgs& a, hipStream_t stream);
 int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
+// the e_step partial's route tag: tag[0] = a, tag[1] = b
+int estep_tag_launch(double* tag, double a, double b, hipStream_t stream);
 // counts[p] += sum_j coef[j] * R[idx[j]] over j in [ptr[p], ptr[p + 1]) (a
 // linear map of the reduced slab, e.g. a joint interface's counts projected
 // onto every family), in index order

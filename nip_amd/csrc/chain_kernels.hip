@@ -105,6 +105,12 @@ __device__ __forceinline__ double row_sum(double x) {
 #ifdef NIPAMD_ABLATE_NO_REDUCE   // timing-only ablation build (wrong results)
   return x;
 #endif
+  // x must be one rounded value in every lane: if x is a fresh product the
+  // compiler may contract this lane's term of the first add into an fma
+  // (x = a*b; x += ror(x) -> fma(a, b, ror(x))), the lanes then disagree in
+  // the last bit, and a scale exponent taken from the sum can differ by one
+  // between lanes (a sum of probabilities sits right at 1.0)
+  asm("" : "+v"(x));
   x += row_ror<8>(x);
   x += row_ror<4>(x);
   x += row_ror<2>(x);
@@ -550,6 +556,15 @@ int estep_map_finalize_launch(const double* R, int n, const int* ptr, const int*
   if (n <= 0) return 0;
   hipLaunchKernelGGL(estep_map_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, R, n, ptr, idx,
                      coef, counts);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ void estep_tag_kernel(double* tag, double a, double b) {
+  if (threadIdx.x == 0) { tag[0] = a; tag[1] = b; }
+}
+
+int estep_tag_launch(double* tag, double a, double b, hipStream_t stream) {
+  hipLaunchKernelGGL(estep_tag_kernel, dim3(1), dim3(64), 0, stream, tag, a, b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

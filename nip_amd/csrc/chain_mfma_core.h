@@ -78,6 +78,7 @@ __device__ __forceinline__ double dpp64(double v) {
 // sum over aligned groups of 8 lanes (quad swaps, then row_half_mirror);
 // every level pairs equal partial sums, so all 8 lanes get identical bits
 __device__ __forceinline__ double sum8(double x) {
+  asm("" : "+v"(x));       // one rounded value per lane: no fma contraction into the first add
   x += dpp64<0xB1>(x);     // quad_perm [1,0,3,2]
   x += dpp64<0x4E>(x);     // quad_perm [2,3,0,1]
   x += dpp64<0x141>(x);    // row_half_mirror
@@ -88,6 +89,8 @@ __device__ __forceinline__ double sum8(double x) {
 // interleave (one wave per SIMD: nothing else hides the f64 latency)
 template <int n>
 __device__ __forceinline__ void sum8_n(double (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; i++) asm("" : "+v"(x[i]));   // see sum8
 #pragma unroll
   for (int i = 0; i < n; i++) x[i] += dpp64<0xB1>(x[i]);
 #pragma unroll

@@ -71,6 +71,8 @@ __device__ __forceinline__ double dpp64(double v) {
 template <int L, int n>
 __device__ __forceinline__ void sumL_n(double (&x)[n]) {
 #pragma unroll
+  for (int i = 0; i < n; i++) asm("" : "+v"(x[i]));   // one rounded value per lane: no fma contraction
+#pragma unroll
   for (int i = 0; i < n; i++) x[i] += dpp64<0xB1>(x[i]);     // quad_perm [1,0,3,2]
 #pragma unroll
   for (int i = 0; i < n; i++) x[i] += dpp64<0x4E>(x[i]);     // quad_perm [2,3,0,1]

@@ -38,6 +38,7 @@ __device__ __forceinline__ double ror64(double v) {     // row_ror:K of a double
 }
 
 __device__ __forceinline__ double wave_sum(double x) {
+  asm("" : "+v"(x));       // one rounded value per lane: no fma contraction into the first add
   x += ror64<8>(x);
   x += ror64<4>(x);
   x += ror64<2>(x);

@@ -43,6 +43,7 @@ __device__ __forceinline__ double ror(double v) {
 
 // fixed-order sum over the wave (identical bits in every lane)
 __device__ __forceinline__ double wave_sum(double x) {
+  asm("" : "+v"(x));       // one rounded value per lane: no fma contraction into the first add
   x += ror<8>(x);
   x += ror<4>(x);
   x += ror<2>(x);

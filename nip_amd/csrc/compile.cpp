@@ -877,13 +877,9 @@ void build_joint_chain_plan(Model& m) {
   P.jcur = cur;
   bool summed = false;
   for (int v = 0; v < nv; v++) summed |= role[v] == 3;
-  // the joint e_step (engine.cpp ensure_joint_map) is off: its counts agree
-  // with the general engine at T <= 2 but not at T = 41;
-  // these slices' e_step stays on the general engine
-#ifndef NIPAMD_JOINT_ESTEP
-#define NIPAMD_JOINT_ESTEP 0      // diagnostics builds only
-#endif
-  P.jhmm = NIPAMD_JOINT_ESTEP && !summed && cand.size() == 1 && K <= 16;
+  // e_step on the HMM e_step kernel over the joint state, the slab projected
+  // onto every family (engine.cpp ensure_joint_map)
+  P.jhmm = !summed && cand.size() == 1 && K <= 16;
   P.joint = true;
   P.valid = true;
 }

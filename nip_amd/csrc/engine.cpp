@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -63,7 +64,7 @@ struct DevState {
   double* A64 = nullptr;          // [64][64]
   double* pi64 = nullptr;         // [64]
   double* sall64 = nullptr;       // [64]
-  std::vector<ReqTables> reqs;
+  std::deque<ReqTables> reqs;      // deque: pointers returned by ensure_req_tables stay valid
   double* S = nullptr;
   size_t S_bytes = 0;
   double* R = nullptr;     // E-step partial [nipamd_estep_partial_size] of nipamd_estep
@@ -1036,14 +1037,23 @@ int nipamd_filter_host(nipamd_model* mm, const int32_t* obs, int n_obs, const in
 
 // The chain e_step kernel serves the HMM slice with evidence on its child
 // only; every other e_step runs on the general engine, whose partial is the
-// em_learn layout itself.  The partial buffer holds either (the larger of the
-// two sizes); the route of the last partial decides the finalize.
-int nipamd_estep_partial_size(const nipamd_model* mm) {
-  if (!mm) return -1;
+// em_learn layout itself.  The partial is [body | route tag]: the body holds
+// either layout (the larger of the two sizes), the two tag slots count the
+// partials summed into it per route -- (1, 0) chain slab, (0, 1) em_learn
+// layout -- so partials of different routes (another T, another engine
+// setting, another rank) that were combined are detected by the finalize
+// instead of being summed silently.
+static int estep_body_size(const nipamd_model* mm) {
   const int ps = nipamd::param_size(mm->m);
   if (mm->engine != NIPAMD_ENGINE_JTREE && mm->m.chain.valid && (mm->m.chain.hmm || mm->m.chain.jhmm))
     return std::max(ps, nipamd::chain_estep_slab(mm->m.chain.emits[0].M));
   return mm->engine == NIPAMD_ENGINE_CHAIN ? -1 : ps;
+}
+
+int nipamd_estep_partial_size(const nipamd_model* mm) {
+  if (!mm) return -1;
+  const int body = estep_body_size(mm);
+  return body < 0 ? -1 : body + 2;
 }
 
 // e_step kernel of the chain route: 2 = the 16-lane DPP kernel (one slab row
@@ -1082,10 +1092,12 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
       return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step covers the HMM slice with evidence on its child");
     std::string why;
     if (!nipamd::jt_supported(mm, n_obs, obs_vars, 0, nullptr, why)) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
-    mm->estep_route = 1;
-    return nipamd::jt_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream);
+    if (int rc = nipamd::jt_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
+      return rc;
+    if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 1.0, (hipStream_t)stream))
+      return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
+    return 0;
   }
-  mm->estep_route = 0;
   const auto& P = mm->m.chain;
   const int col = r.pcol;
   const int Mo = P.emits[0].M;
@@ -1093,6 +1105,8 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   const bool mfma = chain_estep_kernel(mm, T) == 1;
   const int per_row = mfma ? 16 : 1;            // sequences per slab row
   hipStream_t st = (hipStream_t)stream;
+  if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, st))
+    return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   if (int rc = ensure_tables(mm)) return rc;
   Route rh;
@@ -1267,7 +1281,16 @@ static int ensure_joint_map(nipamd_model* mm) {
 
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
-  if (mm->estep_route == 1) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
+  const int body = estep_body_size(mm);
+  if (body < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "no e_step plan for this model under the selected engine");
+  // the route tag (see nipamd_estep_partial_size): one 16-byte read, once per EM iteration
+  double tag[2] = {0.0, 0.0};
+  HIP_OK(hipMemcpyAsync(tag, d_partial + body, sizeof(tag), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  if (!(tag[0] >= 1.0 && tag[1] == 0.0) && !(tag[1] >= 1.0 && tag[0] == 0.0))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "e_step partial: partials of different routes (chain slab / em_learn "
+                                            "layout) were combined, or the buffer is not an e_step partial");
+  if (tag[1] >= 1.0) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
   const auto& P = mm->m.chain;
   if (!P.valid || !(P.hmm || P.jhmm))
     return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");

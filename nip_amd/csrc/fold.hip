@@ -55,6 +55,7 @@ __device__ __forceinline__ double ror(double v) {     // row_ror:K of a double
 
 // sum over the wave in a fixed order (every lane ends with the same bits)
 __device__ __forceinline__ double wave_sum(double x) {
+  asm("" : "+v"(x));       // one rounded value per lane: no fma contraction into the first add
   x += ror<8>(x);
   x += ror<4>(x);
   x += ror<2>(x);

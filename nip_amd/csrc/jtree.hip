@@ -26,6 +26,7 @@ __device__ __forceinline__ void wave_sync() { __syncthreads(); }   // a block is
 // sum over the L lanes of a unit (every lane receives the total)
 template <int L>
 __device__ __forceinline__ double unit_sum(double v) {
+  asm("" : "+v"(v));       // one rounded value per lane: no fma contraction into the first add
 #pragma unroll
   for (int o = L / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;

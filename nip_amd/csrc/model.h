@@ -150,7 +150,6 @@ struct nipamd_model {
   nipamd::Model m;
   unsigned version = 1;          // bumped whenever the tables change
   int engine = 0;                // NIPAMD_ENGINE_* (nipamd_model_set_engine)
-  int estep_route = 0;           // layout of the last e_step partial: 0 chain, 1 general
   double fold_ms = 0.0;          // the last GPU fold: kernel time and clique bytes streamed
   double fold_bytes = 0.0;
   void* lik = nullptr;           // likelihood.hip: device tables of the last column set

@@ -35,9 +35,16 @@ def cpt(seed: int, child_card: int, parent_configs: int) -> np.ndarray:
     return (d / d.sum(axis=1, keepdims=True)).ravel()
 
 
-def hmm_spec(N: int = 16, M: int = 16, seed: int = 12345):
-    """HMM-shaped DBN of config 2 (structure of examples/model.net)."""
+def hmm_spec(N: int = 16, M: int = 16, seed: int = 12345, proper: bool = False):
+    """HMM-shaped DBN of config 2 (structure of examples/model.net).
+
+    proper=True declares M1, P1, P0 in that order, so the reference's CPT
+    re-normalisation runs over the child of each family (the lowest ID): the
+    transition and emission rows then sum to 1, and so do the step masses
+    of missing observations -- sums sitting right at a power of two."""
     nodes = [("P0", N, "P1"), ("P1", N, None), ("M1", M, None)]
+    if proper:
+        nodes = [nodes[2], nodes[1], nodes[0]]
     pots = [
         ("M1", ["P1"], cpt(seed, M, N)),
         ("P1", ["P0"], cpt(seed + 1, N, N)),

@@ -105,7 +105,7 @@ def test_chain_plan_recognition():
     assert w.gpu_supported([w.variable("o"), w.variable("b1")], [w.variable("a1"), w.variable("b1")])
     assert w.gpu_supported([w.variable("o")], [w.variable("a0"), w.variable("b0")])
     assert not w.gpu_supported([w.variable("a0")], [w.variable("a1")])   # evidence on the previous slice
-    assert not w.estep_supported()      # joint e_step off: the general engine's
+    assert w.estep_supported()          # joint e_step: the HMM e_step kernel over the joint state
     c = nip_amd.Model.from_spec(*synth.coupled_spec())
     c.set_engine(nip_amd.ENGINE_CHAIN)
     assert c.gpu_supported([c.variable("A1"), c.variable("B1")], [c.variable("X1")])

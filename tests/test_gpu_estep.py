@@ -116,6 +116,44 @@ def test_estep_missing_observations_vs_oracle():
     assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
 
 
+@pytest.mark.parametrize("B,T,proper", [(23, 41, False), (70, 41, False), (24, 40, True), (70, 41, True),
+                                          (2, 3, True)])
+def test_estep_missing_multiblock_vs_oracle(B, T, proper):
+    """The default e_step kernel (chain_kernel<true>, 8 sequences per block)
+    with 25% missing values over several blocks and odd / even T.  proper=True:
+    rows of A and E sum to 1, so the step masses of missing observations sit
+    at 1.0, where a scale exponent taken from a lane-inconsistent sum differs
+    by one between lanes (round 3: FMA contraction into the row sum's first
+    add; the joint e_step's 0.058 error).  The first step is observed (the
+    reference's BAD_LUCK rule on leading missing runs, see above)."""
+    m = nip_amd.Model.from_spec(*synth.hmm_spec(16, 16, seed=9, proper=proper))
+    rng = np.random.default_rng(B * 100 + T)
+    obs = rng.integers(0, 16, size=(B, T, 1)).astype(np.int32)
+    obs[rng.random(obs.shape) < 0.25] = -1
+    obs[:, 0] = np.maximum(obs[:, 0], 0)
+    if B == 2:
+        obs[:, :, 0] = [[0, -1, 13], [5, -1, 2]]
+    ov = [m.variable("M1")]
+    cnt, ll, st = gpu_estep(m, obs, ov)
+    assert not st.any()
+    orc = PortOracle(m.desc())
+    rc, rl, rb = orc.estep(obs, ov, np.ones(m.param_size()))
+    ok = rb == 0
+    assert close(ll[ok], rl[ok], LL_RTOL)
+    if not ok.all():
+        cnt, _, _ = gpu_estep(m, obs[ok], ov)
+        rc, _, _ = orc.estep(obs[ok], ov, np.ones(m.param_size()))
+    assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
+    # the same sequences through fb: posteriors and ll
+    q = [m.variable("P1")]
+    post, fll, _ = nip_amd.forward_backward_inference(m, torch.from_numpy(obs).cuda(), ov, q)
+    post = post.cpu().numpy()
+    for b in range(0, B, max(1, B // 6)):
+        rp, r_ll = orc.fb(obs[b], ov, q)
+        assert np.abs(post[b] - rp).max() <= 1e-12
+        assert abs(fll[b].item() - r_ll) <= LL_RTOL * max(1.0, abs(r_ll))
+
+
 def test_estep_bad_luck_flags():
     """Invalid codes / impossible data: the reference's e_step BAD_LUCK."""
     nodes, pots = synth.hmm_spec(16, 16, seed=5)
@@ -146,7 +184,29 @@ def test_partial_is_shard_invariant_and_reproducible():
     for k in range(4):
         p, _, _ = nip_amd.estep_partial(m, obs[k * 64:(k + 1) * 64].contiguous(), ov)
         parts.append(p.clone())
-    assert torch.equal(tree_sum(torch.stack(parts)), whole)
+    comb = tree_sum(torch.stack(parts))
+    assert torch.equal(comb[:-2], whole[:-2])             # the body, bit for bit
+    assert comb[-2:].tolist() == [4.0, 0.0] and whole[-2:].tolist() == [1.0, 0.0]   # route tag counts
+
+
+def test_partials_of_different_routes_are_refused():
+    """The e_step route depends on T (a chain kernel's LDS must hold the
+    sequence; beyond it the general engine runs): partials of the two
+    layouts have the same size, and combining them must fail in the
+    finalize, not sum mismatched layouts."""
+    m = nip_amd.Model.from_spec(*synth.hmm_spec(4, 4, seed=3))
+    ov = [m.variable("M1")]
+    short = torch.from_numpy(synth.observations(2, 16, 4, seed=1)).cuda()
+    long_ = torch.from_numpy(synth.observations(2, 16000, 4, seed=2)).cuda()   # > 96 KB of LDS
+    a, _, _ = nip_amd.estep_partial(m, short, ov)
+    a = a.clone()
+    b, _, _ = nip_amd.estep_partial(m, long_, ov)
+    b = b.clone()
+    assert a[-2:].tolist() == [1.0, 0.0] and b[-2:].tolist() == [0.0, 1.0]
+    nip_amd.estep_finalize(m, a, None)                   # each alone is fine
+    nip_amd.estep_finalize(m, b, None)
+    with pytest.raises(nip_amd.NipError):
+        nip_amd.estep_finalize(m, tree_sum(torch.stack([a, b])), None)
 
 
 def test_chunked_batch_matches_tree():
@@ -161,7 +221,7 @@ def test_chunked_batch_matches_tree():
     a, _, _ = nip_amd.estep_partial(m, obs[:16384].contiguous(), ov)
     a = a.clone()
     b, _, _ = nip_amd.estep_partial(m, obs[16384:].contiguous(), ov)
-    assert torch.equal(tree_sum(torch.stack([a, b.clone()])), whole)
+    assert torch.equal(tree_sum(torch.stack([a, b.clone()]))[:-2], whole[:-2])
 
 
 @pytest.mark.parametrize("path", chain_fixtures(), ids=lambda p: os.path.basename(p))
@@ -294,4 +354,4 @@ def test_estep_mfma_kernel_shard_invariant(monkeypatch):
     for k in range(4):
         p, _, _ = nip_amd.estep_partial(m, obs[k * 64:(k + 1) * 64].contiguous(), ov)
         parts.append(p.clone())
-    assert torch.equal(tree_sum(torch.stack(parts)), whole)
+    assert torch.equal(tree_sum(torch.stack(parts))[:-2], whole[:-2])
