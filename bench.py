@@ -4,9 +4,13 @@
 One "step" = one pass of the hot path (nipamd_fb: forward_backward_inference,
 src/nip.c:1320, batched) over one batch of B synthetic sequences x T time
 slices resident in HBM -- SURVEY 8(d) config 2: HMM-shaped DBN with 16 hidden
-and 16 observed states, B = 4096 sequences per GPU, T = 1024.
+and 16 observed states, B = 4096 sequences per GPU, T = 1024.  The same JSON
+line carries a `secondary` object with SURVEY 8(d)'s other GPU configs timed
+the same way in the same run: config 3 (demo1 @ 32 states, 65536 x 256),
+config 4 (one em_learn iteration over the 131072 x 1024 per-GPU shard) and
+config 5 (the 64^4 wide clique, 256 x 128).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--no-secondary]
 
 N > 1: one process per GPU.  Run directly with --gpus N, bench.py starts
 ``python -m torch.distributed.run --nproc-per-node N`` on itself as a child
@@ -16,13 +20,27 @@ workloads shard sequences with no data-path collective (RCCL only for the
 barrier and the max-over-ranks timing, "scaling": "weak"); the em workload
  exchanges one packed all-gather per EM iteration.
 Rank 0 prints one JSON line.
+
+Roofline accounting:
+  roofline.achieved   the bytes the dominant kernel's algorithm moves per
+                      sequence-timestep (`bytes_per_unit`, e.g. 196 B for the
+                      checkpoint kernel: obs + checkpoints written and read +
+                      posterior) x units / kernel time (HIP events on the launch
+                      stream) -- never bytes the kernel does not move
+  roofline.primary    SURVEY 8(d)'s per-unit figure (392 B at config 2, with
+                      the alpha/beta round trip) at the same time: a like-for-
+                      like comparison across kernels, NOT delivered bandwidth
+  roofline.latency    the second roof: the filters' dependency chain, T steps
+                      of the measured minimal step (profiles/r03/r03_mb_lat.txt)
+                      per block round, against the kernel time
+  roofline.traffic    HBM bytes per step from the committed rocprofv3 PMC pass
+                      (profiles/pmc_traffic.json, gfx950 FETCH_SIZE x2)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import platform
 import socket
 import subprocess
 import sys
@@ -37,47 +55,60 @@ from nip_amd import synth  # noqa: E402  (numpy only; the HIP library loads on f
 
 METRIC = "sequence-timesteps/s fwd-bwd smoothing, 16-state DBN; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0            # MI355X spec (MI355X_MICROARCH.md chip table)
+N_CU = 256
+# Dependency-chain floors of the matrix-core filters, measured by
+# profiles/r03/mb_lat.hip (one wave per CU, s_memtime cycles; r03_mb_lat.txt):
+# kernel -> (cycles per filter step, sequences per block, blocks resident per CU)
+LATENCY_STEP = {
+    "chain_fb_ckpt_kernel": (328.0, 16, 1),            # 4 chained v_mfma_f64_16x16x4, D -> next B
+    "chain_fb_mfma_kernel": (328.0, 16, 1),
+    "chain_mfma_wide_kernel<1>": (328.0, 16, 1),
+    "chain_mfma_wide_kernel<2>": (1136.1, 16, 1),      # 2 x 8 chained, interleaved (93 KB LDS: 1 block/CU)
+}
+CLOCK_GHZ = 2.39                 # in-kernel clock under the chain loop (s_memtime / s_memrealtime, r03_mb_lat.txt)
+
+# SURVEY 8(d)'s primary per-unit figures (HBM bytes per sequence-timestep)
+PRIMARY_BYTES = {"config2": 392, "config3": 784, "config4": 264, "config5": 1544}
 
 
-def algorithmic_bytes_per_seq_step(N: int, n_obs: int = 1, posterior: bool = True) -> int:
-    """What the path must move per sequence-timestep:
-    the int32 observations read once (4 B per observed variable), one N-wide
-    fp64 interface message written and read back (alpha for t < T/2, beta for
-    t >= T/2: 2 x 8N B), the N-wide fp64 posterior written (8N B, fb only)."""
-    return 4 * n_obs + 2 * 8 * N + (8 * N if posterior else 0)
+def kernel_bytes(kname: str, N: int, n_obs: int, posterior: bool):
+    """Bytes per sequence-timestep the dominant kernel's algorithm moves in HBM,
+    and the breakdown."""
+    if kname == "chain_fb_ckpt_kernel":
+        ck = 8 * N // 4
+        return (4 * n_obs + 2 * ck + 8 * N,
+                "obs %d + every 4th interface message as a checkpoint (%d written + %d read) + posterior %d"
+                % (4 * n_obs, ck, ck, 8 * N))
+    post = 8 * N if posterior else 0
+    return (4 * n_obs + 16 * N + post,
+            "obs %d + interface message written and read back (%d + %d)%s"
+            % (4 * n_obs, 8 * N, 8 * N, " + posterior %d" % post if post else " (counts stay on chip)"))
 
 
-# name -> (SURVEY 8(d) config, spec builder, observed vars, query var, default B, T)
+# name -> (SURVEY 8(d) config, spec builder, observed vars, query var, default B, T, default steps)
 WORKLOADS = {
-    "fb": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 4096, 1024),
-    "estep": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024),
-    "config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256),
-    "config5": ("config5", lambda a: synth.wide_spec(64, 16), ["O1"], "X1", 256, 128),
-    "generate": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 65536, 1024),
-    "em": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024),
+    "fb": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 4096, 1024, 20),
+    "estep": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024, 5),
+    "config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256, 10),
+    "config5": ("config5", lambda a: synth.wide_spec(64, 16), ["O1"], "X1", 256, 128, 20),
+    "generate": ("config2", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 65536, 1024, 20),
+    "em": ("config4", lambda a: synth.hmm_spec(a.N, a.M), ["M1"], "P1", 131072, 1024, 5),
     # the general join-tree engine (not a BASELINE config): a factorial HMM,
     # two 4-state chains with one 16-state observation of both (interface {X1, Y1})
-    "jtree": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024),
+    "jtree": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024, 5),
     # the same slice as a joint-interface chain (16 joint states) on the
     # matrix-core chain kernels -- what the automatic engine choice runs
-    "joint": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024),
+    "joint": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024, 20),
 }
+# the default line: the headline, then these under "secondary" (SURVEY 8(d) configs 3-5)
+SECONDARY = ["config3", "em", "config5"]
 
 
 def host_info():
     """CPU model and the cores the baseline may use (the GPU box grants 16
     per GPU: OMP_NUM_THREADS; os.cpu_count() shows the whole machine)."""
-    model = platform.processor() or "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    return model, cores, os.cpu_count()
+    return cores
 
 
 def free_port():
@@ -105,6 +136,312 @@ def launch_or_check(args, argv):
     return world
 
 
+def cpu_baselines(workloads, budget):
+    """The reference's own code (and the C port) on the host's granted cores,
+    one process per core (oracle/cpu_bench.py), run as a child process
+    before this process touches the GPU.  -> {workload: record}."""
+    cmap = {"fb": "fb", "config3": "config3", "em": "em", "estep": "em", "config5": "config5"}
+    wl = [cmap[w] for w in workloads if w in cmap]
+    if not wl:
+        return {}
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_bench.py"), "--procs", str(host_info()),
+           "--budget", str(budget), *wl]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    except Exception as e:
+        return {w: {"error": str(e)[:200]} for w in workloads}
+    got = {}
+    for line in r.stdout.splitlines():
+        if line.startswith("{"):
+            d = json.loads(line)
+            got[d["workload"]] = d
+    out = {}
+    for w in workloads:
+        d = got.get(cmap.get(w))
+        if d is None:
+            out[w] = {"error": "no baseline: " + r.stderr[-300:]}
+            continue
+        ref, port = d.get("reference"), d.get("port")
+        rec = dict(ref if ref else (port or {}))
+        if not rec:
+            out[w] = {"error": d.get("error", "no baseline")}
+            continue
+        rec["cpu_model"], rec["host_cpus"] = d["cpu_model"], d["host_cpus"]
+        if ref and port:
+            rec["port"] = {k: port[k] for k in ("value", "cores", "kind", "sample")}
+            rec["r_port_over_ref"] = port["value"] / ref["value"]
+        if not ref:
+            rec["note"] = "the reference build (oracle/_ref) is absent: the C port is the baseline"
+        out[w] = rec
+    return out
+
+
+def load_traffic(workload: str):
+    """HBM bytes per step from the committed rocprofv3 PMC pass (profiles/)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")   # profiles/summarize.py
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get("entries", {}).get(workload)
+        if e:
+            return e.get("hbm_bytes_per_step", e.get("hbm_bytes_per_launch"))
+    except Exception:
+        pass
+    return None
+
+
+def run_workload(name, args, world, rank, dev, steps, warmup):
+    """Time `steps` steps of one workload (barrier + synchronize on both sides,
+    max over ranks) and build its record."""
+    import torch
+    import torch.distributed as dist
+    import nip_amd
+
+    cfg, spec, ov_names, q_name, B0, T0, _ = WORKLOADS[name]
+    headline = name == args.workload
+    B = (args.batch if headline and args.batch else B0)
+    T = (args.T if headline and args.T else T0)
+    nodes, pots = spec(args)
+    model = nip_amd.Model.from_spec(nodes, pots)
+    ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
+    if name == "jtree":
+        model.set_engine(nip_amd.ENGINE_JTREE)     # the joint-interface chain would take it otherwise
+    N, M = model.card(q), model.card(ov[0])
+    obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
+                             for i, v in enumerate(ov)], axis=2)
+    obs = torch.from_numpy(obs_np).to(dev)
+    ll = torch.empty((B,), dtype=torch.float64, device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+    em_state = None
+    if name == "generate":
+        sample = torch.empty((B, T, model.num_vars), dtype=torch.int32, device=dev)
+        st.zero_()
+        ll.zero_()
+
+        def step():
+            nip_amd.generate_data(model, 12345 + rank, B, T, sample)
+    elif name == "em":
+        from nip_amd import em as nem
+        group = dist.group.WORLD if world > 1 else None
+        em_state = {"params": synth.uniform01(2024, model.param_size()) + 0.05, "ll": [], "exchange_ms": []}
+
+        def step():
+            tm = {}
+            p, l, bad = nem.iteration(model, em_state["params"], obs, ov, group, timing=tm)
+            if bad:
+                raise SystemExit("bench: e_step BAD_LUCK on synthetic data")
+            em_state["params"] = p
+            em_state["ll"].append(l)
+            em_state["exchange_ms"].append(tm.get("exchange_ms", 0.0))
+    elif name != "estep":
+        post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
+
+        def step():
+            nip_amd.forward_backward_inference(model, obs, ov, [q], post, ll, st)
+    else:
+        counts = torch.ones((model.param_size(),), dtype=torch.float64, device=dev)
+
+        def step():
+            nip_amd.e_step(model, obs, ov, counts, ll, st)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[dev.index])
+        torch.cuda.synchronize()
+
+    for _ in range(warmup):
+        step()
+    barrier()
+    kname = nip_amd.last_kernel()       # the kernel the engine chose for this request
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        step()
+        evs[i][1].record()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    if name == "em":
+        ll.zero_()
+        st.zero_()
+    if not args.no_check and (not bool(torch.isfinite(ll).all()) or int(st.abs().sum()) != 0):
+        raise SystemExit("bench: non-finite log-likelihood / zero-mass status on synthetic data (%s)" % name)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    units = B * T * steps * world
+    value = units / elapsed
+    posterior = name not in ("estep", "em")
+    bpu, bnote = kernel_bytes(kname, N, len(ov), posterior)
+    metric = METRIC
+    extra = {}
+    if name == "fb":
+        workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (N, M, B, T)
+    elif name == "estep":
+        workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
+            N, M, B, T)
+        metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
+        kname += " + tree64 + finalize"
+    elif name == "em":
+        kname += " + tree64 + finalize"
+        workload = ("config4: em_learn iterations of HMM-shaped DBN, %d hidden x %d observed, "
+                    "B=%d seq/GPU x T=%d, %d GPU(s), one packed RCCL all-gather per iteration" % (
+                        N, M, B, T, world))
+        metric = "sequence-timesteps/s em_learn (E-step + exchange + M-step per iteration), 16-state DBN"
+        P = model.partial_size()
+        extra["em"] = {"iterations_timed": steps, "ll_per_iteration": em_state["ll"][-steps:],
+                       "exchange_ms_median": float(np.median(em_state["exchange_ms"][-steps:])),
+                       "exchange_bytes_per_rank": 8 * (P + 2),
+                       "note": "kernel_ms is the whole iteration on the launch stream (e_step kernels over "
+                               "8 launches of 16384 sequences, exchange, finalize, host m_step); the "
+                               "exchange packs the e_step partial (%d doubles incl. its 2-slot route tag), "
+                               "the ll tree sum and the failure count" % P}
+    elif name == "generate":
+        bpu, bnote = 4 * model.num_vars, "the int32 draws written; the tables stay in cache"
+        workload = "generate_data: HMM-shaped DBN, %d hidden x %d observed states, B=%d series/GPU x T=%d" % (
+            N, M, B, T)
+        metric = "sequence-timesteps/s generate_data (sampling), 16-state DBN"
+    elif name == "jtree":
+        bpu, bnote = 4 + 8 * N, "the request's I/O only: the engine is latency-bound (DESIGN.md 4)"
+        workload = ("general join-tree engine: factorial HMM, X and Y 4 states each, O1 16 states of both, "
+                    "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
+        metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
+    elif name == "joint":
+        K = 16                         # joint interface states (X1, Y1)
+        kb, _ = kernel_bytes(kname, K, len(ov), True)
+        bpu, bnote = kb + 8 * K + 8 * N, ("the chain kernel's bytes at K = 16 joint states, then the "
+                                          "projection: the joint posterior read back, X1's marginal written")
+        kname += " + project_kernel"
+        workload = ("joint-interface chain: factorial HMM, X and Y 4 states each, O1 16 states of both, "
+                    "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
+        metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (joint-interface chain kernels)"
+    elif name == "config3":
+        workload = "config3: demo1.net structure, 5 vars x 32 states, A1 B1 observed, C1 posterior, " \
+                   "B=%d seq/GPU x T=%d" % (B, T)
+        metric = "sequence-timesteps/s fwd-bwd smoothing, demo1 @ 32 states"
+    else:
+        workload = "config5: wide clique {X0,Y1,Z1,X1} 64^4 entries, O1 16 states observed, X1 posterior, " \
+                   "B=%d seq/GPU x T=%d" % (B, T)
+        metric = "sequence-timesteps/s fwd-bwd smoothing, wide-clique DBN (64^4 in-clique)"
+    achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(workload), "kernel": kname,
+            "kernel_ms": kern_ms, "bytes_per_unit": bpu, "bytes_note": bnote}
+    if cfg in PRIMARY_BYTES and name in ("fb", "config3", "em", "estep", "config5"):
+        pb = PRIMARY_BYTES[cfg]
+        rate = pb * B * T / (kern_ms * 1e-3) / 1e9
+        roof["primary"] = {"bytes_per_unit": pb, "equivalent_gbs": rate, "frac": rate / HBM_PEAK_GBS,
+                           "note": "SURVEY 8(d)'s per-unit figure at this kernel time: a like-for-like "
+                                   "comparison, not bandwidth the chip delivered"}
+    base = kname.split(" + ")[0]
+    if base in LATENCY_STEP:
+        cyc, spb, bpc = LATENCY_STEP[base]
+        rounds = -(-((B + spb - 1) // spb) // (N_CU * bpc))
+        floor_ms = rounds * T * cyc / (CLOCK_GHZ * 1e9) * 1e3
+        roof["latency"] = {"bound": "filter dependency chain", "cycles_per_step": cyc, "steps": T,
+                           "block_rounds": rounds, "clock_ghz": CLOCK_GHZ, "floor_ms": floor_ms,
+                           "frac": floor_ms / kern_ms,
+                           "source": "profiles/r03/r03_mb_lat.txt (mb_lat.hip: the step's MFMA chain alone)"}
+    rec = {"metric": metric, "value": value, "unit": "sequence-timesteps/s", "n_gpus": world,
+           "steps": steps, "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic",
+           "config": {"workload": workload, "B_per_gpu": B, "T": T, "hidden_states": N,
+                      "observed_states": M, "observed_vars": len(ov), "parallelism": "dp%d" % world},
+           "roofline": roof}
+    rec.update(extra)
+    if rank == 0 and world == 1 and name in ("fb", "config3", "config5") and headline:
+        # PCIe-inclusive figure (DESIGN.md 8): the same batch from host buffers
+        # through nipamd_fb_host (H2D obs, kernels, D2H posteriors)
+        host_obs = np.ascontiguousarray(obs_np)
+        nip_amd.forward_backward_inference_host(model, host_obs, ov, [q])
+        t1 = time.perf_counter()
+        nip_amd.forward_backward_inference_host(model, host_obs, ov, [q])
+        el1 = time.perf_counter() - t1
+        rec["pcie_inclusive"] = {"value": B * T / el1, "unit": "sequence-timesteps/s", "ms": el1 * 1e3,
+                                 "note": "host buffers in and out (pageable), one call; not the headline"}
+    if name == "config5":
+        # the in-clique marginalisation: 64^4 entries summed over the hidden
+        # parents on the GPU (fold.hip), once per model version
+        fms, fby = [], 0.0
+        for _ in range(5):
+            _, ms_f, fby = model.fold()
+            fms.append(ms_f)
+        fk = float(np.median(fms))
+        rec["fold"] = {"kernel": "fold_lane_kernel + fold_sum_kernel", "kernel_ms": fk, "bytes": fby,
+                       "roofline": {"bound": "hbm", "achieved": fby / (fk * 1e-3) / 1e9,
+                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": fby / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                       "note": "A[x][y] = sum over Y1, Z1 of the 134 MB clique x priors, per model version"}
+    del obs, ll, st
+    torch.cuda.empty_cache()
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=0, help="timed steps of the headline (0: the workload's)")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=0, help="sequences per GPU (0: the workload's)")
+    ap.add_argument("--T", type=int, default=0, help="time slices (0: the workload's)")
+    ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb",
+                    help="fb: the headline metric (config 2 smoothing) plus the secondary configs; "
+                         "estep: one batched e_step (config 4 per-GPU shard); em: config 4, one step = "
+                         "one em_learn iteration (m_step, e_step of the shard, the packed all-gather "
+                         "over RCCL, finalize); config3: demo1 @ 32 states smoothing; config5: wide-"
+                         "clique smoothing; jtree: a factorial HMM on the general join-tree engine; "
+                         "joint: the same slice as a joint-interface chain; generate: generate_data")
+    ap.add_argument("--no-secondary", action="store_true", help="the headline workload only")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline")
+    ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
+    args = ap.parse_args()
+    world = launch_or_check(args, sys.argv[1:])
+    rank = int(os.environ.get("RANK", "0"))
+    secondary = [] if (args.no_secondary or args.workload != "fb" or args.batch or args.T) else SECONDARY
+
+    # CPU baselines first, in a child process, while nothing here has touched the GPU
+    cpu = {}
+    if world == 1 and rank == 0 and not args.no_cpu_baseline and args.workload != "generate":
+        cpu = cpu_baselines([args.workload] + secondary, args.cpu_budget)
+
+    import torch
+    import torch.distributed as dist
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    steps = args.steps or WORKLOADS[args.workload][6]
+    rec = run_workload(args.workload, args, world, rank, dev, steps, args.warmup)
+    if args.workload in cpu:
+        rec["cpu_baseline"] = cpu[args.workload]
+    if world == 1 and rank == 0 and not args.no_cpu_baseline and args.workload == "generate":
+        rec["cpu_baseline"] = cpu_baseline_generate(*WORKLOADS["generate"][1](args), T=rec["config"]["T"])
+    if secondary:
+        sec = {}
+        for w in secondary:
+            r = run_workload(w, args, world, rank, dev, WORKLOADS[w][6], 2 if w != "em" else 1)
+            if w in cpu:
+                r["cpu_baseline"] = cpu[w]
+            sec[WORKLOADS[w][0]] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "config",
+                                                      "roofline", "cpu_baseline", "em", "fold") if k in r}
+        rec["secondary"] = sec
+    if rank == 0:
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def cpu_baseline_generate(nodes, pots, T, budget_s: float = 12.0):
     """The reference's generate_data (oracle/_ref harness: nip.c's sampling
     loop over the reference's own join-tree code) on this host, one core,
@@ -123,293 +460,6 @@ def cpu_baseline_generate(nodes, pots, T, budget_s: float = 12.0):
             "sample": "%d series x T=%d, generate_data (nip.c:2325-2478 loop over the reference's "
                       "nippotential/nipjointree code compiled from /root/reference sources), gcc -O2, "
                       "%.1f s" % (n, T, el)}
-
-
-def cpu_baseline(nodes, pots, obs, ov, q, budget_s: float = 12.0, t_sample: int = 0):
-    """Reference-equivalent CPU path on this host over a bounded sample of the
-    bench workload: the C restatement of forward_backward_inference
-    (oracle/nip_oracle.c, bit-identical to the reference's own code on every
-    golden case) with OpenMP over sequences on all granted cores, one
-    sequence per thread.  Where oracle/_ref exists (built in
-    the build container), the reference's own compiled code is also timed
-    on one core and r = port/ref per-core throughput is reported.  ov / q
-    are variable indices in declaration order; t_sample > 0 times only the
-    first t_sample slices of each sequence (config 5's 16.7M-entry clique)."""
-    from oracle import bind
-    import nip_amd
-    cpu, cores, ncpu = host_info()
-    T = t_sample or obs.shape[1]
-    orc = bind.PortOracle(nip_amd.Model.from_spec(nodes, pots).desc())
-    # size the sample: one sequence on one thread first
-    t0 = time.perf_counter()
-    orc.fb(obs[0][:T], ov, [q])
-    one = max(time.perf_counter() - t0, 1e-6)
-    n = int(max(cores, min(obs.shape[0], budget_s / one * cores)))
-    n = max(cores, (n // cores) * cores)
-    sample = np.ascontiguousarray(obs[:n, :T])
-    t0 = time.perf_counter()
-    orc.fb_batch(sample, ov, [q], nthreads=cores)
-    el = time.perf_counter() - t0
-    rec = {"value": n * T / el, "unit": "sequence-timesteps/s", "cores": cores, "kind": "port",
-           "cpu_model": cpu, "host_cpus": ncpu,
-           "sample": "%d sequences x T=%d of the bench workload, forward_backward_inference with ll, "
-                     "C restatement (oracle/nip_oracle.c, gcc -O2) with OpenMP over %d threads, "
-                     "%.1f s" % (n, T, cores, el)}
-    try:
-        if bind.ref_available():
-            ref = bind.RefHarness(synth.spec_to_replay(nodes, pots), cards=[x[1] for x in nodes])
-            k, t0 = 0, time.perf_counter()
-            while True:
-                ref.fb(obs[k][:T], ov, [q])
-                k += 1
-                if time.perf_counter() - t0 >= budget_s / 4 or k >= obs.shape[0]:
-                    break
-            ref_rate = k * T / (time.perf_counter() - t0)
-            rec["reference_1core"] = ref_rate
-            rec["r_port_over_ref_per_core"] = (rec["value"] / cores) / ref_rate
-    except Exception as e:  # the reference build is optional on the GPU box
-        rec["reference_1core_error"] = str(e)[:200]
-    return rec
-
-
-def load_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")   # profiles/summarize.py
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        e = d.get("entries", {}).get(workload)
-        if e:
-            return e.get("hbm_bytes_per_launch")
-    except Exception:
-        pass
-    return None
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=0, help="sequences per GPU (0: the workload's)")
-    ap.add_argument("--T", type=int, default=0, help="time slices (0: the workload's)")
-    ap.add_argument("--N", type=int, default=16)
-    ap.add_argument("--M", type=int, default=16)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb",
-                    help="fb: the headline metric (config 2 smoothing); estep: one batched "
-                         "e_step (config 4 per-GPU shard: counts + ll, no posterior write); "
-                         "em: config 4, one step = one em_learn iteration (m_step, e_step of "
-                         "the shard, the packed all-gather over RCCL, finalize); "
-                         "config3: demo1 @ 32 states smoothing; config5: wide-clique smoothing; "
-                         "jtree: a factorial HMM on the general join-tree engine; "
-                         "joint: the same slice as a joint-interface chain")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
-    args = ap.parse_args()
-    world = launch_or_check(args, sys.argv[1:])
-
-    import torch
-    import torch.distributed as dist
-    import nip_amd
-
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
-
-    cfg, spec, ov_names, q_name, B0, T0 = WORKLOADS[args.workload]
-    B, T = args.batch or B0, args.T or T0
-    nodes, pots = spec(args)
-    model = nip_amd.Model.from_spec(nodes, pots)
-    ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
-    if args.workload == "jtree":
-        model.set_engine(nip_amd.ENGINE_JTREE)     # the joint-interface chain would take it otherwise
-    N, M = model.card(q), model.card(ov[0])
-    obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
-                             for i, v in enumerate(ov)], axis=2)
-    obs = torch.from_numpy(obs_np).to(dev)
-    ll = torch.empty((B,), dtype=torch.float64, device=dev)
-    st = torch.empty((B,), dtype=torch.int32, device=dev)
-    if args.workload == "generate":
-        sample = torch.empty((B, T, model.num_vars), dtype=torch.int32, device=dev)
-        st.zero_()
-        ll.zero_()
-
-        def step():
-            nip_amd.generate_data(model, 12345 + rank, B, T, sample)
-    elif args.workload == "em":
-        from nip_amd import em as nem
-        group = dist.group.WORLD if world > 1 else None
-        em_state = {"params": synth.uniform01(2024, model.param_size()) + 0.05, "ll": [],
-                    "exchange_ms": []}
-
-        def step():
-            tm = {}
-            p, l, bad = nem.iteration(model, em_state["params"], obs, ov, group, timing=tm)
-            if bad:
-                raise SystemExit("bench: e_step BAD_LUCK on synthetic data")
-            em_state["params"] = p
-            em_state["ll"].append(l)
-            em_state["exchange_ms"].append(tm.get("exchange_ms", 0.0))
-    elif args.workload != "estep":
-        post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
-
-        def step():
-            nip_amd.forward_backward_inference(model, obs, ov, [q], post, ll, st)
-    else:
-        counts = torch.ones((model.param_size(),), dtype=torch.float64, device=dev)
-
-        def step():
-            nip_amd.e_step(model, obs, ov, counts, ll, st)
-
-    def barrier():
-        if world > 1:
-            dist.barrier(device_ids=[dev.index])
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record()
-        step()
-        evs[i][1].record()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if args.workload == "em":
-        ll.zero_()
-        st.zero_()
-    if not args.no_check and (not bool(torch.isfinite(ll).all()) or int(st.abs().sum()) != 0):
-        raise SystemExit("bench: non-finite log-likelihood / zero-mass status on synthetic data")
-
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    units = B * T * args.steps * world
-    value = units / elapsed
-    bpu = algorithmic_bytes_per_seq_step(N, len(ov), args.workload not in ("estep", "em"))
-    narrow = N <= 16 and len(ov) <= 1
-    if not narrow and N <= 32 and os.environ.get("NIPAMD_FB_KERNEL") != "wide":
-        kname = "chain_mfma_wide_kernel<%d>" % (1 if N <= 16 else 2)
-    elif not narrow:
-        kname = ("chain_wide4_kernel" if N > 32 and os.environ.get("NIPAMD_WIDE_KERNEL") != "wave1"
-                 else "chain_wide_kernel<%d>" % (16 if N <= 16 else 32 if N <= 32 else 64))
-    elif os.environ.get("NIPAMD_FB_KERNEL") == "scratch":
-        kname = "chain_fb_mfma_kernel"
-    elif os.environ.get("NIPAMD_FB_KERNEL") != "dpp":
-        kname = "chain_fb_ckpt_kernel"     # 16-state posteriors (config 2); else chain_fb_mfma_kernel
-    else:
-        kname = "chain_kernel<false>"
-    metric = METRIC
-    if args.workload == "fb":
-        workload = "config2: HMM-shaped DBN, %d hidden x %d observed states, B=%d seq/GPU x T=%d" % (
-            N, M, B, T)
-    elif args.workload == "estep":
-        kname = ("chain_fb_mfma_kernel<true, true>" if os.environ.get("NIPAMD_ESTEP_KERNEL") == "mfma"
-                 else "chain_kernel<true>") + " + tree64 + finalize"
-        workload = "config4 shard: e_step of HMM-shaped DBN, %d hidden x %d observed, B=%d seq/GPU x T=%d" % (
-            N, M, B, T)
-        metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
-    elif args.workload == "em":
-        kname = "chain_kernel<true> + tree64 + finalize"
-        workload = ("config4: em_learn iterations of HMM-shaped DBN, %d hidden x %d observed, "
-                    "B=%d seq/GPU x T=%d, %d GPU(s), one packed RCCL all-gather per iteration" % (
-                        N, M, B, T, world))
-        metric = "sequence-timesteps/s em_learn (E-step + exchange + M-step per iteration), 16-state DBN"
-    elif args.workload == "generate":
-        kname = "generate_kernel"
-        bpu = 4 * model.num_vars       # the int32 draws written; the tables stay in cache
-        workload = "generate_data: HMM-shaped DBN, %d hidden x %d observed states, B=%d series/GPU x T=%d" % (
-            N, M, B, T)
-        metric = "sequence-timesteps/s generate_data (sampling), 16-state DBN"
-    elif args.workload == "jtree":
-        kname = "jt_filter_kernel + jt_post_kernel"
-        bpu = 4 + 8 * N                # I/O only: the obs read, the posterior written
-        workload = ("general join-tree engine: factorial HMM, X and Y 4 states each, O1 16 states of both, "
-                    "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
-        metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
-    elif args.workload == "joint":
-        K = 16                         # joint interface states (X1, Y1)
-        kname = "chain_fb_ckpt_kernel + derive_kernel"
-        # the chain kernel's bytes at K states, then the derive pass: the joint
-        # posterior read back, X1's marginal written
-        bpu = algorithmic_bytes_per_seq_step(K, len(ov), True) + 8 * K + 8 * N
-        workload = ("joint-interface chain: factorial HMM, X and Y 4 states each, O1 16 states of both, "
-                    "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
-        metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (joint-interface chain kernels)"
-    elif args.workload == "config3":
-        workload = "config3: demo1.net structure, 5 vars x 32 states, A1 B1 observed, C1 posterior, " \
-                   "B=%d seq/GPU x T=%d" % (B, T)
-        metric = "sequence-timesteps/s fwd-bwd smoothing, demo1 @ 32 states"
-    else:
-        workload = "config5: wide clique {X0,Y1,Z1,X1} 64^4 entries, O1 16 states observed, X1 posterior, " \
-                   "B=%d seq/GPU x T=%d" % (B, T)
-        metric = "sequence-timesteps/s fwd-bwd smoothing, wide-clique DBN (64^4 in-clique)"
-    achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(workload)
-    if rank == 0:
-        rec = {
-            "metric": metric, "value": value, "unit": "sequence-timesteps/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": workload, "B_per_gpu": B, "T": T, "hidden_states": N,
-                       "observed_states": M, "observed_vars": len(ov), "parallelism": "dp%d" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": kname,
-                         "kernel_ms": kern_ms, "bytes_per_unit": bpu},
-        }
-        if args.workload == "em":
-            rec["em"] = {"iterations_timed": args.steps, "ll_per_iteration": em_state["ll"][-args.steps:],
-                         "exchange_ms_median": float(np.median(em_state["exchange_ms"][-args.steps:])),
-                         "exchange_bytes_per_rank": 8 * (model.param_size() + 2),
-                         "note": "kernel_ms is the whole iteration on the launch stream "
-                                 "(e_step kernels, exchange, finalize, host m_step)"}
-        if args.workload == "jtree":
-            rec["roofline"]["note"] = "bytes are the request's I/O only; the engine is latency-bound (DESIGN.md 4)"
-        if world == 1 and args.workload in ("fb", "config3", "config5"):
-            # PCIe-inclusive figure (DESIGN.md 8): the same batch from host
-            # buffers through nipamd_fb_host (H2D obs, kernels, D2H posteriors)
-            host_obs = np.ascontiguousarray(obs_np)
-            nip_amd.forward_backward_inference_host(model, host_obs, ov, [q])
-            t1 = time.perf_counter()
-            nip_amd.forward_backward_inference_host(model, host_obs, ov, [q])
-            el1 = time.perf_counter() - t1
-            rec["pcie_inclusive"] = {"value": B * T / el1, "unit": "sequence-timesteps/s", "ms": el1 * 1e3,
-                                     "note": "host buffers in and out (pageable), one call; not the headline"}
-        if args.workload == "config5":
-            # the in-clique marginalisation: 64^4 entries summed over the hidden
-            # parents on the GPU (fold.hip), once per model version
-            fms, fby = [], 0.0
-            for _ in range(5):
-                _, ms_f, fby = model.fold()
-                fms.append(ms_f)
-            fk = float(np.median(fms))
-            rec["fold"] = {"kernel": "fold_kernel", "kernel_ms": fk, "bytes": fby,
-                           "roofline": {"bound": "hbm", "achieved": fby / (fk * 1e-3) / 1e9,
-                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                        "frac": fby / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                           "note": "A[x][y] = sum over Y1, Z1 of the 134 MB clique x priors, per model version"}
-        if world == 1 and not args.no_cpu_baseline and args.workload == "generate":
-            rec["cpu_baseline"] = cpu_baseline_generate(nodes, pots, T)
-        elif world == 1 and not args.no_cpu_baseline and args.workload not in ("estep", "em"):
-            names = [n[0] for n in nodes]
-            rec["cpu_baseline"] = cpu_baseline(
-                nodes, pots, obs_np, [names.index(v) for v in ov_names], names.index(q_name),
-                t_sample=2 if args.workload == "config5" else 0)
-        print(json.dumps(rec))
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

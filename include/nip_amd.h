@@ -290,6 +290,9 @@ int nipamd_model_set_tables(nipamd_model* m, int n_cliques, const double* const*
 
 /* Last error message (thread-local), for diagnostics. */
 const char* nipamd_last_error(void);
+/* Name of the dominant kernel of the library's last hot-path launch (e.g.
+ * "chain_fb_ckpt_kernel"), for measurement labels; "" before any launch. */
+const char* nipamd_last_kernel(void);
 
 /* Name of state `state` of variable `var` (the .net `states` field; "0".."card-1"
  * for models built from a spec).  Copies at most cap-1 bytes into buf; returns

@@ -48,7 +48,7 @@ EXPORTS = [
     "nipamd_model_num_vars", "nipamd_model_var_index", "nipamd_model_var_card",
     "nipamd_model_desc_json", "nipamd_model_param_size", "nipamd_model_gpu_supported",
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
-    "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error",
+    "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error", "nipamd_last_kernel",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
     "nipamd_estep_finalize", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
@@ -108,6 +108,7 @@ def lib():
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
         L.nipamd_model_prior.argtypes = [vp, C.c_int, dp]
         L.nipamd_last_error.restype = C.c_char_p
+        L.nipamd_last_kernel.restype = C.c_char_p
         L.nipamd_graph_cliques.argtypes = [C.c_int, ip, C.c_int, ip, C.c_int, ip, ip, C.c_int]
         L.nipamd_model_state_name.argtypes = [vp, C.c_int, C.c_int, C.c_char_p, C.c_int]
         L.nipamd_read_timeseries.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
@@ -132,6 +133,12 @@ def lib():
 def _check(rc):
     if rc != 0:
         raise NipError(rc, lib().nipamd_last_error().decode())
+
+
+def last_kernel() -> str:
+    """The dominant kernel of the library's last hot-path launch (a label for
+    measurements, nipamd_last_kernel)."""
+    return lib().nipamd_last_kernel().decode()
 
 
 def _ints(xs):
@@ -219,6 +226,11 @@ class Model:
     def gpu_supported(self, obs_vars, query) -> bool:
         return bool(lib().nipamd_model_gpu_supported(self._h, len(obs_vars), _ints(obs_vars),
                                                      len(query), _ints(query)))
+
+    def partial_size(self) -> int:
+        """Doubles in an e_step partial (nipamd_estep_partial_size): the count
+        body plus the 2-slot route tag; -1 without an e_step plan."""
+        return lib().nipamd_estep_partial_size(self._h)
 
     def estep_supported(self) -> bool:
         """Whether the batched e_step has a GPU plan for this model under the

@@ -10,6 +10,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "libnip_amd.so")
+# the diagnostics build: the same sources with -DNIPAMD_DIAGNOSTICS (kernel-
+# selection A/B switches read from the environment, per-block phase stamps);
+# selected with NIPAMD_LIB, never by the product path (csrc/diag.h)
+DIAG_LIB = os.path.join(LIB_DIR, "diag", "libnip_amd_diag.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("NIPAMD_ARCH", "gfx950")
 
@@ -71,6 +75,7 @@ def build(verbose: bool = False, defines=(), out: str = LIB) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
     if out == LIB:
+        build(verbose, defines=["NIPAMD_DIAGNOSTICS=1"], out=DIAG_LIB)
         build_tools(verbose)
     return out
 

@@ -487,6 +487,7 @@ int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream) {
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel), lds, lds_set)) return -1;
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
   hipLaunchKernelGGL(chain_fb_ckpt_kernel, dim3(blocks), dim3(kCThreads), lds, stream, a);
+  g_last_kernel = "chain_fb_ckpt_kernel";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -21,6 +21,10 @@ inline int ensure_dyn_lds(const void* kernel, size_t lds, size_t (&set)[kMaxDevi
   return 0;
 }
 
+// Name of the dominant kernel of the library's last hot-path launch (set by
+// the launch functions; nipamd_last_kernel), for measurement labels.
+extern const char* g_last_kernel;
+
 struct ChainArgs {
   const int* obs;        // int32 observations
   long obs_bstride;      // elements between sequences

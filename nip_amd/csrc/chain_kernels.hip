@@ -479,6 +479,7 @@ int chain_fb_launch(const ChainArgs& a, hipStream_t stream) {
   const int blocks = (int)((a.B + kChainsPerBlock - 1) / kChainsPerBlock);
   const size_t lds = (chain_lds_bytes(a.M, a.T, false) + 15) & ~(size_t)15;
   hipLaunchKernelGGL(chain_kernel<false>, dim3(blocks), dim3(kThreads), lds, stream, a);
+  g_last_kernel = "chain_kernel<false>";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -486,6 +487,7 @@ int chain_estep_launch(const ChainArgs& a, hipStream_t stream) {
   const int blocks = (int)((a.B + kChainsPerBlock - 1) / kChainsPerBlock);
   const size_t lds = (chain_lds_bytes(a.M, a.T, true) + 15) & ~(size_t)15;
   hipLaunchKernelGGL(chain_kernel<true>, dim3(blocks), dim3(kThreads), lds, stream, a);
+  g_last_kernel = "chain_kernel<true>";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -50,6 +50,7 @@
 
 #include "chain_kernels.h"
 #include "chain_mfma_core.h"
+#include "diag.h"
 
 namespace nipamd {
 
@@ -695,6 +696,7 @@ int launch_mfma(const ChainArgs& a, size_t lds, hipStream_t stream) {
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA, ES>), lds, lds_set)) return -1;
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
   hipLaunchKernelGGL((chain_fb_mfma_kernel<DMA, ES>), dim3(blocks), dim3(kMThreads), lds, stream, a);
+  g_last_kernel = ES ? "chain_fb_mfma_kernel<estep>" : "chain_fb_mfma_kernel";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace
@@ -703,7 +705,7 @@ int chain_fb_mfma_launch(const ChainArgs& a, hipStream_t stream) {
   // 16-wide posterior rows: the checkpoint + recompute kernel (chain_ckpt.hip)
   // unless NIPAMD_FB_KERNEL=scratch asks for this file's scratch round trip
   static const bool ckpt = [] {
-    const char* e = std::getenv("NIPAMD_FB_KERNEL");
+    const char* e = diag_env("NIPAMD_FB_KERNEL");
     return !(e && std::strcmp(e, "scratch") == 0);
   }();
   if (ckpt) {

@@ -550,6 +550,7 @@ int launch_wide(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
   const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
   hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
                      lds, stream, a);
+  g_last_kernel = NT == 1 ? "chain_mfma_wide_kernel<1>" : "chain_mfma_wide_kernel<2>";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace

@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "chain_kernels.h"
+#include "diag.h"
 
 namespace nipamd {
 
@@ -213,7 +214,7 @@ int chain_wide_launch(const WideArgs& a, hipStream_t stream) {
   // 33..64 states: the four-waves-per-direction kernel (chain_wide4.hip);
   // NIPAMD_WIDE_KERNEL=wave1 keeps this one-wave form for A/B measurements
   static const bool wave1 = [] {
-    const char* e = std::getenv("NIPAMD_WIDE_KERNEL");
+    const char* e = diag_env("NIPAMD_WIDE_KERNEL");
     return e && std::string(e) == "wave1";
   }();
   if (a.N > 32 && !wave1) {
@@ -222,6 +223,7 @@ int chain_wide_launch(const WideArgs& a, hipStream_t stream) {
   }
   const size_t lds = (chain_wide_lds_bytes(a.ncol, a.T) + 15) & ~(size_t)15;
   const dim3 grid((unsigned)a.B), block(128);
+  g_last_kernel = a.N <= 16 ? "chain_wide_kernel<16>" : a.N <= 32 ? "chain_wide_kernel<32>" : "chain_wide_kernel<64>";
   if (a.N <= 16) hipLaunchKernelGGL(chain_wide_kernel<16>, grid, block, lds, stream, a);
   else if (a.N <= 32) hipLaunchKernelGGL(chain_wide_kernel<32>, grid, block, lds, stream, a);
   else hipLaunchKernelGGL(chain_wide_kernel<64>, grid, block, lds, stream, a);

@@ -377,6 +377,7 @@ int chain_wide4_launch(const WideArgs& a, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel), lds, lds_set)) return -1;
   hipLaunchKernelGGL(chain_wide4_kernel, dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
+  g_last_kernel = "chain_wide4_kernel";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "chain_kernels.h"
+#include "diag.h"
 #include "model.h"
 #include "nip_amd.h"
 
@@ -356,7 +357,7 @@ int reduce_rows(const double* in, long n, int S, double* tA, double* tB, double*
 // (the 16-lane DPP kernel, kept for the e_step and for A/B measurements)
 bool use_mfma() {
   static const bool v = [] {
-    const char* e = std::getenv("NIPAMD_FB_KERNEL");
+    const char* e = nipamd::diag_env("NIPAMD_FB_KERNEL");
     return !(e && std::string(e) == "dpp");
   }();
   return v;
@@ -425,11 +426,14 @@ struct DevBufs {
 
 namespace nipamd {
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
+const char* g_last_kernel = "";
 }  // namespace nipamd
 
 extern "C" {
 
 const char* nipamd_last_error(void) { return g_err.c_str(); }
+
+const char* nipamd_last_kernel(void) { return nipamd::g_last_kernel; }
 
 int nipamd_model_from_spec(int n_nodes, const char* const* symbols, const int* card,
                            const int* next, int n_pots, const int* pot_child,
@@ -661,7 +665,7 @@ enum ChainKernel { kNoChain = 0, kMfmaWide, kNarrowMfma, kNarrowDpp, kWide64 };
 static int pick_kernel(const nipamd_model* mm, const Route& r, const ReqTables* rt, int T, bool filt) {
   const auto& P = mm->m.chain;
   static const bool force_wide = [] {
-    const char* e = std::getenv("NIPAMD_FB_KERNEL");
+    const char* e = nipamd::diag_env("NIPAMD_FB_KERNEL");
     return e && std::string(e) == "wide";
   }();
   if ((!r.narrow || filt) && P.N <= 32 && !force_wide &&
@@ -1065,7 +1069,7 @@ int nipamd_estep_partial_size(const nipamd_model* mm) {
 static int chain_estep_kernel(const nipamd_model* mm, int T) {
   const auto& P = mm->m.chain;
   const int M = P.emits[0].M;
-  const char* ek = std::getenv("NIPAMD_ESTEP_KERNEL");
+  const char* ek = nipamd::diag_env("NIPAMD_ESTEP_KERNEL");
   const bool want_mfma = ek && std::string(ek) == "mfma";
   if (want_mfma && P.N <= 16 && M <= 16 && nipamd::chain_estep_mfma_lds_bytes(M, T) <= 160 * 1024) return 1;
   if (nipamd::chain_lds_bytes(M, T, true) <= 96 * 1024) return 2;

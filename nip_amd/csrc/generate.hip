@@ -163,6 +163,7 @@ int rand_window_launch(int B, const uint32_t* qd_base, uint32_t* win, hipStream_
 }
 
 int generate_launch(const GenArgs& a, hipStream_t stream) {
+  g_last_kernel = "generate_kernel";
   if (a.B <= 0 || a.T <= 0) return 0;
   GenArgs g = a;
   g.stage = std::max(1, std::min(16, (256 - 31) / std::max(1, a.nv)));   // <= 64 KB LDS per block

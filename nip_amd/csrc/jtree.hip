@@ -15,6 +15,7 @@
 
 #include <cfloat>
 
+#include "chain_kernels.h"
 #include "jtree.h"
 #include "nip_amd.h"
 
@@ -348,6 +349,7 @@ int post_launch(const JtRun& r, hipStream_t st) {
 }  // namespace
 
 int jt_filter_launch(const JtRun& r, int L, bool lds, int dirs, hipStream_t st) {
+  g_last_kernel = "jt_filter_kernel + jt_post_kernel";
   if (L == 16) return lds ? filter_launch<16, true>(r, dirs, st) : filter_launch<16, false>(r, dirs, st);
   if (L == 32) return lds ? filter_launch<32, true>(r, dirs, st) : filter_launch<32, false>(r, dirs, st);
   return lds ? filter_launch<64, true>(r, dirs, st) : filter_launch<64, false>(r, dirs, st);

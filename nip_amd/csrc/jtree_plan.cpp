@@ -28,6 +28,7 @@
 #include "jtree.h"
 #include "model.h"
 #include "nip_amd.h"
+#include "diag.h"
 
 namespace nipamd {
 namespace {
@@ -390,7 +391,7 @@ static int build_plan(const nipamd_model* mm, int n_obs, const int* obs_vars, in
   if (I.size() > (size_t)0x7fffffff) { why = "schedule too large"; return NIPAMD_ERROR_UNSUPPORTED; }
 
   P.L = maxc <= 64 && K <= 64 && maxout <= 64 ? 16 : 64;
-  if (const char* e = std::getenv("NIPAMD_JT_L")) {       // A/B: lanes per unit (16, 32 or 64)
+  if (const char* e = diag_env("NIPAMD_JT_L")) {       // A/B: lanes per unit (16, 32 or 64)
     const int l = std::atoi(e);
     if (l == 16 || l == 32 || l == 64) P.L = l;
   }

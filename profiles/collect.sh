@@ -3,25 +3,26 @@
 # separate PMC passes (counters never combined with sys/runtime traces).
 # Usage (on the GPU box, from the repo root):  bash profiles/collect.sh <tag> [workloads...]
 # then, back in the build container:  python profiles/summarize.py <tag>
-# Workloads: fb (config 2, the headline), config3, config5, estep (config 4 shard).
+# Workloads: fb (config 2, the headline), config3, config5, em (config 4: one
+# em_learn iteration over the 131072 x 1024 shard), estep (its e_step alone).
 set -euo pipefail
 TAG=${1:-run}
 shift || true
-WLS=${*:-fb config3 config5 estep}
+WLS=${*:-fb config3 config5 em}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
-mkdir -p $OUT; for W in ${*:-fb config3 config5 estep}; do mkdir -p $OUT/$W; done
+mkdir -p $OUT; for W in $WLS; do mkdir -p $OUT/$W; done
 cd /tmp && export TMPDIR=/tmp
 for W in $WLS; do
   case $W in
-    estep) ARGS="--workload estep --batch 131072 --steps 3 --warmup 1" ;;
-    *) ARGS="--workload $W --steps 5 --warmup 1 --no-cpu-baseline" ;;
+    estep|em) ARGS="--workload $W --steps 3 --warmup 1 --no-cpu-baseline" ;;
+    *) ARGS="--workload $W --no-secondary --steps 5 --warmup 1 --no-cpu-baseline" ;;
   esac
   B="$R/bench.py $ARGS"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$W/trace -o run --output-format csv -- python3 $B > $OUT/$W/trace.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/$W/pmc2 -o run --output-format csv -- python3 $B > $OUT/$W/pmc2.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/$W/pmc3 -o run --output-format csv -- python3 $B > $OUT/$W/pmc3.log 2>&1
-  if [ "$W" = fb ]; then
+  if [ "$W" = fb ] || [ "$W" = config3 ] || [ "$W" = em ]; then
     timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $OUT/$W/pmc1 -o run --output-format csv -- python3 $B > $OUT/$W/pmc1.log 2>&1
   fi
   echo "$W done"

@@ -75,9 +75,14 @@ def main(tag):
         fetch, write = counters.get("FETCH_SIZE"), counters.get("WRITE_SIZE")
         if rec and fetch is not None and write is not None:
             rd, wr = 2 * fetch * 1024, write * 1024
+            calls = [int(r["Calls"]) for r in csv.DictReader(open(stats)) if r["Name"] == kname][0]
+            # e.g. 8 e_step chunks per em step; the PCIe-inclusive leg's two extra
+            # calls (fb / config3 / config5 headlines) round away
+            per_step = max(1, int(calls / float(rec["steps"] + rec["warmup"])))
             e = {"kernel": kname, "tag": tag, "fetch_size_kib": fetch, "write_size_kib": write,
                  "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-                 "hbm_bytes_per_launch": rd + wr,
+                 "hbm_bytes_per_launch": rd + wr, "launches_per_step": per_step,
+                 "hbm_bytes_per_step": (rd + wr) * per_step,
                  "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KiB -> bytes"}
             table["entries"][rec["config"]["workload"]] = e
             print(w, json.dumps(e))

@@ -1,9 +1,10 @@
 """The checkpoint + recompute forward-backward kernel (chain_ckpt.hip).
 
-NIPAMD_FB_KERNEL selects the 16-state fb kernel once per process: this
-process runs the default (the checkpoint kernel), a worker process
-(tests/_fb_worker.py) run with NIPAMD_FB_KERNEL=scratch the scratch-round-trip
-kernel (chain_mfma.hip).  Both are checked against the oracle (1e-12, as
+NIPAMD_FB_KERNEL selects the 16-state fb kernel once per process in the
+diagnostics build (csrc/diag.h): this process runs the default (the
+checkpoint kernel), a worker process (tests/_fb_worker.py) on the diagnostics
+library with NIPAMD_FB_KERNEL=scratch the scratch-round-trip kernel
+(chain_mfma.hip).  Both are checked against the oracle (1e-12, as
 tests/test_gpu_parity.py) and against each other: the recomputed messages and
 the sparse phase-B rescaling change only the powers of two the vectors carry
 and the rounding of the last bits, so the two kernels agree to 4e-16
@@ -34,7 +35,8 @@ DBL_MAX = np.finfo(np.float64).max
 def scratch_results():
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "scratch.npz")
-        env = dict(os.environ, NIPAMD_FB_KERNEL="scratch")
+        from nip_amd import build as nb
+        env = dict(os.environ, NIPAMD_FB_KERNEL="scratch", NIPAMD_LIB=nb.DIAG_LIB)   # a diagnostics-build switch
         r = subprocess.run([sys.executable, os.path.join(HERE, "_fb_worker.py"), out], env=env,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr

@@ -172,7 +172,8 @@ def test_wide4_matches_one_wave_kernel_config5():
         "torch.cuda.synchronize()\n"
         "np.savez(sys.argv[1], p=p.cpu().numpy(), l=l.cpu().numpy())\n")
     outs = []
-    for env in ({}, {"NIPAMD_WIDE_KERNEL": "wave1"}):
+    from nip_amd import build as nb
+    for env in ({}, {"NIPAMD_WIDE_KERNEL": "wave1", "NIPAMD_LIB": nb.DIAG_LIB}):   # a diagnostics-build switch
         path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "wide4_%d.npz" % len(outs))
         r = subprocess.run([sys.executable, "-c", "import sys\n" + code, path],
                            env=dict(os.environ, **env), timeout=300)
