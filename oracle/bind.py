@@ -9,7 +9,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-PORT_SO = os.path.join(HERE, "libnip_oracle.so")
+# NIPAMD_ORACLE_SO: another build of the port (the sanitizer test loads an ASan/UBSan one)
+PORT_SO = os.environ.get("NIPAMD_ORACLE_SO", os.path.join(HERE, "libnip_oracle.so"))
 REF_SO = os.path.join(HERE, "_ref", "libnipref.so")
 REF_SRC = os.environ.get("NIP_REFERENCE_SRC", "/root/reference/src")
 

@@ -1,0 +1,139 @@
+"""AddressSanitizer + UndefinedBehaviorSanitizer builds of the host C/C++
+code (memory-safety checks of the CPU side; GPU sanitizers are not
+available on this pool, so they cover host code only):
+
+  - the oracle's C restatement (oracle/nip_oracle.c) -- fb, filter, e_step,
+    em_learn on HMM, demo1 and factorial slices, bit-identical to the plain
+    build (no FMA contraction on x86-64 without -mfma);
+  - libnip.so's host code (nip_amd/compat: the reference's nippotential /
+    nipjointree / nipvariable / niplists API and parse_model) under the
+    reference's own test/potentialtest.c (its known-answer md5) and the
+    seeded single-slice host scripts of test_slice.py (no propagation, so no
+    GPU), bit-identical to the plain build.
+
+Every sanitizer report aborts the process (-fno-sanitize-recover=all)."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from nip_amd import build, synth
+
+import slice_util as su
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "_bin", "asan")
+SAN = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+
+
+def _cc(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, " ".join(cmd) + "\n" + r.stderr[-3000:]
+
+
+@pytest.fixture(scope="module")
+def asan_port():
+    os.makedirs(OUT, exist_ok=True)
+    so = os.path.join(OUT, "libnip_oracle_asan.so")
+    _cc(["gcc", *SAN, "-fPIC", "-std=gnu99", "-w", "-fopenmp", "-shared", "-o", so,
+         os.path.join(ROOT, "oracle", "nip_oracle.c"), "-lm"])
+    return so
+
+
+PORT_SCRIPT = r'''
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import nip_amd
+from nip_amd import synth
+from oracle.bind import PortOracle
+out = {}
+cases = [("hmm", synth.hmm_spec(6, 5), ["M1"], ["P1", "P0"]),
+         ("demo1", synth.demo1_spec(4), ["A1", "B1"], ["C1", "D1"]),
+         ("factorial", synth.factorial_spec(3, 2, 4), ["O1"], ["X1", "Y1"])]
+rng = np.random.default_rng(5)
+for name, spec, ovs, qs in cases:
+    m = nip_amd.Model.from_spec(*spec)
+    ov, q = [m.variable(v) for v in ovs], [m.variable(v) for v in qs]
+    obs = np.stack([rng.integers(-1, m.card(v), size=(5, 17)) for v in ov], axis=2).astype(np.int32)
+    obs[:, 0] = np.maximum(obs[:, 0], 0)
+    orc = PortOracle(m.desc())
+    for b in range(obs.shape[0]):
+        p, l = orc.fb(obs[b], ov, q)
+        f, fl = orc.fb(obs[b], ov, q, filter_only=True)
+        out["%s/fb%d" % (name, b)] = [p.tolist(), l, f.tolist(), fl]
+    c, l, bad = orc.estep(obs, ov, np.ones(m.param_size()))
+    out[name + "/estep"] = [c.tolist(), l.tolist(), bad.tolist()]
+    pb, lb = orc.fb_batch(obs, ov, q, nthreads=2)
+    out[name + "/batch"] = [pb.tolist(), lb.tolist()]
+    init = np.random.default_rng(1).random(m.param_size())
+    it, curve = orc.em(obs, ov, init, 1e-6, 5)
+    out[name + "/em"] = [int(it), np.asarray(curve).tolist()]
+print(json.dumps(out))
+'''
+
+
+def _run_port(so=None):
+    env = dict(ENV)
+    if so:
+        env["NIPAMD_ORACLE_SO"] = so
+        env["LD_PRELOAD"] = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True,
+                                           text=True).stdout.strip()
+    r = subprocess.run([sys.executable, "-c", PORT_SCRIPT, ROOT], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_oracle_port_under_asan_ubsan(asan_port):
+    assert _run_port(asan_port) == _run_port()
+
+
+@pytest.fixture(scope="module")
+def asan_compat():
+    os.makedirs(OUT, exist_ok=True)
+    inc = ["-I" + os.path.join(ROOT, "include", "compat"), "-I" + os.path.join(ROOT, "include")]
+    lib = os.path.join(OUT, "libnip.so")
+    srcs = sorted(os.path.join(ROOT, "nip_amd", "compat", f) for f in os.listdir(os.path.join(ROOT, "nip_amd", "compat"))
+                  if f.endswith(".cpp"))
+    _cc(["g++", *SAN, "-std=c++17", "-fPIC", "-shared", *inc, *srcs, "-L" + build.LIB_DIR, "-lnip_amd",
+         "-Wl,-rpath," + build.LIB_DIR, "-o", lib])
+    driver = os.path.join(OUT, "slice_driver")
+    _cc(["gcc", *SAN, "-std=gnu99", *inc, "-I" + os.path.join(ROOT, "oracle", "ref"),
+         os.path.join(ROOT, "tests", "capi", "slice_driver.c"), "-L" + OUT, "-lnip", "-L" + build.LIB_DIR,
+         "-lnip_amd", "-lm", "-Wl,-rpath," + OUT, "-Wl,-rpath," + build.LIB_DIR, "-o", driver])
+    out = {"driver": driver}
+    ptest = os.path.join(build.REF_TEST, "potentialtest.c")
+    if os.path.exists(ptest):
+        exe = os.path.join(OUT, "potentialtest")
+        _cc(["gcc", *SAN, "-w", *inc, ptest, "-L" + OUT, "-lnip", "-L" + build.LIB_DIR, "-lnip_amd", "-lm",
+             "-Wl,-rpath," + OUT, "-Wl,-rpath," + build.LIB_DIR, "-o", exe])
+        out["potentialtest"] = exe
+    return out
+
+
+def test_compat_potentialtest_under_asan_ubsan(asan_compat):
+    exe = asan_compat.get("potentialtest")
+    if exe is None:
+        pytest.skip("the reference's test/potentialtest.c is not present here")
+    r = subprocess.run([exe], capture_output=True, env=ENV, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:].decode(errors="replace")
+    assert hashlib.md5(r.stdout).hexdigest().startswith("ac8ecd1b")
+
+
+def test_compat_host_slice_scripts_under_asan_ubsan(asan_compat, tmp_path):
+    models = dict(list(su.contract_models().items())[:6])
+    nets = {k: su.spec_to_net(n, p, str(tmp_path / (k + ".net"))) for k, (n, p) in models.items()}
+    nets["model"] = os.path.join(su.GOLD, "model.net")
+    nets["demo1"] = os.path.join(su.GOLD, "demo1.net")
+    for name, net in sorted(nets.items()):
+        script = su.random_script(net, 0, propagate=False)
+        r = subprocess.run([asan_compat["driver"], net, script], capture_output=True, text=True, env=ENV,
+                           timeout=300)
+        assert r.returncode == 0, (name, r.stderr[-4000:])
+        assert r.stdout == su.compat_slice(net, script), name
