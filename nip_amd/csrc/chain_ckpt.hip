@@ -4,10 +4,11 @@
 // chain_fb_mfma_kernel (chain_mfma.hip) hands every phase-A message to phase
 // B through HBM: alpha_t (t < H) and beta_t (t >= H) are written once and read
 // once, 256 of its 388 bytes per sequence-step.  Here phase A keeps one
-// message in four (checkpoints), and phase B recomputes each chunk's eight
-// messages from two of them -- two independent 4-step chains, interleaved --
-// on the partner SIMDs, one chunk at a time, in step with the filter that
-// consumes them:
+// message in four (checkpoints), and phase B rebuilds each chunk's eight
+// messages from two of them -- each checkpoint is one of the chunk's rows and
+// seeds a 3-step chain for the other three of its half (two independent
+// chains, interleaved) -- on the partner SIMDs, one chunk at a time, in step
+// with the filter that consumes them:
 //
 //   SIMD 0: wave 0 forward filter (alpha, rings, z2)        wave 4 backward posteriors,
 //                                                                    chains 8-15
@@ -77,19 +78,22 @@ struct CkDiag {
   }
 };
 
-// Message recomputation for the other direction's phase-B chunks.
+// Message recomputation for the other direction's phase-B chunks.  Sub-chain
+// h of chunk ci covers the rows 4h..4h+3; its checkpoint is one of them:
 //   !FWD (wave 6): beta_t for the forward filter's chunk ci, t = H + 8ci + k, into
-//     ring row k; sub-chain h (rows 4h..4h+3) from beta_{H+8ci+4h+4} (a
-//     checkpoint, or beta_{T-1} = 1 written by the backward filter);
+//     ring row k; sub-chain h from beta_{H+8ci+4h+3} (its top row: a
+//     checkpoint, or beta_{T-1} = 1 written by the backward filter) down;
 //   FWD (wave 7): alpha_t for the backward filter's chunk ci, t = H - 1 - 8ci - k,
-//     into row k; sub-chain h from alpha_{H-5-8ci-4h} (a checkpoint, or the
-//     prior alpha_{-1}).
-// The two sub-chains of a chunk are independent: interleaved, one's
-// matrix-core latency hides the other's.  Each starts from a vector rescaled
-// to sum ~1 and runs at most four steps without rescaling (the bound phase A's
-// sparse rescaling already relies on); the posterior normalisation removes
-// the scale.  The next chunk's evidence vectors and the checkpoints two
-// chunks ahead are loaded while a chunk runs.
+//     into row k; sub-chain h from alpha_{H-4-8ci-4h} (its lowest t: a
+//     checkpoint) up, or from the prior alpha_{-1} where that t is negative.
+// A full chunk is then 2 x 3 mat-vecs, not 2 x 4: the matrix-core pipe (64
+// cycles per v_mfma_f64_16x16x4, dependent or not: profiles/r03/r03_mb_pipe.txt)
+// is what this wave's time is made of.  The two sub-chains of a chunk are
+// independent and interleaved.  Each starts from a vector rescaled to sum ~1
+// and runs at most three steps without rescaling (phase A's sparse rescaling
+// relies on four); the posterior normalisation removes the scale.  The next
+// chunk's evidence vectors and the checkpoints two chunks ahead are loaded
+// while a chunk runs.
 template <bool FWD>
 __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx& c, const double* Sw, int lane,
                                                int nchA, int nchB, CkDiag& dg) {
@@ -108,20 +112,19 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
 
   const int n = FWD ? H : T - H;                 // steps of the consuming filter's phase B
   auto tof = [&](int ci, int k) { return FWD ? H - 1 - 8 * ci - k : H + 8 * ci + k; };   // t of row k
-  // start step of sub-chain h: backward above its rows (clamped to T-1),
-  // forward below them (-1: the prior)
+  // the checkpoint row of sub-chain h: backward its top t (clamped to T-1),
+  // forward its lowest t (-1: none, the chain starts from the prior)
   auto start = [&](int ci, int h) {
     if (FWD) {
       const int lo = H - 4 - 8 * ci - 4 * h;
-      return lo > 0 ? lo - 1 : -1;
+      return lo >= 0 ? lo : -1;
     }
-    const int ts = H + 8 * ci + 4 * h + 4;
+    const int ts = H + 8 * ci + 4 * h + 3;
     return ts < T - 1 ? ts : T - 1;
   };
   auto ld = [&](int ci, int h) { return load4(Sw + (long)start(ci < nchB ? ci : nchB - 1, h) * kSStep); };
-  // a chunk's evidence rows; backward also row 8 (the next chunk's row 0,
-  // sub-chain 1's start), so that no start waits on a load just issued
-  constexpr int kE = FWD ? kMChunk : kMChunk + 1;
+  // a chunk's evidence rows
+  constexpr int kE = kMChunk;
   // codes two chunks ahead, evidence rows one chunk ahead: no load waits on
   // another load issued in the same chunk
   auto ldC = [&](int ci, int (&C)[kE]) {
@@ -168,27 +171,14 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
       ldC(ci + 2, Cnn);
     };
     const int rem = n - 8 * ci;                  // rows of this chunk (<= 0: none)
-    if (FWD && rem >= kMChunk) {
-      // rows 3..0 (sub-chain 0) and 7..4 (sub-chain 1) in increasing t
-      // the checkpoints (and the prior) sum to ~1: no rescale at the start
-      v4d X0 = start(ci, 0) >= 0 ? cur0 : prior, X1 = start(ci, 1) >= 0 ? cur1 : prior;
+    if (rem >= kMChunk) {
+      // the checkpoints are rows 3 and 7 (they sum to ~1, beta_{T-1} = 1 to
+      // N: three evidence factors per sub-chain at most, no rescale); rows
+      // 2..0 and 6..4 follow, forward in increasing t, backward in decreasing t
+      row(slot, 3, cur0);
+      row(slot, 7, cur1);
+      v4d X0 = FWD ? cur0 : cur0 * E[3], X1 = FWD ? cur1 : cur1 * E[7];
       dg.lap(&dg.x1);
-      step(X0, 0, slot, 3, E[3]);
-      step(X1, 0, slot, 7, E[7]);
-      issue();
-#pragma unroll
-      for (int q = 2; q >= 0; q--) {
-        step(X0, 0, slot, q, E[q]);
-        step(X1, 0, slot, q + 4, E[q + 4]);
-      }
-    } else if (!FWD && rem > kMChunk) {
-      // start rows 4 and 8 (= the next chunk's row 0); rows 3..0 and 7..4 in decreasing t
-      // checkpoints sum to ~1 (beta_{T-1} = 1 to N): four evidence factors
-      // per sub-chain at most, no rescale
-      v4d X0 = cur0 * E[4], X1 = cur1 * E[kE - 1];
-      dg.lap(&dg.x1);
-      step(X0, 0, slot, 3, E[3]);
-      step(X1, 0, slot, 7, E[7]);
       issue();
 #pragma unroll
       for (int q = 2; q >= 0; q--) {
@@ -205,6 +195,7 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
         if (FWD) {
           const int hiT = H - 1 - 8 * ci;
           if (hiT - 4 * h < 0) continue;          // no valid row
+          if (ts >= 0) row(slot, hiT - ts, cur);  // the checkpoint row
           v4d X = ts >= 0 ? cur : prior;
           int sc = ts >= 0 ? norm_exp(cur) : 0;
           for (int t = ts + 1; t <= hiT - 4 * h; t++) {
@@ -215,8 +206,7 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
         } else {
           const int lo = H + 8 * ci + 4 * h;
           if (lo > T - 1) continue;               // no valid row
-          const int ks = ts - (H + 8 * ci);
-          if (ts < lo + 4) row(slot, ks, cur);    // beta_{T-1} inside the chunk
+          row(slot, ts - (H + 8 * ci), cur);      // the checkpoint row (or beta_{T-1})
           v4d X = cur * load4(c.Et + c.codes[ts] * c.es);
           int sc = norm_exp(X);
           for (int t = ts - 1; t >= lo; t--) {
@@ -297,8 +287,6 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
   const int nA = FWD ? H : T - 1 - H, nB = FWD ? T - H : H;
   const int tA = FWD ? 0 : T - 2, tB = FWD ? H : H - 1;
   constexpr int dir = FWD ? 1 : -1;
-  const int kB = FWD ? hi : kMChunk - 1 - hi;
-  auto tlow = [&](int ci) { return FWD ? tB + ci * kMChunk : tB - ci * kMChunk - (kMChunk - 1); };
 
   LL ll;
   if (FWD) ll.init(a, lane, false);
@@ -331,8 +319,8 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
     for (int k = 0; k < kMChunk; k++) {
       const int i = ci * kMChunk + k;
       const int t = tA + dir * i;
-      // forward: alpha_{H-5-4m} >= 0; backward: beta_{H+4+4m} <= T-2
-      const bool ck = i < nA && (FWD ? (((H - 1 - t) & 3) == 0 && t <= H - 5) : (((t - H) & 3) == 0 && t >= H + 4));
+      // forward: alpha_{H-4-4m} >= 0; backward: beta_{H+3+4m} <= T-2 (recompute_wave)
+      const bool ck = i < nA && (FWD ? (((H - t) & 3) == 0 && t <= H - 4) : (((t - H) & 3) == 3 && t >= H + 3));
       if (!ck) continue;
       // stored rescaled to sum ~1 (the chain's 16 states are the 8 lanes of
       // an aligned DPP row group): a recompute chain starts from it as is
