@@ -37,7 +37,7 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 
 #ifndef NIPAMD_MW_ABLATE
 #define NIPAMD_MW_ABLATE 0     // timing-only builds: 1 partners only keep the barriers,
-#endif                         // 2 filters skip the mat-vec, 3 filters skip the evidence
+#endif                         // 2 filters skip the mat-vec
 constexpr int kWSeq = 16;
 constexpr int kWThreads = 256;
 constexpr int kWG = kScratchGuard;
@@ -120,6 +120,10 @@ struct Geo {
   static constexpr int CH = 64 / LPC;         // steps per chunk (= chains per partner pass)
   static constexpr int QN = kWSeq / CH;       // partner passes over the 16 chains
   static constexpr int kStep = kWSeq * NP;    // doubles per step of 16 chains
+  // LDS evidence-table row stride: NP + 2 doubles, so that sixteen chains
+  // reading sixteen different rows start at banks 4 * row apart instead of
+  // all at bank 0 (an NP-double row is 128 or 256 B: 16-way conflicts)
+  static constexpr int NPS = NP + 2;
   static constexpr int kSlot = CH * kStep;    // doubles per ring slot (16 KB)
   // chain j's piece p (16 bytes) within a step, XOR-swizzled by j & 7
   __device__ static int piece_off(int j, int p) { return j * NP + ((p ^ (j & 7)) << 1); }
@@ -138,7 +142,10 @@ struct WCtx {
   bool zw;
 };
 
-template <bool FWD, int NT>
+// NC: observed columns (1..4; 0 runs as 1, column 0 carrying the row sums),
+// a template parameter so that the per-step evidence gather is branch-free and
+// its LDS loads can be scheduled under the MFMAs
+template <bool FWD, int NT, int NC>
 struct WChain {
   using G = Geo<NT>;
   double Aop[NT][NT][4];
@@ -146,21 +153,57 @@ struct WChain {
   int sc = 0;
 
   __device__ __forceinline__ void evidence(const WCtx& c, int t, v4d (&e)[NT]) const {
-    const int NP = G::NP;
     int code = c.codes[t];
 #pragma unroll
-    for (int q = 0; q < NT; q++) e[q] = load4(c.tab + c.tab_off[0] + code * NP + 16 * q);
+    for (int q = 0; q < NT; q++) e[q] = load4(c.tab + c.tab_off[0] + code * G::NPS + 16 * q);
 #pragma unroll
-    for (int k = 1; k < 4; k++) {
-      if (k >= c.ncol) break;
+    for (int k = 1; k < NC; k++) {
       code = c.codes[k * kWSeq * c.Tr + t];
 #pragma unroll
-      for (int q = 0; q < NT; q++) e[q] *= load4(c.tab + c.tab_off[k] + code * NP + 16 * q);
+      for (int q = 0; q < NT; q++) e[q] *= load4(c.tab + c.tab_off[k] + code * G::NPS + 16 * q);
     }
+  }
+
+  // the step's observation codes, one per observed column (read a step
+  // ahead: the table rows they select are loaded while the step's MFMAs run)
+  __device__ __forceinline__ void codes_of(const WCtx& c, int t, int (&cd)[NC]) const {
+#pragma unroll
+    for (int k = 0; k < NC; k++) cd[k] = c.codes[k * kWSeq * c.Tr + t];
+  }
+  __device__ __forceinline__ void rows_of(const WCtx& c, const int (&cd)[NC], v4d (&r)[NC][NT]) const {
+#pragma unroll
+    for (int k = 0; k < NC; k++) {
+#pragma unroll
+      for (int q = 0; q < NT; q++) r[k][q] = load4(c.tab + c.tab_off[k] + cd[k] * G::NPS + 16 * q);
+    }
+  }
+  __device__ __forceinline__ void product(const WCtx& c, const v4d (&r)[NC][NT], v4d (&e)[NT]) const {
+#pragma unroll
+    for (int q = 0; q < NT; q++) e[q] = r[0][q];
+#pragma unroll
+    for (int k = 1; k < NC; k++) {
+#pragma unroll
+      for (int q = 0; q < NT; q++) e[q] *= r[k][q];
+    }
+  }
+
+  // one step with the evidence rows loaded at its start: the MFMAs first, the
+  // evidence product after them (its LDS loads complete under the MFMAs)
+  __device__ __forceinline__ void step_rows(const WCtx& c, double* L, double* Z, const v4d (&r)[NC][NT]) {
+    v4d d[NT];
+    matvec(d);
+    v4d e[NT];
+    product(c, r, e);
+    finish(c, L, Z, d, e);
   }
 
   __device__ __forceinline__ void step(const WCtx& c, double* L, double* Z, const v4d (&e)[NT]) {
     v4d d[NT];
+    matvec(d);
+    finish(c, L, Z, d, e);
+  }
+
+  __device__ __forceinline__ void matvec(v4d (&d)[NT]) {
 #pragma unroll
     for (int qo = 0; qo < NT; qo++) d[qo] = v4d{0.0, 0.0, 0.0, 0.0};
 #if NIPAMD_MW_ABLATE == 2
@@ -180,6 +223,10 @@ struct WChain {
       d[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[0][qi][3], X[qi].w, d[0], 0, 0, 0);
       if (NT > 1) d[NT - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Aop[NT - 1][qi][3], X[qi].w, d[NT - 1], 0, 0, 0);
     }
+  }
+
+  __device__ __forceinline__ void finish(const WCtx& c, double* L, double* Z, const v4d (&d)[NT],
+                                         const v4d (&e)[NT]) {
     double part = 0.0;
 #pragma unroll
     for (int q = 0; q < NT; q++) {
@@ -199,24 +246,26 @@ struct WChain {
   __device__ __forceinline__ void run(const WCtx& c, int n, int nch, int t0, int lane) {
     constexpr int dir = FWD ? 1 : -1;
     constexpr int CH = G::CH;
+    int cd[NC];
+    codes_of(c, t0, cd);
     for (int ci = 0; ci < nch; ci++) {
       double* slot = c.out + (ci & 1) * G::kSlot;
       double* zs = FWD ? c.zr + (ci & 1) * CH * kWSeq + (lane & 15) : nullptr;
       const int base = ci * CH;
-      v4d e[CH][NT];
-#pragma unroll
-      for (int k = 0; k < CH; k++) {
-#if NIPAMD_MW_ABLATE == 3
-#pragma unroll
-        for (int q = 0; q < NT; q++) e[k][q] = v4d{0.5, 0.5, 0.5, 0.5};
-#else
-        evidence(c, t0 + dir * (base + k), e[k]);   // guards cover over-run
-#endif
-      }
       if (base + CH <= n) {
+        // per step: the rows its codes (read a step ahead) select, the next
+        // step's codes, then the MFMAs; guards cover the over-run
 #pragma unroll
-        for (int k = 0; k < CH; k++) step(c, slot + k * G::kStep, zs + k * kWSeq, e[k]);
+        for (int k = 0; k < CH; k++) {
+          v4d r[NC][NT];
+          rows_of(c, cd, r);
+          codes_of(c, t0 + dir * (base + k + 1), cd);
+          step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
+        }
       } else {
+        v4d e[CH][NT];
+#pragma unroll
+        for (int k = 0; k < CH; k++) evidence(c, t0 + dir * (base + k), e[k]);   // guards cover over-run
 #pragma unroll
         for (int k = 0; k < CH; k++)
           if (base + k < n) step(c, slot + k * G::kStep, zs + k * kWSeq, e[k]);
@@ -226,13 +275,13 @@ struct WChain {
   }
 };
 
-template <bool FWD, int NT>
+template <bool FWD, int NT, int NC>
 __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, double* Sblk, int lane,
                                         int nchA, int nchB) {
   using G = Geo<NT>;
   const int j = lane & 15, g = lane >> 4;
   const int T = a.T, H = a.H;
-  WChain<FWD, NT> ch;
+  WChain<FWD, NT, NC> ch;
 #pragma unroll
   for (int qo = 0; qo < NT; qo++)
 #pragma unroll
@@ -459,7 +508,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
 }
 
 // FILT: forward_inference (filtering only): waves 0 (filter) and 1 (partner), H = T
-template <int NT, bool FILT>
+template <int NT, bool FILT, int NC>
 __global__ __launch_bounds__(FILT ? kWThreads / 2 : kWThreads, 1)
 void chain_mfma_wide_kernel(WideMfmaArgs a) {
   constexpr int kThreads = FILT ? kWThreads / 2 : kWThreads;
@@ -469,13 +518,13 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   double* zr = out + 4 * G::kSlot;                          // [2 slots][CH][16]
   double* tab = zr + 2 * G::CH * kWSeq;                     // [sum (M_k + 2)][NP]
   const int ncol = a.ncol > 0 ? a.ncol : 1;
-  uint8_t* codes = reinterpret_cast<uint8_t*>(tab + a.tab_rows * G::NP);   // [ncol][16][Tr]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(tab + a.tab_rows * G::NPS);   // [ncol][16][Tr]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * kWSeq;
   const int T = a.T, Tr = chain_codes_row(T);
 
-  for (int i = tid; i < a.tab_rows * G::NP; i += kThreads) tab[i] = a.tab[i];
+  for (int i = tid; i < a.tab_rows * G::NP; i += kThreads) tab[(i / G::NP) * G::NPS + i % G::NP] = a.tab[i];
   const int nseq = (int)((a.B - b0) < kWSeq ? (a.B - b0) : kWSeq);
   for (int k = 0; k < ncol; k++) {
     const int M = a.ncol > 0 ? a.M[k] : 0;
@@ -516,7 +565,7 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   c.ncol = ncol;
   c.Tr = Tr;
 #pragma unroll
-  for (int k = 0; k < 4; k++) c.tab_off[k] = (k < ncol ? a.tab_off[k] : 0) + 2 * g;
+  for (int k = 0; k < 4; k++) c.tab_off[k] = (k < ncol ? a.tab_off[k] / G::NP * G::NPS : 0) + 2 * g;
   c.out = ring;
   c.zr = zr;
   c.zw = g == 0;
@@ -525,8 +574,8 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
     c.wo[q][0] = Geo<NT>::piece_off(j, 8 * q + g);
     c.wo[q][1] = Geo<NT>::piece_off(j, 8 * q + 4 + g);
   }
-  if (fwd) wfilter<true, NT>(a, c, Sblk, lane, nchA, nchB);
-  else if (!FILT) wfilter<false, NT>(a, c, Sblk, lane, nchA, nchB);
+  if (fwd) wfilter<true, NT, NC>(a, c, Sblk, lane, nchA, nchB);
+  else if (!FILT) wfilter<false, NT, NC>(a, c, Sblk, lane, nchA, nchB);
 }
 
 }  // namespace
@@ -534,7 +583,7 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
 size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T) {
   const size_t slot = 2048;                                  // doubles per ring slot
   const size_t ch = 8 / NT;
-  return (4 * slot + 2 * ch * kWSeq + (size_t)tab_rows * 16 * NT) * sizeof(double) +
+  return (4 * slot + 2 * ch * kWSeq + (size_t)tab_rows * (16 * NT + 2)) * sizeof(double) +
          (size_t)(ncol > 0 ? ncol : 1) * kWSeq * chain_codes_row(T);
 }
 
@@ -543,15 +592,24 @@ size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
 }
 
 namespace {
-template <int NT, bool FILT>
-int launch_wide(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
+template <int NT, bool FILT, int NC>
+int launch_wide_nc(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
   static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT>), lds, set)) return -1;
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT, NC>), lds, set)) return -1;
   const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
-  hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
+  hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT, NC>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
                      lds, stream, a);
   g_last_kernel = NT == 1 ? "chain_mfma_wide_kernel<1>" : "chain_mfma_wide_kernel<2>";
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+template <int NT, bool FILT>
+int launch_wide(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
+  switch (a.ncol > 1 ? a.ncol : 1) {
+    case 1: return launch_wide_nc<NT, FILT, 1>(a, lds, stream);
+    case 2: return launch_wide_nc<NT, FILT, 2>(a, lds, stream);
+    case 3: return launch_wide_nc<NT, FILT, 3>(a, lds, stream);
+    default: return launch_wide_nc<NT, FILT, 4>(a, lds, stream);
+  }
 }
 }  // namespace
 
