@@ -128,6 +128,7 @@ struct WideMfmaArgs {
   int post_off;
   double* ll;
   unsigned* status;
+  unsigned long long* diag;   // stamps builds (NIPAMD_WAIT_TIMES): per block [4 waves][4] cycles, else null
 };
 size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T);
 size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T);

@@ -109,8 +109,34 @@ __device__ __forceinline__ v4d load4(const double* p) {      // p = row + 16q + 
   return v4d{a.x, a.y, b.x, b.y};
 }
 
-__device__ __forceinline__ void barrier_lds() {
+#ifndef NIPAMD_WAIT_TIMES
+#define NIPAMD_WAIT_TIMES 0        // stamps builds: per-wave phase and barrier-wait cycles (a.diag)
+#endif
+// per-wave cycle stamps of the stamps build: phase A / its barrier waits /
+// phase B / its barrier waits, into a.diag[block][wave][4]
+struct MwDiag {
+  unsigned long long t0 = 0, ta = 0, wa = 0, wb = 0;
+  bool inB = false;
+  __device__ __forceinline__ void start() { if (NIPAMD_WAIT_TIMES) t0 = __builtin_readcyclecounter(); }
+  __device__ __forceinline__ void phase() {
+    if (NIPAMD_WAIT_TIMES) { ta = __builtin_readcyclecounter(); inB = true; }
+  }
+  __device__ __forceinline__ void write(unsigned long long* d, int wave, int lane) {
+    if (!NIPAMD_WAIT_TIMES || !d || lane != 0) return;
+    unsigned long long* p = d + (size_t)blockIdx.x * 16 + wave * 4;
+    p[0] = ta - t0; p[1] = wa; p[2] = __builtin_readcyclecounter() - ta; p[3] = wb;
+  }
+};
+
+__device__ __forceinline__ void barrier_lds(MwDiag* dg = nullptr) {
+#if NIPAMD_WAIT_TIMES
+  const unsigned long long t = __builtin_readcyclecounter();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (dg) (dg->inB ? dg->wb : dg->wa) += __builtin_readcyclecounter() - t;
+#else
+  (void)dg;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
 }
 
 template <int NT>
@@ -243,7 +269,7 @@ struct WChain {
     sc = -__builtin_amdgcn_frexp_exp(z2);
   }
 
-  __device__ __forceinline__ void run(const WCtx& c, int n, int nch, int t0, int lane) {
+  __device__ __forceinline__ void run(const WCtx& c, int n, int nch, int t0, int lane, MwDiag& dg) {
     constexpr int dir = FWD ? 1 : -1;
     constexpr int CH = G::CH;
     int cd[NC];
@@ -270,7 +296,7 @@ struct WChain {
         for (int k = 0; k < CH; k++)
           if (base + k < n) step(c, slot + k * G::kStep, zs + k * kWSeq, e[k]);
       }
-      barrier_lds();
+      barrier_lds(&dg);
     }
   }
 };
@@ -311,11 +337,15 @@ __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, do
     }
     ch.sc = -__builtin_amdgcn_frexp_exp(swap16_sum(swap32_sum(part)));
   }
-  if (FWD) ch.run(c, H, nchA, 0, lane);
-  else ch.run(c, T - 1 - H, nchA, T - 2, lane);
+  MwDiag dg;
+  dg.start();
+  if (FWD) ch.run(c, H, nchA, 0, lane, dg);
+  else ch.run(c, T - 1 - H, nchA, T - 2, lane, dg);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
-  if (FWD) ch.run(c, T - H, nchB, H, lane);
-  else ch.run(c, H, nchB, H - 1, lane);
+  dg.phase();
+  if (FWD) ch.run(c, T - H, nchB, H, lane, dg);
+  else ch.run(c, H, nchB, H - 1, lane, dg);
+  dg.write(a.diag, FWD ? 0 : 1, lane);
 }
 
 // ll of the forward filter (nip.c:1461-1474), kept by the forward partner:
@@ -330,12 +360,32 @@ struct WLL {
   int e2[G::QN], e1[G::QN];
   double w0, w1;
 
-  __device__ __forceinline__ void init(const WideMfmaArgs& a, int s) {
+  // first: the forward partner's accumulators start with y_{-1} = prior . w;
+  // the backward partner's share (phase-B chunks it takes over) starts at 1
+  __device__ __forceinline__ void init(const WideMfmaArgs& a, int s, bool first = true) {
     w0 = a.w[2 * s]; w1 = a.w[2 * s + 1];
     double y[1] = {a.pi[2 * s] * w0 + a.pi[2 * s + 1] * w1};
     sumL_n<G::LPC>(y);
 #pragma unroll
-    for (int q = 0; q < G::QN; q++) { m2[q] = 1.0; m1[q] = y[0]; zmin[q] = 1.0; e2[q] = 0; e1[q] = 0; }
+    for (int q = 0; q < G::QN; q++) { m2[q] = 1.0; m1[q] = first ? y[0] : 1.0; zmin[q] = 1.0; e2[q] = 0; e1[q] = 0; }
+  }
+  // the backward partner's share to LDS (5 values per lane and pass), and its product into this one
+  __device__ __forceinline__ void put(double* L, int lane) const {
+#pragma unroll
+    for (int q = 0; q < G::QN; q++) {
+      double* p = L + (q * 64 + lane) * 5;
+      p[0] = m2[q]; p[1] = m1[q]; p[2] = zmin[q]; p[3] = (double)e2[q]; p[4] = (double)e1[q];
+    }
+  }
+  __device__ __forceinline__ void take(const double* L, int lane) {
+#pragma unroll
+    for (int q = 0; q < G::QN; q++) {
+      const double* p = L + (q * 64 + lane) * 5;
+      m2[q] *= p[0]; m1[q] *= p[1]; zmin[q] = __builtin_fmin(zmin[q], p[2]);
+      e2[q] += (int)p[3]; e1[q] += (int)p[4];
+      const int k2 = __builtin_amdgcn_frexp_exp(m2[q]); m2[q] = __builtin_ldexp(m2[q], -k2); e2[q] += k2;
+      const int k1 = __builtin_amdgcn_frexp_exp(m1[q]); m1[q] = __builtin_ldexp(m1[q], -k1); e1[q] += k1;
+    }
   }
   __device__ __forceinline__ void step(int q, double y, double z2, bool last, bool renorm) {
     zmin[q] = __builtin_fmin(zmin[q], z2);
@@ -368,9 +418,13 @@ struct WLL {
 // direction's vector (scratch, one chunk prefetched), normalised over the
 // chain's LPC lanes; with N == NP and dense rows, one contiguous 1 KB
 // posterior run per store instruction.
+// Phase B's ll work is shared: the forward partner takes the forward ring's
+// even chunks, the backward partner (which has no ll of its own and waits at
+// the barriers otherwise) the odd ones; its partial products join the forward
+// partner's through LDS after the block's closing barrier.
 template <bool FWD, bool PVEC, int NT, bool FILT>
-__device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* out, const double* zr,
-                                         double* Sblk, int lane, long b0, int nchA, int nchB) {
+__device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* out, const double* fring,
+                                         const double* zr, double* Sblk, int lane, long b0, int nchA, int nchB) {
   using G = Geo<NT>;
   constexpr int NP = G::NP, LPC = G::LPC, CH = G::CH, QN = G::QN;
   const int T = a.T, H = a.H;
@@ -381,10 +435,12 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   const int kB = FWD ? hi : CH - 1 - hi;
   auto tlow = [&](int ci) { return FWD ? tB + ci * CH : tB - ci * CH - (CH - 1); };
 
+  MwDiag dg;
+  dg.start();
   WLL<NT> ll;
-  if (FWD) ll.init(a, s);
+  ll.init(a, s, FWD);
   auto ll_chunk = [&](int ci, int n, int t0) {
-    const double* slot = out + (ci & 1) * G::kSlot;
+    const double* slot = fring + (ci & 1) * G::kSlot;
     const double* zs = zr + (ci & 1) * CH * kWSeq;
     const bool full = ci * CH + CH <= n;
     double y[CH * QN];
@@ -468,11 +524,12 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   };
   for (int ci = 0; ci < nchA; ci++) {
     if (ci > 0) drainA(ci - 1);
-    barrier_lds();
+    barrier_lds(&dg);
   }
   if (nchA > 0) drainA(nchA - 1);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  dg.phase();
 
   if constexpr (FILT) {
     if (FWD) ll.write(a, b0, lane);
@@ -485,9 +542,10 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
 #pragma unroll
     for (int c = 0; c < kWSeq; c++) o[c] = *reinterpret_cast<const v2d*>(q + c * NP);
   };
+  const int nBf = T - H;                         // the forward side's phase-B steps (from t = H)
   auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {
     if (NIPAMD_MW_ABLATE == 1) return;
-    if (FWD) ll_chunk(ci, nB, tB);
+    if (FWD == ((ci & 1) == 0) && ci * CH < nBf) ll_chunk(ci, nBf, H);
     if (!PVEC && !a.post) return;
     const double* slot = out + (ci & 1) * G::kSlot;
     const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
@@ -497,14 +555,24 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   load_other(oa, 0);
   for (int ci = 0; ci < nchB; ci += 2) {
     load_other(ob, ci + 1 < last ? ci + 1 : last);
-    barrier_lds();
+    barrier_lds(&dg);
     drainB(ci, oa);
     if (ci + 1 >= nchB) break;
     load_other(oa, ci + 2 < last ? ci + 2 : last);
-    barrier_lds();
+    barrier_lds(&dg);
     drainB(ci + 1, ob);
   }
-  if (FWD) ll.write(a, b0, lane);
+  // the forward side has nchB chunks when T - H > H (odd T): the last one is
+  // the forward partner's or the backward partner's by its parity like the rest
+  dg.write(a.diag, FWD ? 2 : 3, lane);
+  // the forward ring slot the last chunk did not use (its readers passed the last loop barrier)
+  double* share = const_cast<double*>(fring) + ((((nchB > 0 ? nchB : 1) - 1) & 1) ^ 1) * G::kSlot;
+  if (!FWD) ll.put(share, lane);
+  barrier_lds();                                 // the block's closing barrier
+  if (FWD) {
+    ll.take(share, lane);
+    ll.write(a, b0, lane);
+  }
 }
 
 // FILT: forward_inference (filtering only): waves 0 (filter) and 1 (partner), H = T
@@ -526,17 +594,50 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
 
   for (int i = tid; i < a.tab_rows * G::NP; i += kThreads) tab[(i / G::NP) * G::NPS + i % G::NP] = a.tab[i];
   const int nseq = (int)((a.B - b0) < kWSeq ? (a.B - b0) : kWSeq);
+  // the block's 16 sequences are one contiguous [16][T][n_obs] int32 run
+  // (the usual layout): 16-byte loads, all of a thread's issued before any is
+  // unpacked; otherwise (strided views, a partial block) one element at a time
+  const int W = a.obs_tstride;
+  const bool fast = a.ncol > 0 && a.obs_bstride == (long)T * W && nseq == kWSeq;
   for (int k = 0; k < ncol; k++) {
     const int M = a.ncol > 0 ? a.M[k] : 0;
     uint8_t* ck = codes + (size_t)k * kWSeq * Tr;
     for (int i = tid; i < kWSeq * Tr; i += kThreads) {
       const int cq = i / Tr, t = i - cq * Tr - kWG;
       int c = M;                                            // missing / guard / absent sequence
-      if (a.ncol > 0 && cq < nseq && t >= 0 && t < T) {
+      if (!fast && a.ncol > 0 && cq < nseq && t >= 0 && t < T) {
         const int o = a.obs[(b0 + cq) * a.obs_bstride + (long)t * a.obs_tstride + a.col[k]];
         c = o < 0 ? M : (o < M ? o : M + 1);
       }
       ck[i] = (uint8_t)c;
+    }
+  }
+  if (fast) {
+    __syncthreads();                                        // guards before the interior
+    const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * a.obs_bstride);
+    const int n4 = (kWSeq * T * W) >> 2;                    // 16 T W is a multiple of 4
+    constexpr int kU = 8;                                   // loads in flight per thread
+    for (int i0 = tid; i0 < n4; i0 += kThreads * kU) {
+      int4 r[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++)
+        if (i0 + u * kThreads < n4) r[u] = src[i0 + u * kThreads];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int i4 = i0 + u * kThreads;
+        if (i4 >= n4) break;
+        const int v[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int i = 4 * i4 + e, cq = i / (T * W), rem = i - cq * T * W, t = rem / W, col = rem - t * W;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            if (k >= a.ncol || a.col[k] != col) continue;
+            const int M = a.M[k], o = v[e];
+            codes[(size_t)k * kWSeq * Tr + cq * Tr + kWG + t] = (uint8_t)(o < 0 ? M : (o < M ? o : M + 1));
+          }
+        }
+      }
     }
   }
   __syncthreads();
@@ -551,11 +652,11 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
     const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
                       (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
     if (pvec) {
-      if (fwd) wpartner<true, true, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
-      else wpartner<false, true, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, true, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, true, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
     } else {
-      if (fwd) wpartner<true, false, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
-      else wpartner<false, false, NT, FILT>(a, ring, zr, Sblk, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, false, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, false, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
     }
     return;
   }
@@ -576,6 +677,7 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   }
   if (fwd) wfilter<true, NT, NC>(a, c, Sblk, lane, nchA, nchB);
   else if (!FILT) wfilter<false, NT, NC>(a, c, Sblk, lane, nchA, nchB);
+  if (!FILT) barrier_lds();                       // the block's closing barrier (wpartner)
 }
 
 }  // namespace

@@ -750,8 +750,32 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     w.post = dst;
     w.post_bstride = dbs; w.post_tstride = dts; w.post_off = doff;
     w.ll = d_ll; w.status = d_status;
+#ifdef NIPAMD_DIAGNOSTICS
+    static const bool mtimes = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
+    const int nblk = (B + 15) / 16;
+    if (mtimes && !filt) {
+      HIP_OK(hipMalloc(&w.diag, (size_t)nblk * 16 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(w.diag, 0, (size_t)nblk * 16 * sizeof(unsigned long long), (hipStream_t)stream));
+    }
+#endif
     if (nipamd::chain_mfma_wide_launch(w, NT, filt, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+#ifdef NIPAMD_DIAGNOSTICS
+    if (w.diag) {
+      std::vector<unsigned long long> h((size_t)nblk * 16);
+      HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+      HIP_OK(hipMemcpy(h.data(), w.diag, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      (void)hipFree(w.diag);
+      double m[16] = {0};
+      for (int k = 0; k < nblk; k++)
+        for (int i = 0; i < 16; i++) m[i] += (double)h[(size_t)k * 16 + i] / nblk;
+      static const char* names[4] = {"fwd filter", "bwd filter", "fwd partner", "bwd partner"};
+      std::fprintf(stderr, "[nipamd] mfma_wide cycles per wave (phase A / its barrier waits / phase B / its barrier waits):\n");
+      for (int v = 0; v < 4; v++)
+        std::fprintf(stderr, "[nipamd]   %-12s %9.0f %9.0f %9.0f %9.0f\n", names[v], m[v * 4], m[v * 4 + 1], m[v * 4 + 2],
+                     m[v * 4 + 3]);
+    }
+#endif
     return 0;
   }
   if (kind == kWide64) {
