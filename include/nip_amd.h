@@ -243,6 +243,18 @@ int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,
 int nipamd_estep_finalize(nipamd_model* m, const double* d_partial,
                           double* d_counts, void* stream);
 
+/*
+ * The e_step's verdict on a leading run of missing observations: the first
+ * step k < T at which the reference's e_step rejects (BAD_LUCK, nip.c:1836-
+ * 1840) a series that observed nothing at steps 0..k -- its running ll of pure
+ * rounding turned > 0, or a mass was <= 0 -- or -1 if no such step exists.
+ * nipamd_estep / _partial set NIPAMD_STATUS_BAD_LUCK on every such series in
+ * d_status.  Computed on the host once per model version (the join tree's
+ * state over missing steps does not depend on the data); -2 when the model's
+ * tables exceed 2^20 entries, whose leading missing runs are not simulated.
+ */
+int nipamd_estep_prefix_first_bad(nipamd_model* m, int T);
+
 /* m_step() (src/nip.c:2010-2071): normalise params (host, em_learn layout)
  * and re-initialise the model's tables and priors from them. */
 int nipamd_m_step(nipamd_model* m, const double* params);

@@ -50,7 +50,7 @@ EXPORTS = [
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error", "nipamd_last_kernel",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
-    "nipamd_estep_finalize", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
+    "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
     "nipamd_series_data", "nipamd_series_free", "nipamd_write_uncertainseries",
@@ -103,6 +103,7 @@ def lib():
         L.nipamd_estep_partial_size.argtypes = [vp]
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
+        L.nipamd_estep_prefix_first_bad.argtypes = [vp, C.c_int]
         L.nipamd_estep_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp]
         L.nipamd_m_step.argtypes = [vp, dp]
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
@@ -231,6 +232,12 @@ class Model:
         """Doubles in an e_step partial (nipamd_estep_partial_size): the count
         body plus the 2-slot route tag; -1 without an e_step plan."""
         return lib().nipamd_estep_partial_size(self._h)
+
+    def estep_prefix_first_bad(self, T: int) -> int:
+        """nipamd_estep_prefix_first_bad: the first step k < T at which the
+        reference's e_step rejects a series that observed nothing at steps
+        0..k (-1: none; -2: model too large to simulate).  Host only."""
+        return lib().nipamd_estep_prefix_first_bad(self._h, int(T))
 
     def estep_supported(self) -> bool:
         """Whether the batched e_step has a GPU plan for this model under the

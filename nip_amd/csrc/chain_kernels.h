@@ -226,6 +226,9 @@ int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
 // the e_step partial's route tag: tag[0] = a, tag[1] = b
 int estep_tag_launch(double* tag, double a, double b, hipStream_t stream);
+// BAD_LUCK for sequences missing every observation at steps 0..first_bad (prefix.cpp)
+int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, uint32_t* status,
+                             hipStream_t stream);
 // counts[p] += sum_j coef[j] * R[idx[j]] over j in [ptr[p], ptr[p + 1]) (a
 // linear map of the reduced slab, e.g. a joint interface's counts projected
 // onto every family), in index order

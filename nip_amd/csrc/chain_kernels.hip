@@ -570,6 +570,30 @@ int estep_tag_launch(double* tag, double a, double b, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The e_step's verdict on a leading missing run (prefix.cpp): a sequence
+// whose observations at steps 0..first_bad are all missing (< 0) gets
+// BAD_LUCK.  One thread per sequence; almost every sequence leaves at its
+// first step, so the launch reads a few bytes per sequence.
+__global__ void estep_prefix_flag_kernel(const int32_t* obs, long bstride, int n_obs, int B, int first_bad,
+                                         uint32_t* status) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int32_t* o = obs + (long)b * bstride;
+  for (int t = 0; t <= first_bad; t++)
+    for (int c = 0; c < n_obs; c++)
+      if (o[(long)t * n_obs + c] >= 0) return;
+  status[b] |= 2u;                                   // NIPAMD_STATUS_BAD_LUCK
+}
+
+int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, uint32_t* status,
+                             hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (first_bad < 0 || first_bad >= T || (n_obs > 0 && !obs)) return -1;
+  hipLaunchKernelGGL(estep_prefix_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, obs,
+                     (long)T * n_obs, n_obs, B, first_bad, status);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream) {
   hipLaunchKernelGGL(estep_finalize_kernel, dim3(1), dim3(256), 0, stream, R, f, counts);
   return hipGetLastError() == hipSuccess ? 0 : -1;

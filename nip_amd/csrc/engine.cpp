@@ -1109,11 +1109,54 @@ static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_var
   return chain_estep_kernel(mm, T) != 0;
 }
 
+// The reference's verdict on a leading run of missing observations
+// (prefix.cpp), once per model version and T; -1: no step is rejected.
+// Models whose join tree has more than kPrefixMaxEntries table entries are
+// not simulated (-2: their leading missing runs are accepted).
+constexpr long kPrefixMaxEntries = 1L << 20;
+
+static int prefix_first_bad(nipamd_model* mm, int T) {
+  const int c = mm->pf_first_bad;
+  const bool hit = mm->pf_version == mm->version && (c == -2 || c >= 0 || T <= mm->pf_T);
+  if (!hit) {
+    mm->pf_first_bad = nipamd::estep_prefix_entries(mm->m) > kPrefixMaxEntries
+                           ? -2 : nipamd::estep_prefix_first_bad(mm->m, T, nullptr);
+    mm->pf_version = mm->version;
+    mm->pf_T = T;
+  }
+  const int k = mm->pf_first_bad;
+  return k >= 0 && k < T ? k : -1;
+}
+
+static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                                int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
+                                void* stream);
+
 int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                          int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
                          void* stream) {
   if (!mm || B < 0 || T < 1 || !d_partial || (n_obs > 0 && (!d_obs || !obs_vars)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (int rc = estep_partial_routes(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
+    return rc;
+  if (!d_status || B == 0) return 0;
+  // the kernels are queued: this host work overlaps them
+  const int k = prefix_first_bad(mm, T);
+  if (k < 0) return 0;
+  if (nipamd::estep_prefix_flag_launch(d_obs, n_obs, B, T, k, d_status, (hipStream_t)stream))
+    return fail(NIPAMD_ERROR_DEVICE, "prefix flag launch failed");
+  return 0;
+}
+
+int nipamd_estep_prefix_first_bad(nipamd_model* mm, int T) {
+  if (!mm || T < 1) { fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments"); return -2; }
+  if (nipamd::estep_prefix_entries(mm->m) > kPrefixMaxEntries) return -2;
+  return prefix_first_bad(mm, T);
+}
+
+static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                                int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
+                                void* stream) {
   Route r;
   if (!chain_estep_ok(mm, n_obs, obs_vars, T, r)) {
     if (mm->engine == NIPAMD_ENGINE_CHAIN)

@@ -153,6 +153,10 @@ struct nipamd_model {
   double fold_ms = 0.0;          // the last GPU fold: kernel time and clique bytes streamed
   double fold_bytes = 0.0;
   void* lik = nullptr;           // likelihood.hip: device tables of the last column set
+  // prefix.cpp: the e_step's leading-missing-run verdict for `version`, valid
+  // for T <= pf_T (-1: none below pf_T; -2: not decided, model too large)
+  unsigned pf_version = 0;
+  int pf_T = 0, pf_first_bad = -1;
 };
 
 namespace nipamd {
@@ -162,6 +166,10 @@ int chain_fold_gpu(const Model& m, int keep, std::vector<double>& out, double* m
                    std::string& err);
 // engine.cpp: complete a deferred fold (ChainPlan::fold_gpu) before host use of A64
 int ensure_fold(nipamd_model* mm);
+// prefix.cpp: the first step k < T at which the reference's e_step rejects a
+// series that observed nothing at steps 0..k (-1: none)
+int estep_prefix_first_bad(const Model& m, int T, int* steps);
+long estep_prefix_entries(const Model& m);
 // likelihood.hip: drop a model's cached likelihood tables (nipamd_model_free)
 void likelihood_release(nipamd_model* mm);
 // generate.cpp: drop a model's cached generate_data tables (nipamd_model_free)

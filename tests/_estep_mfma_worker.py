@@ -51,7 +51,7 @@ def vs_oracle(N, M, B, T):
     cnt, ll, st = gpu_estep(m, obs, ov)
     assert nip_amd.last_kernel() == "chain_fb_mfma_kernel<estep>", nip_amd.last_kernel()
     rc, rl, rb = PortOracle(m.desc()).estep(obs, ov, np.ones(m.param_size()))
-    assert not st.any()
+    assert np.array_equal(st != 0, rb != 0)        # incl. the leading-missing-run verdict
     ok = rb == 0
     assert close(ll[ok], rl[ok], LL_RTOL)
     if ok.all():
@@ -75,6 +75,7 @@ def missing_and_bad_luck():
     assert ll[0] == 0.0
     _, rl, rb = PortOracle(m.desc()).estep(obs, ov, np.ones(m.param_size()))
     assert (st[2] & nip_amd.STATUS_BAD_LUCK) != 0 and rb[2] != 0
+    assert np.array_equal(st != 0, rb != 0)
     good = rb == 0                                 # the sequences the reference accepts
     assert good.sum() >= 17
     cg, _, sg = gpu_estep(m, obs[good], ov)

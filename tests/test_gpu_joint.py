@@ -162,7 +162,6 @@ def test_joint_estep_equals_general_engine(name, spec, osym, T):
     assert m.estep_supported()
     rng = np.random.default_rng(T + 11)
     obs = make_obs(rng, 23, T, [m.card(ov[0])], missing=0.25)
-    obs[:, 0] = np.maximum(obs[:, 0], 0)          # the reference's BAD_LUCK rule on leading missing runs
     ca, la, sa = estep(m, obs, ov)
     m.set_engine(nip_amd.ENGINE_JTREE)
     cb, lb, sb = estep(m, obs, ov)
@@ -195,3 +194,17 @@ def test_joint_estep_vs_oracle():
         assert not rb.any() and not st.any()
         assert close_ll(ll, rl)
         assert np.allclose(c, rc, rtol=1e-11, atol=0), (obs.shape, np.abs(c - rc).max())
+    # leading missing runs of every length: the reference's BAD_LUCK verdict
+    # (prefix.cpp) flag for flag, parity on the sequences it accepts
+    T = 30
+    obs = rng.integers(0, 16, size=(T + 1, T, 1)).astype(np.int32)
+    for L in range(T + 1):
+        obs[L, :L] = -1
+    c, ll, st = estep(m, obs, ov)
+    rc, rl, rb = orc.estep(obs, ov, np.ones(m.param_size()))
+    assert np.array_equal((st & nip_amd.STATUS_BAD_LUCK) != 0, rb != 0)
+    ok = rb == 0
+    assert close_ll(ll[ok], rl[ok])
+    c, _, _ = estep(m, obs[ok], ov)
+    rc, _, _ = orc.estep(obs[ok], ov, np.ones(m.param_size()))
+    assert np.allclose(c, rc, rtol=1e-11, atol=0), np.abs(c - rc).max()

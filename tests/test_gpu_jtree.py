@@ -25,6 +25,7 @@ import nip_amd
 from nip_amd import synth
 from nip_amd.em import em_learn, NIP_NO_ERROR, NIP_ERROR_BAD_LUCK
 from oracle.bind import PortOracle
+from em_util import check_em_curve
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 GEN = sorted(glob.glob(os.path.join(GOLD, "gen_*.npz")))
@@ -94,12 +95,9 @@ def test_general_estep_matches_reference(path):
     cnt, ll, st = nip_amd.e_step(m, o, ov)
     cnt, ll, st = cnt.cpu().numpy(), ll.cpu().numpy(), st.cpu().numpy()
     bad = z["estep_bad"] != 0
-    mine = (st & nip_amd.STATUS_BAD_LUCK) != 0
-    # the reference's missing-value rounding quirk can only add BAD_LUCK flags
-    # (DESIGN.md 6); every sequence it accepts must be accepted here
-    assert not np.any(mine & ~bad)
-    has_gap = (z["obs"] < 0).any(axis=(1, 2))
-    assert np.all(mine[bad] | has_gap[bad])
+    # flag for flag, including the verdict on leading missing runs (prefix.cpp)
+    assert np.array_equal(st != 0, bad)
+    assert close_ll(ll[~bad], z["estep_ll"][~bad])
     if not bad.any():
         assert close_ll(ll, z["estep_ll"])
         assert np.all(np.abs(cnt - z["counts"]) <= CNT_RTOL * np.maximum(1.0, np.abs(z["counts"])))
@@ -108,19 +106,11 @@ def test_general_estep_matches_reference(path):
 @pytest.mark.parametrize("path", GEN, ids=[os.path.basename(p) for p in GEN])
 def test_general_em_learn_curve(path):
     z = np.load(path)
-    if (z["obs"] < 0).any() or z["estep_bad"].any():
-        pytest.skip("missing data: the reference's BAD_LUCK rounding quirk (DESIGN.md 6)")
     m = gen_model(z)
     obs = torch.from_numpy(np.ascontiguousarray(z["obs"])).cuda()
     curve = []
     rc = em_learn(m, obs, list(z["obs_vars"]), 1e-6, curve, init=z["em_init"], max_iterations=8)
-    it = int(z["em_iters"])
-    ref = z["em_curve"]
-    n = it if it >= 0 else int(np.argmax(np.append(ref, 0.0) == 0.0))
-    assert len(curve) >= n
-    assert np.all(np.abs(np.array(curve[:n]) - ref[:n]) <= 1e-10 * np.abs(ref[:n]))
-    if it >= 0:
-        assert rc == NIP_NO_ERROR and len(curve) == it
+    check_em_curve(z, rc, curve, 1e-10)
 
 
 CHAIN_CASES = [

@@ -26,7 +26,6 @@ from nip_amd import build, synth
 import slice_util as su
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "tests", "_bin", "asan")
 SAN = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
 ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
 
@@ -37,8 +36,8 @@ def _cc(cmd):
 
 
 @pytest.fixture(scope="module")
-def asan_port():
-    os.makedirs(OUT, exist_ok=True)
+def asan_port(tmp_path_factory):
+    OUT = str(tmp_path_factory.mktemp("asan_port"))     # per worker: no build races under xdist
     so = os.path.join(OUT, "libnip_oracle_asan.so")
     _cc(["gcc", *SAN, "-fPIC", "-std=gnu99", "-w", "-fopenmp", "-shared", "-o", so,
          os.path.join(ROOT, "oracle", "nip_oracle.c"), "-lm"])
@@ -95,8 +94,8 @@ def test_oracle_port_under_asan_ubsan(asan_port):
 
 
 @pytest.fixture(scope="module")
-def asan_compat():
-    os.makedirs(OUT, exist_ok=True)
+def asan_compat(tmp_path_factory):
+    OUT = str(tmp_path_factory.mktemp("asan_compat"))
     inc = ["-I" + os.path.join(ROOT, "include", "compat"), "-I" + os.path.join(ROOT, "include")]
     lib = os.path.join(OUT, "libnip.so")
     srcs = sorted(os.path.join(ROOT, "nip_amd", "compat", f) for f in os.listdir(os.path.join(ROOT, "nip_amd", "compat"))
