@@ -61,6 +61,7 @@ N_CU = 256
 # kernel -> (cycles per filter step, sequences per block, blocks resident per CU)
 LATENCY_STEP = {
     "chain_fb_ckpt_kernel": (328.0, 16, 1),            # 4 chained v_mfma_f64_16x16x4, D -> next B
+    "chain_fb_ckpt_kernel<proj>": (328.0, 16, 1),
     "chain_fb_mfma_kernel": (328.0, 16, 1),
     "chain_mfma_wide_kernel<1>": (328.0, 16, 1),
     "chain_mfma_wide_kernel<2>": (1136.1, 16, 1),      # 2 x 8 chained, interleaved (93 KB LDS: 1 block/CU)
@@ -311,10 +312,17 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
     elif name == "joint":
         K = 16                         # joint interface states (X1, Y1)
-        kb, _ = kernel_bytes(kname, K, len(ov), True)
-        bpu, bnote = kb + 8 * K + 8 * N, ("the chain kernel's bytes at K = 16 joint states, then the "
-                                          "projection: the joint posterior read back, X1's marginal written")
-        kname += " + project_kernel"
+        if kname == "chain_fb_ckpt_kernel<proj>":
+            # X1's marginal written by the chain kernel itself (chain_ckpt.hip norm_store)
+            ck = 8 * K // 4
+            bpu, bnote = 4 * len(ov) + 2 * ck + 8 * N, (
+                "obs %d + every 4th joint message as a checkpoint (%d written + %d read) + X1's marginal %d, "
+                "written by the chain kernel (the joint posterior stays on chip)" % (4 * len(ov), ck, ck, 8 * N))
+        else:
+            kb, _ = kernel_bytes(kname, K, len(ov), True)
+            bpu, bnote = kb + 8 * K + 8 * N, ("the chain kernel's bytes at K = 16 joint states, then the "
+                                              "projection: the joint posterior read back, X1's marginal written")
+            kname += " + project_kernel"
         workload = ("joint-interface chain: factorial HMM, X and Y 4 states each, O1 16 states of both, "
                     "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
         metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (joint-interface chain kernels)"

@@ -235,7 +235,7 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
 // (lane L: chain 8 part + (L & 7), slot step L >> 3), written over o; then
 // each chain's 8 steps leave as one contiguous 1 KB run per store
 // instruction (lane L: step L >> 3 in address order, piece L & 7).
-template <bool FWD>
+template <bool FWD, int PROJ>
 __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fslot, double* rslot, int part,
                                            int lane, long b0, int ci, double* sink) {
   const int T = a.T, H = a.H;
@@ -256,6 +256,44 @@ __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fsl
     double z0 = pr[0] + pr[1], z1 = pr[2] + pr[3], z2 = pr[4] + pr[5], z3 = pr[6] + pr[7];
     z0 += pr[8] + pr[9]; z1 += pr[10] + pr[11]; z2 += pr[12] + pr[13]; z3 += pr[14] + pr[15];
     const double r = recip((z0 + z1) + (z2 + z3));    // an all-zero row stays zero
+    if constexpr (PROJ > 0) {
+      // joint interface: each requested variable's marginal straight from the
+      // normalised joint posterior -- digit sums in increasing joint-state
+      // order, then normalised, as derive.hip's project_digit + its
+      // normaliser do on the stored joint (same operations, same bits: a
+      // term outside the digit is an fma with 0, one inside an fma with 1,
+      // i.e. the same add); the joint itself never leaves the CU.  PROJ
+      // accumulators per variable (its cardinality <= PROJ).
+      const int t = FWD ? tB + ci * kMChunk + k : tB - ci * kMChunk - k;
+      const long b = b0 + c;
+      if (ci * kMChunk + k < nB && b < a.B) {
+        double* const dst = a.post + (size_t)b * a.post_bstride + (long)t * a.post_tstride;
+        double nv[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) nv[i] = pr[i] * r;
+        for (int jv = 0; jv < a.nproj; jv++) {
+          double sd[PROJ > 0 ? PROJ : 1];
+#pragma unroll
+          for (int d = 0; d < PROJ; d++) sd[d] = 0.0;
+#pragma unroll
+          for (int i = 0; i < 16; i++) {
+            const int dig = a.proj_digit[jv][i];
+#pragma unroll
+            for (int d = 0; d < PROJ; d++) sd[d] = __builtin_fma(nv[i], dig == d ? 1.0 : 0.0, sd[d]);
+          }
+          double zm = 0.0;
+#pragma unroll
+          for (int d = 0; d < PROJ; d++) zm += sd[d];
+          const double rz = zm != 0.0 ? 1.0 / zm : 1.0;
+          const int card = a.proj_card[jv];
+          double* const o = dst + a.proj_off[jv];
+#pragma unroll
+          for (int d = 0; d < PROJ; d++)
+            if (d < card) o[d] = zm != 0.0 ? sd[d] * rz : sd[d];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < 8; p++)
       *reinterpret_cast<double2*>(rslot + ck_off(k, c, p)) = make_double2(pr[2 * p] * r, pr[2 * p + 1] * r);
@@ -278,7 +316,7 @@ __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fsl
   }
 }
 
-template <bool FWD>
+template <bool FWD, int PROJ>
 __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, double* rring, const double* zr,
                                            double* Sblk, int lane, long b0, int nchA, int nchB, CkDiag& dg) {
   const int T = a.T, H = a.H;
@@ -370,12 +408,13 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
       }
       ll.renorm();
     }
-    norm_store<FWD>(a, out + (ci & 1) * kSlotD, rring + (ci & 1) * kSlotD, 0, lane, b0, ci, sink);
+    norm_store<FWD, PROJ>(a, out + (ci & 1) * kSlotD, rring + (ci & 1) * kSlotD, 0, lane, b0, ci, sink);
   }
   if (FWD) ll.write(a, b0, lane, 1u);
   barrier_lds();                                     // the block's closing barrier
 }
 
+template <int PROJ>
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* out = reinterpret_cast<double*>(smem);     // filter rings [2 dirs][2 slots][8][16][16]
@@ -417,16 +456,16 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
     const int side = f ? 0 : 2 * kSlotD;
     for (int ci = 0; ci < nchB; ci++) {
       barrier_lds(&dg.wb);
-      if (f) norm_store<true>(a, out + side + (ci & 1) * kSlotD, rr + side + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
-      else norm_store<false>(a, out + side + (ci & 1) * kSlotD, rr + side + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
+      if (f) norm_store<true, PROJ>(a, out + side + (ci & 1) * kSlotD, rr + side + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
+      else norm_store<false, PROJ>(a, out + side + (ci & 1) * kSlotD, rr + side + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
     }
     barrier_lds();
     dg.write(a, wave, lane);
     return;
   }
   if (role >= 2 && wave < 4) {
-    if (fwd) ck_partner<true>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
-    else ck_partner<false>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
+    if (fwd) ck_partner<true, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
+    else ck_partner<false, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
     dg.write(a, wave, lane);
     return;
   }
@@ -470,12 +509,32 @@ int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream) {
   const bool pvec = a.post && a.N == 16 && a.post_tstride == 16 &&
                     ((a.post_off | (int)(a.post_bstride & 1)) & 1) == 0 &&
                     ((reinterpret_cast<uintptr_t>(a.post) & 15) == 0);
-  if (lds > 160 * 1024 || !pvec || a.T < 2) return -2;
-  static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel), lds, lds_set)) return -1;
+  const bool proj = a.post && a.nproj > 0 && a.nproj <= 4;
+  if (lds > 160 * 1024 || !(proj || (pvec && a.nproj == 0)) || a.T < 2) return -2;
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
-  hipLaunchKernelGGL(chain_fb_ckpt_kernel, dim3(blocks), dim3(kCThreads), lds, stream, a);
-  g_last_kernel = "chain_fb_ckpt_kernel";
+  if (proj) {
+    int cmax = 0;
+    for (int jv = 0; jv < a.nproj; jv++) cmax = a.proj_card[jv] > cmax ? a.proj_card[jv] : cmax;
+    if (cmax <= 4) {
+      static size_t s4[kMaxDevices] = {};
+      if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<4>), lds, s4)) return -1;
+      hipLaunchKernelGGL(chain_fb_ckpt_kernel<4>, dim3(blocks), dim3(kCThreads), lds, stream, a);
+    } else if (cmax <= 8) {
+      static size_t s8[kMaxDevices] = {};
+      if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<8>), lds, s8)) return -1;
+      hipLaunchKernelGGL(chain_fb_ckpt_kernel<8>, dim3(blocks), dim3(kCThreads), lds, stream, a);
+    } else {
+      static size_t s16[kMaxDevices] = {};
+      if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<16>), lds, s16)) return -1;
+      hipLaunchKernelGGL(chain_fb_ckpt_kernel<16>, dim3(blocks), dim3(kCThreads), lds, stream, a);
+    }
+    g_last_kernel = "chain_fb_ckpt_kernel<proj>";
+  } else {
+    static size_t lds_set[kMaxDevices] = {};
+    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<0>), lds, lds_set)) return -1;
+    hipLaunchKernelGGL(chain_fb_ckpt_kernel<0>, dim3(blocks), dim3(kCThreads), lds, stream, a);
+    g_last_kernel = "chain_fb_ckpt_kernel";
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

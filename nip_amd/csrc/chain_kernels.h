@@ -45,6 +45,13 @@ struct ChainArgs {
   unsigned* status;      // [B] or nullptr
   double* counts;        // E-step only: per-sequence slabs [B][chain_estep_slab(M)]
   unsigned long long* diag;   // diagnostics builds only: per-block wall-clock stamps, else null
+  // chain_fb_ckpt_kernel, joint interface: write the marginals of up to four of
+  // its variables instead of the joint posterior (post_tstride = their summed
+  // cardinalities).  proj_digit[j][i]: variable j's value at joint state i (-1
+  // for a padding state); its marginal goes to proj_off[j] .. + proj_card[j].
+  int nproj;
+  int proj_off[4], proj_card[4];
+  signed char proj_digit[4][16];
 };
 
 // Scratch layout: per sequence kGuard + T + kGuard steps of 16 doubles

@@ -884,6 +884,53 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
 }
 
 
+// Joint interface, smoothing, every query one of the interface's current-slice
+// variables: chain_fb_ckpt_kernel writes their marginals itself (digit sums of
+// the normalised joint posterior, chain_ckpt.hip norm_store) instead of the
+// joint posterior plus one project_kernel pass per variable.  *taken = false
+// when the checkpoint kernel does not take the request (the caller falls back).
+static int launch_joint_marginals(nipamd_model* mm, const Route& r, ReqTables* rt, const int32_t* d_obs,
+                                  int n_obs, int B, int T, int n_query, const int* query, double* d_post,
+                                  double* d_ll, uint32_t* d_status, void* stream, bool* taken) {
+  *taken = false;
+  const auto& P = mm->m.chain;
+  if (!P.joint || P.N > 16 || n_query < 1 || n_query > 4) return 0;
+  nipamd::ChainArgs a{};
+  int stride = 0;
+  for (int i = 0; i < n_query; i++) {
+    const int kind = query_kind(P, query[i]);
+    if (kind < 700 || kind >= 1000) return 0;
+    const int k = kind - 700;
+    int st = 1;
+    for (int j = 0; j < k; j++) st *= mm->m.vars[P.jcur[j]].card;
+    const int card = mm->m.vars[P.jcur[k]].card;
+    a.proj_off[i] = stride;
+    a.proj_card[i] = card;
+    for (int s = 0; s < 16; s++) a.proj_digit[i][s] = (signed char)(s < P.N ? (s / st) % card : -1);
+    stride += card;
+  }
+  a.nproj = n_query;
+  if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes(B, T))) return rc;
+  DevState* d = dev_of(mm);
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  a.obs = r.pcol >= 0 ? d_obs : nullptr;
+  a.obs_bstride = (long)T * ocols;
+  a.obs_tstride = (int)ocols;
+  a.obs_col = r.pcol;
+  a.B = B; a.T = T; a.H = T / 2; a.N = P.N; a.M = rt->M0;
+  a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
+  a.post = d_post;
+  a.post_bstride = (long)T * stride;
+  a.post_tstride = stride;
+  a.ll = d_ll;
+  a.status = d_status;
+  const int rc = nipamd::chain_fb_ckpt_launch(a, (hipStream_t)stream);
+  if (rc == -2) return 0;
+  if (rc) return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  *taken = true;
+  return 0;
+}
+
 // forward_backward_inference (filt = false) / forward_inference (filt = true).
 // The interface variable's marginals come from the chain kernels; every
 // other queried variable's are derived from them (derive.hip), with the
@@ -914,6 +961,13 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     if (mm->engine == NIPAMD_ENGINE_CHAIN) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
     return nipamd::jt_fb(mm, d_obs, n_obs, obs_vars, B, T, n_query, query, d_post, d_ll, d_status,
                          stream, filt);
+  }
+  if (!filt && kk == kNarrowMfma && mm->m.chain.joint) {
+    bool taken = false;
+    if (int rc = launch_joint_marginals(mm, r, rt, d_obs, n_obs, B, T, n_query, query, d_post, d_ll, d_status,
+                                        stream, &taken))
+      return rc;
+    if (taken) return 0;
   }
   const auto& P = mm->m.chain;
   std::vector<int> kind(n_query), off(n_query);

@@ -92,3 +92,26 @@ def test_deferred_fold_fb_matches_oracle_64_states():
     rp, rl = PortOracle(m.desc()).fb(obs[0], ov, q)
     assert np.abs(post[0] - rp).max() <= 1e-12
     assert abs(ll[0] - rl) <= 1e-11 * max(1.0, abs(rl))
+
+
+def test_config5_full_size_vs_textbook():
+    """Config 5 at its bench size (256 x 128, 64 states) through the deferred
+    fold and chain_wide4_kernel, every sequence against the textbook smoother
+    over the model's own tables (tests/textbook_util.py)."""
+    from textbook_util import chain_tables, smoother
+    m = nip_amd.Model.from_spec(*synth.wide_spec(64, 16))
+    X0, X1, O1 = m.variable("X0"), m.variable("X1"), m.variable("O1")
+    obs = synth.observations(256, 128, 16, seed=6)
+    obs[7, :5, 0] = -1                                  # a leading missing run
+    obs[9, 40:50, 0] = -1
+    o = torch.from_numpy(obs).cuda()
+    post, ll, st = nip_amd.forward_backward_inference(m, o, [O1], [X1])
+    fpost, fll, _ = nip_amd.forward_inference(m, o, [O1], [X1])
+    torch.cuda.synchronize()
+    assert not st.any().item()
+    A, pi, Es = chain_tables(m, X0, X1, [O1])
+    tp, tf, tl = smoother(A, pi, Es, [obs[:, :, 0]])
+    assert np.abs(post.cpu().numpy() - tp).max() <= 1e-12
+    assert np.abs(fpost.cpu().numpy() - tf).max() <= 1e-12
+    assert np.all(np.abs(ll.cpu().numpy() - tl) <= 1e-11 * np.abs(tl))
+    assert np.all(np.abs(fll.cpu().numpy() - tl) <= 1e-11 * np.abs(tl))

@@ -100,6 +100,46 @@ def test_joint_chain_vs_oracle(name, spec, osyms, qsyms):
         assert close_ll([ll[b]], [rl])
 
 
+@pytest.mark.parametrize("name,spec,osyms,qsyms", [
+    ("factorial4x4", synth.factorial_spec(4, 4, 16), ["O1"], ["X1", "Y1"]),
+    ("factorial4x3", synth.factorial_spec(4, 3, 5), ["O1"], ["Y1"]),
+    ("coupled_one_obs", synth.coupled_spec(), ["B1"], ["Y1", "X1"]),      # 12 joint states: 4 padding
+], ids=["factorial4x4", "factorial4x3", "coupled_one_obs"])
+def test_joint_marginals_fused_into_chain_kernel(name, spec, osyms, qsyms):
+    """Queries that are all current interface variables: the checkpoint
+    kernel writes their marginals itself (chain_ckpt.hip norm_store, no joint
+    posterior in HBM).  Bit-identical to the unfused path -- joint posterior,
+    then project_kernel -- taken when the request also names a previous-slice
+    variable; and against the general engine and the oracle."""
+    m = nip_amd.Model.from_spec(*spec)
+    ov, q = [m.variable(v) for v in osyms], [m.variable(v) for v in qsyms]
+    rng = np.random.default_rng(len(name))
+    obs = make_obs(rng, 37, 41, [m.card(v) for v in ov], missing=0.15)
+    obs[3, :5] = -1
+    post, ll, st = run(m, obs, ov, q)
+    assert nip_amd.last_kernel() == "chain_fb_ckpt_kernel<proj>", nip_amd.last_kernel()
+    x0 = m.variable(qsyms[0][:-1] + "0")
+    post2, ll2, st2 = run(m, obs, ov, q + [x0])
+    assert nip_amd.last_kernel() != "chain_fb_ckpt_kernel<proj>"
+    w = post.shape[2]
+    joint16 = name.startswith("factorial4x4")
+    if joint16:        # 16 joint states: the unfused path runs the same kernel, storing the joint
+        assert np.array_equal(post, post2[:, :, :w])
+        assert np.array_equal(ll, ll2) and np.array_equal(st, st2)
+    else:              # fewer: the unfused path is chain_fb_mfma_kernel (16-wide rows only on ckpt)
+        assert np.abs(post - post2[:, :, :w]).max() <= POST_TOL
+        assert close_ll(ll, ll2) and np.array_equal(st, st2)
+    (pa, la, sa), (pb, lb, sb) = both_engines(m, obs, ov, q)
+    assert np.array_equal(pa, post)
+    assert np.abs(pa - pb).max() <= POST_TOL
+    assert close_ll(la, lb)
+    orc = PortOracle(m.desc())
+    for b in (0, 3, 36):
+        rp, rl = orc.fb(obs[b], ov, q)
+        assert np.abs(post[b] - rp).max() <= POST_TOL
+        assert close_ll([ll[b]], [rl])
+
+
 def test_joint_chain_zero_mass_and_ragged_batch():
     """Out-of-range codes (an all-zero likelihood) kill a sequence exactly as
     on the general engine; B not a multiple of the kernels' 16-sequence

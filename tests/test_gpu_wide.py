@@ -132,6 +132,45 @@ def test_config3_scale_properties():
         assert abs(ll[b].item() - rl) <= 1e-11 * abs(rl)
 
 
+def test_config3_full_size_properties_and_parity():
+    """Config 3 at its bench size: demo1 @ 32 states, 65,536 sequences x
+    T=256 (chain_mfma_wide_kernel<2>: every launch-grid and LDS path at full B).  Normalised posteriors, finite
+    ll <= 0, filter ll == smoothing ll and the last filtered step == the last
+    smoothed step; 1,024 sequences spread over the batch (first and last
+    block included) against the textbook smoother over the model's own
+    tables, two against the oracle."""
+    from textbook_util import chain_tables, smoother
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(32))
+    ov = [m.variable("A1"), m.variable("B1")]
+    q = [m.variable("C1")]
+    B, T = 65536, 256
+    obs_np = synth.observations(B, T, 32, seed=9, n_obs=2)
+    obs_np[B - 1, :4, :] = -1                           # a leading missing run, last sequence
+    obs_np[1000, 100:140, 0] = -1
+    obs = torch.from_numpy(obs_np).cuda()
+    post, ll, st = nip_amd.forward_backward_inference(m, obs, ov, q)
+    fpost, fll, fst = nip_amd.forward_inference(m, obs, ov, q)
+    torch.cuda.synchronize()
+    assert not st.any().item() and not fst.any().item()
+    s = post.sum(dim=2)
+    assert torch.allclose(s, torch.ones_like(s), atol=1e-12, rtol=0)
+    assert bool((ll <= 0).all()) and bool(torch.isfinite(ll).all())
+    assert bool(((fll - ll).abs() <= 1e-11 * ll.abs()).all())
+    assert float((post[:, -1] - fpost[:, -1]).abs().max()) <= 1e-12
+    idx = np.unique(np.concatenate([np.arange(0, B, 64), [1, 255, 256, 1000, B - 256, B - 2, B - 1]]))
+    A, pi, Es = chain_tables(m, m.variable("C0"), q[0], ov)
+    tp, tf, tl = smoother(A, pi, Es, [obs_np[idx, :, 0], obs_np[idx, :, 1]])
+    sel = torch.from_numpy(idx).cuda()
+    assert np.abs(post[sel].cpu().numpy() - tp).max() <= 1e-12
+    assert np.abs(fpost[sel].cpu().numpy() - tf).max() <= 1e-12
+    assert np.all(np.abs(ll[sel].cpu().numpy() - tl) <= 1e-11 * np.abs(tl))
+    orc = PortOracle(m.desc())
+    for b in (0, B - 1):
+        rp, rl = orc.fb(obs_np[b], ov, q)
+        assert np.abs(post[b].cpu().numpy() - rp).max() <= 1e-12
+        assert abs(ll[b].item() - rl) <= 1e-11 * abs(rl)
+
+
 # 33..64 states: chain_wide4_kernel (four filter waves per direction, one
 # barrier per step, sparse rescaling, partner waves for scratch/posterior/ll)
 @pytest.mark.parametrize("card,B,T", [(48, 3, 21), (40, 2, 2), (64, 2, 9), (33, 3, 1)])
