@@ -229,6 +229,12 @@ int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream);
 size_t chain_estep_mfma_lds_bytes(int M, int T);
 int chain_estep_mfma_launch(const ChainArgs& a, hipStream_t stream);
 int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
+// the default e_step kernel (chain_kernels.hip chain_estep16_kernel): 16
+// sequences per block, direction-uniform waves, analytic phase-B normalisation;
+// its scratch holds the messages plus one exponent per (sequence, step)
+int chain_estep16_launch(const ChainArgs& a, hipStream_t stream);
+size_t chain_estep16_lds_bytes(int M, int T);
+size_t chain_estep16_scratch_bytes(long B, int T);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
 // the e_step partial's route tag: tag[0] = a, tag[1] = b

@@ -469,6 +469,352 @@ void chain_kernel(ChainArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// e_step, direction-uniform waves (chain_estep16_kernel, the default e_step).
+//
+// The same two filters and per-sequence slab as chain_kernel<true>, with two
+// changes to the work per step (the kernel is bound by the SIMDs' f64 issue,
+// DESIGN.md 4):
+//  * waves are direction-uniform: a block holds 16 sequences, waves 0-3 run
+//    the forward rows (4 sequences each), waves 4-7 the backward rows, so
+//    each SIMD holds one wave of each direction, and the backward rows skip
+//    what only the ll needs (the m1 row sum, the mass products);
+//  * phase B normalises analytically: sum_y alpha_t(y) beta_t(y) = Z for
+//    every t, and both filters carry their scale as an exact power of two
+//    per step (alpha^_t = alpha_t 2^Ef_t, beta^_t = beta_t 2^Eb_t; the
+//    exponents travel with the phase-A messages through the scratch), so
+//    c_t = Z 2^(Ef_t + Eb_t): one row sum at the phase's first step gives
+//    1 / c_H, and every later step's posterior and xi weight is a multiply
+//    and an ldexp instead of a row sum, a division and a reciprocal.  The
+//    posteriors then sum to 1 within the filters' rounding drift (~1e-13
+//    relative over T = 1024), well inside DESIGN.md's count tolerance.
+// Per-sequence slabs (chain_estep_slab layout) as chain_kernel<true>, so
+// tree64_kernel and estep_finalize_kernel are shared.
+constexpr int kE16Seqs = 16;
+constexpr int kE16Threads = 512;
+
+namespace {
+
+__host__ __device__ inline long estep16_xrow(int T) { return (long)T + 2 * kGuard; }
+
+struct E16Ctx {
+  const double* Et;        // LDS evidence table, this lane's column (Et + y)
+  const uint8_t* codes;    // LDS codes of this sequence; codes[-kGuard .. T+kGuard)
+  const double* Sload;     // scratch message row of this sequence (+y)
+  double* Sstore;          // same, or a sink
+  long Sstride;            // 16, or 0 for the sink
+  const int* Xload;        // scratch exponent row of this sequence
+};
+
+template <int KC>
+struct Prefetch16 {
+  double e[KC];
+  double s[KC];
+  int c[KC];
+  int x[KC];
+};
+
+template <int KC>
+__device__ __forceinline__ void load_chunk16(const E16Ctx& c, Prefetch16<KC>& p, int t0, int dir, bool with_s) {
+  int code[KC];
+#pragma unroll
+  for (int j = 0; j < KC; j++) {
+    const int t = t0 + dir * j;
+    code[j] = c.codes[t];
+    if (with_s) { p.s[j] = c.Sload[(long)t * 16]; p.x[j] = c.Xload[t]; }
+  }
+#pragma unroll
+  for (int j = 0; j < KC; j++) { p.e[j] = c.Et[code[j] * 16]; p.c[j] = code[j]; }
+}
+
+template <int KC, typename Step>
+__device__ __forceinline__ void run_phase16(const E16Ctx& c, int n, int t0, int dir, bool with_s, Step&& step) {
+  Prefetch16<KC> pa, pb;
+  if (n <= 0) return;
+  load_chunk16(c, pa, t0, dir, with_s);
+  for (int base = 0; base < n; base += 2 * KC) {
+    load_chunk16(c, pb, t0 + dir * (base + KC), dir, with_s);
+#pragma unroll
+    for (int j = 0; j < KC; j++)
+      if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], pa.x[j], pa.c[j], j);
+    if (base + KC >= n) break;
+    load_chunk16(c, pa, t0 + dir * (base + 2 * KC), dir, with_s);
+#pragma unroll
+    for (int j = 0; j < KC; j++)
+      if (base + KC + j < n) step(t0 + dir * (base + KC + j), pb.e[j], pb.s[j], pb.x[j], pb.c[j], j);
+  }
+}
+
+// sum_k x[lane k] * c[k] with two accumulators (dot_bcast has four): two
+// zeroing moves and one add per mat-vec instead of four and three; the
+// other wave on the SIMD covers the longer fma chains
+__device__ __forceinline__ double dot2_bcast(double x, const double (&c)[16]) {
+  double a0 = 0.0, a1 = 0.0;
+  fmac_bcast<0, true>(a0, x, c[0]);   fmac_bcast<1, false>(a1, x, c[1]);
+  fmac_bcast<2, false>(a0, x, c[2]);  fmac_bcast<3, false>(a1, x, c[3]);
+  fmac_bcast<4, false>(a0, x, c[4]);  fmac_bcast<5, false>(a1, x, c[5]);
+  fmac_bcast<6, false>(a0, x, c[6]);  fmac_bcast<7, false>(a1, x, c[7]);
+  fmac_bcast<8, false>(a0, x, c[8]);  fmac_bcast<9, false>(a1, x, c[9]);
+  fmac_bcast<10, false>(a0, x, c[10]); fmac_bcast<11, false>(a1, x, c[11]);
+  fmac_bcast<12, false>(a0, x, c[12]); fmac_bcast<13, false>(a1, x, c[13]);
+  fmac_bcast<14, false>(a0, x, c[14]); fmac_bcast<15, false>(a1, x, c[15]);
+  return a0 + a1;
+}
+
+// One direction's rows of a block (FWD: waves 0-3, backward: waves 4-7).
+template <bool FWD>
+__device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* Et, const uint8_t* codes,
+                                             double* Htab, double* m1x, int lane, int wave, long b0) {
+  constexpr int KC = NIPAMD_ESTEP_CHUNK;
+  const int y = lane & 15, row = lane >> 4;
+  const int seq = (wave & 3) * 4 + row;             // 0..15 within the block
+  const long b = b0 + seq;
+  const bool active = b < a.B;
+  const int T = a.T, H = a.H, M = a.M;
+  const int Tr = chain_codes_row(T);
+
+  double C[16];   // forward: column y of A (C[k] = A[k][y]); backward: row y (A[y][k])
+#pragma unroll
+  for (int k = 0; k < 16; k++) C[k] = FWD ? a.A[k * 16 + y] : a.A[y * 16 + k];
+  const double s_y = Et[M * 16 + y];
+  // backward rows: (A s)(x) for lane x -- the phase-A steps' m1 (below)
+  double As = 0.0;
+  if (!FWD) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) As = __builtin_fma(C[k], Et[M * 16 + k], As);
+  }
+
+  const long nrow = (a.B + kE16Seqs - 1) / kE16Seqs * kE16Seqs;
+  double* const sink = a.S + (size_t)(nrow + 1) * chain_scratch_row(T) + y;
+  double* const Srow = a.S + (size_t)(active ? b : 0) * chain_scratch_row(T) + (size_t)kGuard * 16 + y;
+  int* const X = reinterpret_cast<int*>(a.S + (size_t)(nrow + 2) * chain_scratch_row(T));
+  int* const Xrow = X + (size_t)(active ? b : 0) * estep16_xrow(T) + kGuard;
+  E16Ctx cx;
+  cx.Et = Et + y;
+  cx.codes = codes + seq * Tr + kGuard;
+  cx.Sload = Srow;
+  cx.Sstore = active ? Srow : sink;
+  cx.Sstride = active ? 16 : 0;
+  cx.Xload = Xrow;
+  const bool xw = active && y == 0;
+
+  // chain state: x = this lane's entry of the next mat-vec input, ex its
+  // exponent (x = message * 2^ex): forward alpha^_{t-1}, backward
+  // g_{t+1} = e_{t+1} o beta^_{t+1}
+  double x;
+  int sc = 0, ex = 0;
+  // ll = sum_t log m2_t - log m1_t (nip.c:1461-1474): the forward rows carry
+  // the m2 of every step and the m1 of phase B; the m1 of phase A steps t < H,
+  // sum_y (A^T alpha^_{t-1})(y) s(y) 2^sc_t = (alpha^_{t-1} . A s) 2^sc_t, is
+  // summed by the backward rows in their phase B, where alpha^_{t-1} arrives
+  // from the scratch anyway (the exponents telescope to Ef_{H-1}), and handed
+  // over through LDS: the forward waves' phase A is the heavier one
+  double m2 = 1.0, m1 = 1.0;   // running products (mantissas)
+  int e2 = 0, e1 = 0;          // and their binary exponents
+  if (FWD) {
+    x = a.pi[y];
+  } else {
+    const double beta = y < a.N ? 1.0 : 0.0;
+    cx.Sstore[(long)(T - 1) * cx.Sstride] = beta;     // beta_{T-1} = 1, exponent 0
+    if (xw) Xrow[T - 1] = 0;
+    x = Et[cx.codes[T - 1] * 16 + y] * beta;
+    sc = -exp2_of(row_sum(x));
+  }
+
+  double K[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) K[k] = 0.0;
+  double* Hrow = Htab + ((size_t)(seq * 2 + (FWD ? 0 : 1)) * (M + 2)) * 16 + y;
+  double rc0 = 0.0;           // phase B: 1 / c at the phase's first step
+  int E0 = 0;                 //          and that step's exponent sum
+
+  // one step; combine: phase B (posterior, M1 count, xi), first: its first step
+  auto step = [&](int t, double e, double other, int xo, int code, bool combine, bool first, int j) {
+    const double u = __builtin_ldexp(dot2_bcast(x, C), sc);
+    const int eu = ex + sc;                          // exponent of u (and of p)
+    const double p = u * e;
+    const double keep = FWD ? p : u;                 // alpha^_t / beta^_t
+    // the forward rows need every step's mass (m2); the backward rows only
+    // rescale, every 4th step (j is the unrolled step index: no branch) --
+    // four evidence factors cannot underflow, and the exponents carry any scale
+    const bool rescale = FWD || (j & 3) == 3;
+    const double z2 = rescale ? row_sum(p) : 1.0;
+    if (!FWD && combine) {
+      // m1 mantissa of step t + 1 (< H) from alpha^_t = other
+      if (t + 1 < H) m1 *= row_sum(other * As);
+    }
+    if (!combine) {
+      cx.Sstore[(long)t * cx.Sstride] = keep;
+      if (xw) Xrow[t] = eu;                          // one lane per row (exec-masked store)
+    } else {
+      const double pr = keep * other;                // alpha^_t beta^_t = Z gamma_t 2^(eu + xo)
+      if (first) {
+        const double c = row_sum(pr);
+        rc0 = c != 0.0 ? div_by(1.0, c) : 0.0;
+        E0 = eu + xo;
+      }
+      const double q = __builtin_ldexp(pr * rc0, E0 - (eu + xo));
+      Hrow[code * 16] += q;
+      // xi_t (forward, x = alpha^_{t-1}) / xi_{t+1} (backward, x = g_{t+1}, t + 1 < H):
+      // x(.) A e_t beta_t / Z resp. alpha_t A g_{t+1} / Z, the A factor applied after the reduction
+      const double f = __builtin_ldexp(rc0, E0 - (ex + xo));
+      const double w = FWD ? e * other * f : (t + 1 < H ? other * f : 0.0);
+      acc_bcast(K, x, w);
+    }
+    if (FWD) {
+      m2 *= z2;
+      if (combine) m1 *= row_sum(u * s_y);
+    }
+    if ((FWD || combine) && (j & 3) == 3) {         // renormalise every 4 steps (0 stays 0)
+      if (FWD) { const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2; }
+      const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+    }
+    // the scale of the next step (a zero mass keeps every later vector 0,
+    // whatever the exponent: no zero test)
+    sc = rescale ? -__builtin_amdgcn_frexp_exp(z2) : 0;
+    x = p;
+    ex = eu;
+  };
+
+  constexpr int dir = FWD ? 1 : -1;
+  // phase A: forward t = 0..H-1; backward t = T-2..H
+  run_phase16<KC>(cx, FWD ? H : T - 1 - H, FWD ? 0 : T - 2, dir, false,
+                  [&](int t, double e, double o, int xo, int c, int j) { step(t, e, o, xo, c, false, false, j); });
+  const int efa = ex;                                // forward: Ef_{H-1}, the phase-A m1 exponents' sum
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // phase B: forward t = H..T-1 with beta_t; backward t = H-1..0 with alpha_t
+  {
+    const int n = FWD ? T - H : H;
+    const int t0 = FWD ? H : H - 1;
+    if (n > 0) {
+      step(t0, cx.Et[cx.codes[t0] * 16], cx.Sload[(long)t0 * 16], cx.Xload[t0], cx.codes[t0], true, true, 3);
+      run_phase16<KC>(cx, n - 1, t0 + dir, dir, true,
+                      [&](int t, double e, double o, int xo, int c, int j) { step(t, e, o, xo, c, true, false, j); });
+    }
+  }
+  double* slab = a.counts + (size_t)(active ? b : 0) * chain_estep_slab(M);
+  if (!FWD && H > 0) {
+    // the phase-A m1 part for the forward rows: step 0's from the prior, then
+    // mantissa and exponent through LDS
+    m1 *= row_sum(a.pi[y] * As);
+    const int k1 = __builtin_amdgcn_frexp_exp(m1);
+    m1 = __builtin_ldexp(m1, -k1);
+    e1 += k1;
+    if (y == 0) { m1x[2 * seq] = m1; m1x[2 * seq + 1] = (double)e1; }
+  }
+  if (!FWD) {
+    // one more backward step with alpha_{-1} = prior of prev: its posterior is
+    // the P0 count and its xi is xi_0 (when the forward rows did not cover
+    // t = 0, i.e. H > 0); normalised exactly, as chain_kernel<true>
+    const double pi_y = a.pi[y];
+    const double u = __builtin_ldexp(dot2_bcast(x, C), sc);
+    const double pr = pi_y * u;
+    const double c = row_sum(pr);
+    const double q = div_by(pr, c);
+    const double rc = c != 0.0 ? __builtin_ldexp(div_by(1.0, c), sc) : 0.0;
+    const double w = H > 0 ? pi_y * rc : 0.0;
+    acc_bcast(K, x, w);
+    if (active) slab[chain_slab_p0(M) + y] = q;
+  }
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) slab[FWD ? kSlabKf + k * 16 + y : kSlabKb + y * 16 + k] = K[k];
+  }
+  __syncthreads();                                   // the backward rows' m1 part in LDS
+  if (FWD && active && y == 0) {
+    double lm1 = log(m1);
+    int ee = e2 - e1;
+    if (H > 0) { lm1 += log(m1x[2 * seq]); ee -= (int)m1x[2 * seq + 1] + efa; }
+    const bool dead = m2 == 0.0;                       // some step's m2 == 0 (products renormalised: no underflow)
+    double ll = log(m2) - lm1 + (double)ee * 0.69314718055994530942;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    // e_step's BAD_LUCK (m1 <= 0 || m2 <= 0, nip.c:1827-1854): a zero mass here
+    if (a.status) a.status[b] = dead ? 3u : 0u;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kE16Threads, 1)
+void chain_estep16_kernel(ChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* Et = reinterpret_cast<double*>(smem);                         // [(M+2)][16]
+  uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);      // [16][Tr]
+  double* Htab = reinterpret_cast<double*>(
+      codes + (((size_t)kE16Seqs * chain_codes_row(a.T) + 15) & ~(size_t)15));   // [16][2][(M+2)][16]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const long b0 = (long)blockIdx.x * kE16Seqs;
+  const int T = a.T;
+  const int Tr = chain_codes_row(T);
+
+  for (int i = tid; i < (a.M + 2) * 16; i += kE16Threads) Et[i] = a.Etab[i];
+  const int nseq = (int)((a.B - b0) < kE16Seqs ? (a.B - b0) : kE16Seqs);
+  auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
+  for (int i = tid; i < kE16Seqs * Tr; i += kE16Threads) codes[i] = (uint8_t)a.M;   // missing / guard
+  for (int i = tid; i < kE16Seqs * 2 * (a.M + 2) * 16; i += kE16Threads) Htab[i] = 0.0;
+  __syncthreads();
+  if (a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kE16Seqs) {
+    const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * (long)T);
+    const int n4 = (kE16Seqs * T) >> 2;
+    for (int i0 = tid; i0 < n4; i0 += kE16Threads * 8) {
+      int4 r[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) if (i0 + k * kE16Threads < n4) r[k] = src[i0 + k * kE16Threads];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i4 = i0 + k * kE16Threads;
+        if (i4 < n4) {
+          const int i = i4 << 2, c = i / T, t = i - c * T;
+          const uint32_t packed = (uint32_t)code_of(r[k].x) | ((uint32_t)code_of(r[k].y) << 8) |
+                                  ((uint32_t)code_of(r[k].z) << 16) | ((uint32_t)code_of(r[k].w) << 24);
+          *reinterpret_cast<uint32_t*>(codes + c * Tr + kGuard + t) = packed;
+        }
+      }
+    }
+  } else if (a.obs) {
+    for (int i = tid; i < nseq * T; i += kE16Threads) {
+      const int c = i / T, t = i - c * T;
+      codes[c * Tr + kGuard + t] =
+          (uint8_t)code_of(a.obs[(b0 + c) * a.obs_bstride + (long)t * a.obs_tstride + a.obs_col]);
+    }
+  }
+  __syncthreads();
+  double* m1x = Htab + kE16Seqs * 2 * (a.M + 2) * 16;                   // [16][2]
+  if (wave < 4) estep16_rows<true>(a, Et, codes, Htab, m1x, lane, wave, b0);
+  else estep16_rows<false>(a, Et, codes, Htab, m1x, lane, wave, b0);
+  __syncthreads();
+  for (int i = tid; i < kE16Seqs * 2 * (a.M + 2) * 16; i += kE16Threads) {
+    const int sq = i / (2 * (a.M + 2) * 16), r = i - sq * 2 * (a.M + 2) * 16;
+    if (b0 + sq < a.B) a.counts[(size_t)(b0 + sq) * chain_estep_slab(a.M) + kSlabH + r] = Htab[i];
+  }
+}
+
+size_t chain_estep16_lds_bytes(int M, int T) {
+  const size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kE16Seqs * chain_codes_row(T);
+  return ((n + 15) & ~(size_t)15) + (size_t)kE16Seqs * 2 * (M + 2) * 16 * sizeof(double) +
+         (size_t)kE16Seqs * 2 * sizeof(double);
+}
+
+size_t chain_estep16_scratch_bytes(long B, int T) {
+  const long nrow = (B + kE16Seqs - 1) / kE16Seqs * kE16Seqs;
+  return (size_t)(nrow + 2) * chain_scratch_row(T) * sizeof(double) +
+         (size_t)(nrow + 2) * estep16_xrow(T) * sizeof(int);
+}
+
+int chain_estep16_launch(const ChainArgs& a, hipStream_t stream) {
+  const size_t lds = (chain_estep16_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024 || a.N > 16 || !a.counts) return -2;
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel), lds, lds_set)) return -1;
+  const int blocks = (int)((a.B + kE16Seqs - 1) / kE16Seqs);
+  hipLaunchKernelGGL(chain_estep16_kernel, dim3(blocks), dim3(kE16Threads), lds, stream, a);
+  g_last_kernel = "chain_estep16_kernel";
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 size_t chain_lds_bytes(int M, int T, bool estep) {
   size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kChainsPerBlock * chain_codes_row(T);
   if (estep) n = ((n + 15) & ~(size_t)15) + (size_t)kChainsPerBlock * 2 * (M + 2) * 16 * sizeof(double);

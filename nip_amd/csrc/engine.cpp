@@ -1138,18 +1138,19 @@ int nipamd_estep_partial_size(const nipamd_model* mm) {
   return body < 0 ? -1 : body + 2;
 }
 
-// e_step kernel of the chain route: 2 = the 16-lane DPP kernel (one slab row
-// per sequence; the default), 1 = the matrix-core kernel (one row per
-// 16-sequence block), selected by NIPAMD_ESTEP_KERNEL=mfma.  Measured on
-// config 4: the matrix-core form is partner-bound (per 8-step
-// chunk ~19K cycles of xi / count / normaliser work against the filter's
-// ~4K), 22.4 ms against the DPP kernel's 13.4 ms per 131072 x 1024 shard.
+// e_step kernel of the chain route: 3 = chain_estep16_kernel (16-lane DPP
+// rows, direction-uniform waves, analytic phase-B normalisation; the
+// default), 2 = chain_kernel<true> (the round-2 DPP kernel, mixed-direction
+// waves; NIPAMD_ESTEP_KERNEL=dpp8 in diagnostics builds, or when the 16-seq
+// block's LDS does not fit), 1 = the matrix-core kernel (NIPAMD_ESTEP_KERNEL=mfma).
+// Measured on config 4.
 static int chain_estep_kernel(const nipamd_model* mm, int T) {
   const auto& P = mm->m.chain;
   const int M = P.emits[0].M;
   const char* ek = nipamd::diag_env("NIPAMD_ESTEP_KERNEL");
-  const bool want_mfma = ek && std::string(ek) == "mfma";
-  if (want_mfma && P.N <= 16 && M <= 16 && nipamd::chain_estep_mfma_lds_bytes(M, T) <= 160 * 1024) return 1;
+  const std::string want = ek ? ek : "";
+  if (want == "mfma" && P.N <= 16 && M <= 16 && nipamd::chain_estep_mfma_lds_bytes(M, T) <= 160 * 1024) return 1;
+  if (want != "dpp8" && P.N <= 16 && nipamd::chain_estep16_lds_bytes(M, T) <= 160 * 1024) return 3;
   if (nipamd::chain_lds_bytes(M, T, true) <= 96 * 1024) return 2;
   return 0;
 }
@@ -1227,7 +1228,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   const int col = r.pcol;
   const int Mo = P.emits[0].M;
   const int S = nipamd::chain_estep_slab(Mo);
-  const bool mfma = chain_estep_kernel(mm, T) == 1;
+  const int ek = chain_estep_kernel(mm, T);
+  const bool mfma = ek == 1;
   const int per_row = mfma ? 16 : 1;            // sequences per slab row
   hipStream_t st = (hipStream_t)stream;
   if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, st))
@@ -1243,7 +1245,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   const long rows = (chunk + per_row - 1) / per_row;
   const long lvl = (rows + 63) / 64;
   const size_t work = ((size_t)rows + 2 * lvl + nchunks + 64) * S * sizeof(double);
-  if (int rc = ensure_scratch(mm, nipamd::chain_scratch_bytes((int)chunk, T))) return rc;
+  if (int rc = ensure_scratch(mm, ek == 3 ? nipamd::chain_estep16_scratch_bytes(chunk, T)
+                                          : nipamd::chain_scratch_bytes((int)chunk, T))) return rc;
   if (int rc = ensure_work(mm, work)) return rc;
   DevState* d = dev_of(mm);
   double* slab = d->W;
@@ -1260,6 +1263,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     a.obs_tstride = ocols;
     a.obs_col = col;
     a.B = nb; a.T = T; a.H = T / 2; a.N = P.N; a.M = Mo;
+    if (const char* hp = nipamd::diag_env("NIPAMD_ESTEP_H"))    // split point in % of T (A/B builds)
+      if (ek == 3) a.H = std::min(T - 1, std::max(0, (int)((long)T * std::atoi(hp) / 100)));
     a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
@@ -1272,7 +1277,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 24 * sizeof(unsigned long long), st));
     }
 #endif
-    const int lrc = mfma ? nipamd::chain_estep_mfma_launch(a, st) : nipamd::chain_estep_launch(a, st);
+    const int lrc = mfma ? nipamd::chain_estep_mfma_launch(a, st)
+                    : ek == 3 ? nipamd::chain_estep16_launch(a, st) : nipamd::chain_estep_launch(a, st);
     if (lrc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
 #ifdef NIPAMD_DIAGNOSTICS

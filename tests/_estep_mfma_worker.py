@@ -58,9 +58,16 @@ def vs_oracle(N, M, B, T):
         assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
     mfma(False)
     cnt2, ll2, _ = gpu_estep(m, obs, ov)
-    assert nip_amd.last_kernel() == "chain_kernel<true>", nip_amd.last_kernel()
+    assert nip_amd.last_kernel() == "chain_estep16_kernel", nip_amd.last_kernel()
     assert close(cnt, cnt2, CNT_RTOL)
     assert close(ll, ll2, LL_RTOL)
+    os.environ["NIPAMD_ESTEP_KERNEL"] = "dpp8"         # the round-2 DPP kernel
+    cnt3, ll3, st3 = gpu_estep(m, obs, ov)
+    assert nip_amd.last_kernel() == "chain_kernel<true>", nip_amd.last_kernel()
+    os.environ.pop("NIPAMD_ESTEP_KERNEL", None)
+    assert np.array_equal(st3 != 0, rb != 0)
+    assert close(cnt, cnt3, CNT_RTOL)
+    assert close(ll, ll3, LL_RTOL)
 
 
 def missing_and_bad_luck():
