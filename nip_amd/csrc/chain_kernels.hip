@@ -34,13 +34,17 @@
 // backward continues beta_{H-1}..beta_0 and combines with alpha_t from S.
 #include <hip/hip_runtime.h>
 #include <cfloat>
+#include <cstdlib>
 #include <cstdint>
 
 #include "chain_kernels.h"
+#include "diag.h"
 
 namespace nipamd {
 
 namespace {
+
+typedef double v4d __attribute__((ext_vector_type(4)));   // an f64 MFMA accumulator
 
 // DPP row_ror:K -- every lane of a 16-lane row has a source, so no "old"
 // operand is needed (mov_dpp with bound_ctrl)
@@ -490,8 +494,12 @@ void chain_kernel(ChainArgs a) {
 //    relative over T = 1024), well inside DESIGN.md's count tolerance.
 // Per-sequence slabs (chain_estep_slab layout) as chain_kernel<true>, so
 // tree64_kernel and estep_finalize_kernel are shared.
-constexpr int kE16Seqs = 16;
-constexpr int kE16Threads = 512;
+// NSEQ sequences per block (16: 8 waves, two per SIMD; 24: 12 waves, three
+// per SIMD), waves 0 .. NSEQ/4-1 forward, the rest backward
+constexpr int kE16RowMul = 48;                 // scratch rows rounded to a multiple of every NSEQ
+#ifndef NIPAMD_WAIT_TIMES
+#define NIPAMD_WAIT_TIMES 0                    // stamps builds: per-wave phase cycle stamps into a.diag
+#endif
 
 namespace {
 
@@ -562,12 +570,11 @@ __device__ __forceinline__ double dot2_bcast(double x, const double (&c)[16]) {
 }
 
 // One direction's rows of a block (FWD: waves 0-3, backward: waves 4-7).
-template <bool FWD>
+template <bool FWD, int KC>
 __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* Et, const uint8_t* codes,
-                                             double* Htab, double* m1x, int lane, int wave, long b0) {
-  constexpr int KC = NIPAMD_ESTEP_CHUNK;
+                                             double* Htab, double* m1x, int lane, int grp, long b0) {
   const int y = lane & 15, row = lane >> 4;
-  const int seq = (wave & 3) * 4 + row;             // 0..15 within the block
+  const int seq = grp * 4 + row;                    // within the block
   const long b = b0 + seq;
   const bool active = b < a.B;
   const int T = a.T, H = a.H, M = a.M;
@@ -584,7 +591,7 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     for (int k = 0; k < 16; k++) As = __builtin_fma(C[k], Et[M * 16 + k], As);
   }
 
-  const long nrow = (a.B + kE16Seqs - 1) / kE16Seqs * kE16Seqs;
+  const long nrow = (a.B + kE16RowMul - 1) / kE16RowMul * kE16RowMul;
   double* const sink = a.S + (size_t)(nrow + 1) * chain_scratch_row(T) + y;
   double* const Srow = a.S + (size_t)(active ? b : 0) * chain_scratch_row(T) + (size_t)kGuard * 16 + y;
   int* const X = reinterpret_cast<int*>(a.S + (size_t)(nrow + 2) * chain_scratch_row(T));
@@ -604,32 +611,45 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   double x;
   int sc = 0, ex = 0;
   // ll = sum_t log m2_t - log m1_t (nip.c:1461-1474): the forward rows carry
-  // the m2 of every step and the m1 of phase B; the m1 of phase A steps t < H,
-  // sum_y (A^T alpha^_{t-1})(y) s(y) 2^sc_t = (alpha^_{t-1} . A s) 2^sc_t, is
-  // summed by the backward rows in their phase B, where alpha^_{t-1} arrives
-  // from the scratch anyway (the exponents telescope to Ef_{H-1}), and handed
-  // over through LDS: the forward waves' phase A is the heavier one
+  // every m2 and phase B's m1; phase A's m1 (t < H), (alpha^_{t-1} . A s) at
+  // scale 2^Ef_{t-1} (the scales telescope to Ef_{H-1}, the m2 being at
+  // 2^Ef_t), is summed by the backward rows in their phase B, where alpha^_t
+  // arrives from the scratch anyway, and handed over through LDS -- the
+  // split that measured best (the phase-B backward rows are the critical ones)
   double m2 = 1.0, m1 = 1.0;   // running products (mantissas)
   int e2 = 0, e1 = 0;          // and their binary exponents
+  // rows past the batch run on zeros: every product they feed the block's
+  // matrix-core sums is then 0 without a select per step
   if (FWD) {
-    x = a.pi[y];
+    x = active ? a.pi[y] : 0.0;
   } else {
-    const double beta = y < a.N ? 1.0 : 0.0;
+    const double beta = (active && y < a.N) ? 1.0 : 0.0;
     cx.Sstore[(long)(T - 1) * cx.Sstride] = beta;     // beta_{T-1} = 1, exponent 0
     if (xw) Xrow[T - 1] = 0;
     x = Et[cx.codes[T - 1] * 16 + y] * beta;
     sc = -exp2_of(row_sum(x));
   }
 
-  double K[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) K[k] = 0.0;
+  // xi of the wave's four sequences on the matrix core: the rows' x (lane:
+  // row r, state i) is the A operand (i, k = r) and w (row r, state j) the B
+  // operand (k = r, j) of one v_mfma_f64_16x16x4 per step, D[i][j] +=
+  // sum_r x_r(i) w_r(j) -- the sixteen broadcast fmas of chain_kernel<true>'s
+  // per-row outer product as one instruction, summed over the wave's rows
+  v4d Kd = {0.0, 0.0, 0.0, 0.0};
   double* Hrow = Htab + ((size_t)(seq * 2 + (FWD ? 0 : 1)) * (M + 2)) * 16 + y;
   double rc0 = 0.0;           // phase B: 1 / c at the phase's first step
   int E0 = 0;                 //          and that step's exponent sum
 
   // one step; combine: phase B (posterior, M1 count, xi), first: its first step
   auto step = [&](int t, double e, double other, int xo, int code, bool combine, bool first, int j) {
+    // phase B: this step's M1 count cell, read before the step's arithmetic
+    // so the LDS latency overlaps it (the previous step's write to the same
+    // cell precedes it in the wave's LDS order)
+    double hv = 0.0;
+    if (combine) {
+      hv = Hrow[code * 16];
+      asm volatile("" : "+v"(hv));                   // keep the read here
+    }
     const double u = __builtin_ldexp(dot2_bcast(x, C), sc);
     const int eu = ex + sc;                          // exponent of u (and of p)
     const double p = u * e;
@@ -640,8 +660,8 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     const bool rescale = FWD || (j & 3) == 3;
     const double z2 = rescale ? row_sum(p) : 1.0;
     if (!FWD && combine) {
-      // m1 mantissa of step t + 1 (< H) from alpha^_t = other
-      if (t + 1 < H) m1 *= row_sum(other * As);
+      // the m1 of the forward rows' phase-A step t + 1 (< H) from alpha^_t = other
+      if (!first) m1 *= row_sum(other * As);           // t + 1 < H: every step but the first
     }
     if (!combine) {
       cx.Sstore[(long)t * cx.Sstride] = keep;
@@ -654,12 +674,14 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
         E0 = eu + xo;
       }
       const double q = __builtin_ldexp(pr * rc0, E0 - (eu + xo));
-      Hrow[code * 16] += q;
+      Hrow[code * 16] = hv + q;
       // xi_t (forward, x = alpha^_{t-1}) / xi_{t+1} (backward, x = g_{t+1}, t + 1 < H):
       // x(.) A e_t beta_t / Z resp. alpha_t A g_{t+1} / Z, the A factor applied after the reduction
       const double f = __builtin_ldexp(rc0, E0 - (ex + xo));
-      const double w = FWD ? e * other * f : (t + 1 < H ? other * f : 0.0);
-      acc_bcast(K, x, w);
+      // (backward: the phase's first step, t = H - 1, has no xi_{t+1}: xi_H is the forward rows')
+      const double w = FWD ? e * other * f : (first ? 0.0 : other * f);
+      Kd = FWD ? __builtin_amdgcn_mfma_f64_16x16x4f64(x, w, Kd, 0, 0, 0)
+               : __builtin_amdgcn_mfma_f64_16x16x4f64(w, x, Kd, 0, 0, 0);
     }
     if (FWD) {
       m2 *= z2;
@@ -677,11 +699,15 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   };
 
   constexpr int dir = FWD ? 1 : -1;
+  unsigned long long st[4] = {0, 0, 0, 0};
+  if (NIPAMD_WAIT_TIMES) st[0] = __builtin_readcyclecounter();
   // phase A: forward t = 0..H-1; backward t = T-2..H
   run_phase16<KC>(cx, FWD ? H : T - 1 - H, FWD ? 0 : T - 2, dir, false,
                   [&](int t, double e, double o, int xo, int c, int j) { step(t, e, o, xo, c, false, false, j); });
   const int efa = ex;                                // forward: Ef_{H-1}, the phase-A m1 exponents' sum
+  if (NIPAMD_WAIT_TIMES) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); st[1] = __builtin_readcyclecounter(); }
   __syncthreads();
+  if (NIPAMD_WAIT_TIMES) st[2] = __builtin_readcyclecounter();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // phase B: forward t = H..T-1 with beta_t; backward t = H-1..0 with alpha_t
   {
@@ -693,6 +719,13 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
                       [&](int t, double e, double o, int xo, int c, int j) { step(t, e, o, xo, c, true, false, j); });
     }
   }
+  if (NIPAMD_WAIT_TIMES) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); st[3] = __builtin_readcyclecounter(); }
+  if (NIPAMD_WAIT_TIMES && a.diag && lane == 0) {
+    unsigned long long* d = a.diag + ((size_t)blockIdx.x * 16 + (FWD ? 0 : 8) + grp) * 4;
+    d[0] = st[1] - st[0];                            // phase A
+    d[1] = st[2] - st[1];                            // phase barrier wait
+    d[2] = st[3] - st[2];                            // phase B
+  }
   double* slab = a.counts + (size_t)(active ? b : 0) * chain_estep_slab(M);
   if (!FWD && H > 0) {
     // the phase-A m1 part for the forward rows: step 0's from the prior, then
@@ -701,7 +734,7 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     const int k1 = __builtin_amdgcn_frexp_exp(m1);
     m1 = __builtin_ldexp(m1, -k1);
     e1 += k1;
-    if (y == 0) { m1x[2 * seq] = m1; m1x[2 * seq + 1] = (double)e1; }
+    if (y == 0) { m1x[4 * seq] = m1; m1x[4 * seq + 1] = (double)e1; }
   }
   if (!FWD) {
     // one more backward step with alpha_{-1} = prior of prev: its posterior is
@@ -714,20 +747,37 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     const double q = div_by(pr, c);
     const double rc = c != 0.0 ? __builtin_ldexp(div_by(1.0, c), sc) : 0.0;
     const double w = H > 0 ? pi_y * rc : 0.0;
-    acc_bcast(K, x, w);
+    Kd = __builtin_amdgcn_mfma_f64_16x16x4f64(w, x, Kd, 0, 0, 0);
     if (active) slab[chain_slab_p0(M) + y] = q;
   }
-  if (active) {
+  // the wave's xi sum goes to its first sequence's slab row, zeros to the
+  // other three (the batch tree sums rows; shards are whole 16-sequence blocks)
+  {
+    const int ko = FWD ? kSlabKf : kSlabKb;
+    const long lead = b0 + grp * 4;                  // the group's first sequence
+    if (lead < a.B) {
+      double* const g = a.counts + (size_t)lead * chain_estep_slab(M) + ko;
 #pragma unroll
-    for (int k = 0; k < 16; k++) slab[FWD ? kSlabKf + k * 16 + y : kSlabKb + y * 16 + k] = K[k];
+      for (int r = 0; r < 4; r++) {
+        const int i = (lane >> 4) + 4 * r;           // D row: the previous state x
+        g[i * 16 + y] = Kd[r];                       // lane (row', y): element (x, y)
+      }
+    }
+    if (active && row != 0) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) slab[ko + k * 16 + y] = 0.0;
+    }
   }
   __syncthreads();                                   // the backward rows' m1 part in LDS
   if (FWD && active && y == 0) {
-    double lm1 = log(m1);
+    double lm = log(m2) - log(m1);
     int ee = e2 - e1;
-    if (H > 0) { lm1 += log(m1x[2 * seq]); ee -= (int)m1x[2 * seq + 1] + efa; }
-    const bool dead = m2 == 0.0;                       // some step's m2 == 0 (products renormalised: no underflow)
-    double ll = log(m2) - lm1 + (double)ee * 0.69314718055994530942;
+    bool dead = m2 == 0.0;                             // some step's m2 == 0 (products renormalised: no underflow)
+    if (H > 0) {                                       // phase A's m1, summed by the backward rows
+      lm -= log(m1x[4 * seq]);
+      ee -= (int)m1x[4 * seq + 1] + efa;
+    }
+    double ll = lm + (double)ee * 0.69314718055994530942;
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
     // e_step's BAD_LUCK (m1 <= 0 || m2 <= 0, nip.c:1827-1854): a zero mass here
@@ -737,18 +787,21 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
 
 }  // namespace
 
-__global__ __launch_bounds__(kE16Threads, 1)
+template <int NSEQ, int KC>
+__global__ __launch_bounds__(NSEQ * 32, 1)
 void chain_estep16_kernel(ChainArgs a) {
+  constexpr int kE16Seqs = NSEQ, kE16Threads = NSEQ * 32, G = NSEQ / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* Et = reinterpret_cast<double*>(smem);                         // [(M+2)][16]
   uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);      // [16][Tr]
   double* Htab = reinterpret_cast<double*>(
-      codes + (((size_t)kE16Seqs * chain_codes_row(a.T) + 15) & ~(size_t)15));   // [16][2][(M+2)][16]
+      codes + (((size_t)kE16Seqs * chain_codes_row(a.T) + 15) & ~(size_t)15));   // [NSEQ][2][(M+2)][16]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const long b0 = (long)blockIdx.x * kE16Seqs;
   const int T = a.T;
   const int Tr = chain_codes_row(T);
+  const unsigned long long t_entry = NIPAMD_WAIT_TIMES ? __builtin_readcyclecounter() : 0;
 
   for (int i = tid; i < (a.M + 2) * 16; i += kE16Threads) Et[i] = a.Etab[i];
   const int nseq = (int)((a.B - b0) < kE16Seqs ? (a.B - b0) : kE16Seqs);
@@ -782,37 +835,57 @@ void chain_estep16_kernel(ChainArgs a) {
     }
   }
   __syncthreads();
-  double* m1x = Htab + kE16Seqs * 2 * (a.M + 2) * 16;                   // [16][2]
-  if (wave < 4) estep16_rows<true>(a, Et, codes, Htab, m1x, lane, wave, b0);
-  else estep16_rows<false>(a, Et, codes, Htab, m1x, lane, wave, b0);
+  double* m1x = Htab + kE16Seqs * 2 * (a.M + 2) * 16;                   // [NSEQ][4]
+  if (wave < G) estep16_rows<true, KC>(a, Et, codes, Htab, m1x, lane, wave, b0);
+  else estep16_rows<false, KC>(a, Et, codes, Htab, m1x, lane, wave - G, b0);
   __syncthreads();
   for (int i = tid; i < kE16Seqs * 2 * (a.M + 2) * 16; i += kE16Threads) {
     const int sq = i / (2 * (a.M + 2) * 16), r = i - sq * 2 * (a.M + 2) * 16;
     if (b0 + sq < a.B) a.counts[(size_t)(b0 + sq) * chain_estep_slab(a.M) + kSlabH + r] = Htab[i];
   }
+  if (NIPAMD_WAIT_TIMES && a.diag && lane == 0) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const int dd = wave < G ? 0 : 8, gg = wave < G ? wave : wave - G;
+    a.diag[((size_t)blockIdx.x * 16 + dd + gg) * 4 + 3] = __builtin_readcyclecounter() - t_entry;   // whole block
+  }
 }
 
-size_t chain_estep16_lds_bytes(int M, int T) {
-  const size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)kE16Seqs * chain_codes_row(T);
-  return ((n + 15) & ~(size_t)15) + (size_t)kE16Seqs * 2 * (M + 2) * 16 * sizeof(double) +
-         (size_t)kE16Seqs * 2 * sizeof(double);
+static int estep16_seqs() {
+  static const int n = [] {
+    const char* e = diag_env("NIPAMD_ESTEP16_SEQS");       // A/B builds: 16 or 24
+    return e && std::atoi(e) == 24 ? 24 : 16;
+  }();
+  return n;
 }
+
+static size_t estep16_lds(int nseq, int M, int T) {
+  const size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)nseq * chain_codes_row(T);
+  return ((n + 15) & ~(size_t)15) + (size_t)nseq * 2 * (M + 2) * 16 * sizeof(double) + (size_t)nseq * 4 * sizeof(double);
+}
+
+size_t chain_estep16_lds_bytes(int M, int T) { return estep16_lds(estep16_seqs(), M, T); }
 
 size_t chain_estep16_scratch_bytes(long B, int T) {
-  const long nrow = (B + kE16Seqs - 1) / kE16Seqs * kE16Seqs;
+  const long nrow = (B + kE16RowMul - 1) / kE16RowMul * kE16RowMul;
   return (size_t)(nrow + 2) * chain_scratch_row(T) * sizeof(double) +
          (size_t)(nrow + 2) * estep16_xrow(T) * sizeof(int);
 }
 
-int chain_estep16_launch(const ChainArgs& a, hipStream_t stream) {
-  const size_t lds = (chain_estep16_lds_bytes(a.M, a.T) + 15) & ~(size_t)15;
-  if (lds > 160 * 1024 || a.N > 16 || !a.counts) return -2;
+template <int NSEQ, int KC>
+static int estep16_launch(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel), lds, lds_set)) return -1;
-  const int blocks = (int)((a.B + kE16Seqs - 1) / kE16Seqs);
-  hipLaunchKernelGGL(chain_estep16_kernel, dim3(blocks), dim3(kE16Threads), lds, stream, a);
-  g_last_kernel = "chain_estep16_kernel";
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC>), lds, lds_set)) return -1;
+  const int blocks = (int)((a.B + NSEQ - 1) / NSEQ);
+  hipLaunchKernelGGL((chain_estep16_kernel<NSEQ, KC>), dim3(blocks), dim3(NSEQ * 32), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int chain_estep16_launch(const ChainArgs& a, hipStream_t stream) {
+  const int nseq = estep16_seqs();
+  const size_t lds = (estep16_lds(nseq, a.M, a.T) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024 || a.N > 16 || !a.counts) return -2;
+  g_last_kernel = "chain_estep16_kernel";
+  return nseq == 24 ? estep16_launch<24, 4>(a, lds, stream) : estep16_launch<16, NIPAMD_ESTEP_CHUNK>(a, lds, stream);
 }
 
 size_t chain_lds_bytes(int M, int T, bool estep) {

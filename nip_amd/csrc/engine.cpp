@@ -1276,12 +1276,40 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       HIP_OK(hipMalloc(&a.diag, (size_t)nblk * 24 * sizeof(unsigned long long)));
       HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 24 * sizeof(unsigned long long), st));
     }
+    unsigned long long* e16d = nullptr;              // chain_estep16_kernel's per-wave stamps [block][16][4]
+    if (ek == 3 && times && c == 0) {
+      HIP_OK(hipMalloc(&e16d, (size_t)nblk * 64 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(e16d, 0, (size_t)nblk * 64 * sizeof(unsigned long long), st));
+      a.diag = e16d;
+    }
 #endif
     const int lrc = mfma ? nipamd::chain_estep_mfma_launch(a, st)
                     : ek == 3 ? nipamd::chain_estep16_launch(a, st) : nipamd::chain_estep_launch(a, st);
     if (lrc)
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
 #ifdef NIPAMD_DIAGNOSTICS
+    if (e16d) {
+      std::vector<unsigned long long> h((size_t)nblk * 64);
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(h.data(), e16d, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      (void)hipFree(e16d);
+      a.diag = nullptr;
+      double m[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+      int nw[2] = {0, 0};
+      for (int k = 0; k < nblk; k++)
+        for (int w = 0; w < 16; w++) {
+          const unsigned long long* r = h.data() + ((size_t)k * 16 + w) * 4;
+          if (r[0] + r[2] == 0) continue;
+          const int dd = w < 8 ? 0 : 1;
+          for (int i = 0; i < 4; i++) m[dd][i] += (double)r[i];
+          nw[dd]++;
+        }
+      for (int dd = 0; dd < 2; dd++)
+        if (nw[dd])
+          std::fprintf(stderr, "[nipamd] estep16 %s waves: phase A %.0f  barrier wait %.0f  phase B %.0f  "
+                       "block entry to exit %.0f cycles (mean of %d)\n", dd ? "backward" : "forward",
+                       m[dd][0] / nw[dd], m[dd][1] / nw[dd], m[dd][2] / nw[dd], m[dd][3] / nw[dd], nw[dd]);
+    }
     if (a.diag) {
       std::vector<unsigned long long> h((size_t)nblk * 24);
       HIP_OK(hipStreamSynchronize(st));
