@@ -100,6 +100,11 @@ WORKLOADS = {
     # the same slice as a joint-interface chain (16 joint states) on the
     # matrix-core chain kernels -- what the automatic engine choice runs
     "joint": ("general", lambda a: synth.factorial_spec(4, 4, 16), ["O1"], "X1", 4096, 1024, 20),
+    # demo1's structure (6 states) with its hidden parent D1 observed: no
+    # interface-chain plan; the evidence-indexed chain (opchain.hip) by default,
+    # the general join-tree engine as "opchain_jt"
+    "opchain": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 20),
+    "opchain_jt": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 2),
 }
 # the default line: the headline, then these under "secondary" 
 SECONDARY = ["config3", "em", "config5"]
@@ -205,8 +210,8 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
     nodes, pots = spec(args)
     model = nip_amd.Model.from_spec(nodes, pots)
     ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
-    if name == "jtree":
-        model.set_engine(nip_amd.ENGINE_JTREE)     # the joint-interface chain would take it otherwise
+    if name in ("jtree", "opchain_jt"):
+        model.set_engine(nip_amd.ENGINE_JTREE)     # the chain kernels would take it otherwise
     N, M = model.card(q), model.card(ov[0])
     obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
                              for i, v in enumerate(ov)], axis=2)
@@ -310,6 +315,16 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         workload = ("general join-tree engine: factorial HMM, X and Y 4 states each, O1 16 states of both, "
                     "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
         metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
+    elif name in ("opchain", "opchain_jt"):
+        if kname == "op_fb_kernel":
+            bpu, bnote = 4 * len(ov) + 2 * 128 + 8 * N, (
+                "obs %d + the 16-wide interface message written and read back (128 + 128) + posterior %d"
+                % (4 * len(ov), 8 * N))
+        else:
+            bpu, bnote = 4 * len(ov) + 8 * N, "the request's I/O only: the engine is latency-bound (DESIGN.md 4)"
+        workload = ("demo1 structure, 6 states, A1 B1 and the hidden parent D1 observed, C1 posterior, "
+                    "B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
+        metric = "sequence-timesteps/s fwd-bwd smoothing, demo1 with its hidden parent observed"
     elif name == "joint":
         K = 16                         # joint interface states (X1, Y1)
         if kname == "chain_fb_ckpt_kernel<proj>":

@@ -488,6 +488,7 @@ void nipamd_model_free(nipamd_model* mm) {
   if (!mm) return;
   nipamd::generate_release(mm);
   nipamd::jt_release(mm);
+  nipamd::op_release(mm);
   nipamd::likelihood_release(mm);
   DevState* d = static_cast<DevState*>(mm->m.dev);
   dev_release(d);
@@ -527,6 +528,9 @@ int nipamd_model_gpu_supported(const nipamd_model* mm, int n_obs, const int* obs
   if (!mm) return 0;
   Route r; std::string why;
   if (mm->engine != NIPAMD_ENGINE_JTREE && route_request(mm, n_obs, obs_vars, n_query, query, r, why)) return 1;
+  if (mm->engine != NIPAMD_ENGINE_JTREE &&
+      nipamd::op_supported(const_cast<nipamd_model*>(mm), n_obs, obs_vars, n_query, query, why))
+    return 1;
   return mm->engine != NIPAMD_ENGINE_CHAIN && nipamd::jt_supported(mm, n_obs, obs_vars, n_query, query, why);
 }
 
@@ -931,6 +935,8 @@ static int launch_joint_marginals(nipamd_model* mm, const Route& r, ReqTables* r
   return 0;
 }
 
+static int rc_or_fail(int rc, const std::string& err) { return rc ? fail(rc, err) : 0; }
+
 // forward_backward_inference (filt = false) / forward_inference (filt = true).
 // The interface variable's marginals come from the chain kernels; every
 // other queried variable's are derived from them (derive.hip), with the
@@ -955,6 +961,49 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
     for (int i = 0; i < n_query && kk != kNoChain && !filt; i++)
       if (query_kind(mm->m.chain, query[i]) >= 1000 && pick_kernel(mm, r, rt, T, true) == kNoChain) kk = kNoChain;
     if (kk == kNoChain) why = "sequence too long for the interface-chain kernels' LDS-resident codes";
+  }
+  if (kk == kNoChain && mm->engine != NIPAMD_ENGINE_JTREE) {
+    // the evidence-indexed interface chain (opchain.h): the slice as one K x K
+    // operator per evidence combination, K <= 16 joint interface states
+    std::string why2;
+    if (nipamd::op_supported(mm, n_obs, obs_vars, n_query, query, why2)) {
+      if (int rc = ensure_device(mm)) return rc;
+      const auto& out = mm->m.outgoing;
+      std::string err;
+      int K = 0;
+      if (n_query == 1 && out.size() == 1) {           // the interface variable itself: straight into its rows
+        const int card = mm->m.vars[query[0]].card;
+        return (rc_or_fail(nipamd::op_fb(mm, d_obs, n_obs, obs_vars, B, T, d_post, (long)T * card, card, 0, d_ll,
+                                         d_status, stream, filt, &K, err), err));
+      }
+      long stride = 0;
+      for (int i = 0; i < n_query; i++) stride += mm->m.vars[query[i]].card;
+      long Kj = 1;
+      for (int v : out) Kj *= mm->m.vars[v].card;
+      if (int rc = ensure_q(mm, (size_t)B * T * Kj * sizeof(double))) return rc;
+      double* q = dev_of(mm)->Q;
+      if (int rc = nipamd::op_fb(mm, d_obs, n_obs, obs_vars, B, T, q, (long)T * Kj, (int)Kj, 0, d_ll, d_status,
+                                 stream, filt, &K, err))
+        return fail(rc, err);
+      long off = 0;
+      for (int i = 0; i < n_query; i++) {
+        nipamd::DeriveArgs g{};
+        g.kind = nipamd::kDeriveProject;
+        g.filter = filt ? 1 : 0;
+        g.B = B; g.T = T; g.N = (int)Kj;
+        g.cur = q; g.cur_bstride = (long)T * Kj; g.cur_tstride = (int)Kj;
+        g.alpha = q; g.al_bstride = g.cur_bstride; g.al_tstride = g.cur_tstride;
+        g.out = d_post; g.out_bstride = (long)T * stride; g.out_tstride = (int)stride; g.out_off = (int)off;
+        g.prev_stride = 1;
+        for (size_t j = 0; j < out.size() && out[j] != query[i]; j++) g.prev_stride *= mm->m.vars[out[j]].card;
+        g.prev_card = mm->m.vars[query[i]].card;
+        g.child_col = -1;
+        if (nipamd::derive_launch(g, (hipStream_t)stream))
+          return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+        off += g.prev_card;
+      }
+      return 0;
+    }
   }
   if (kk == kNoChain) {
     // the general join-tree engine (jtree.hip): any slice, any T

@@ -153,6 +153,7 @@ struct nipamd_model {
   double fold_ms = 0.0;          // the last GPU fold: kernel time and clique bytes streamed
   double fold_bytes = 0.0;
   void* lik = nullptr;           // likelihood.hip: device tables of the last column set
+  void* op = nullptr;            // opchain.cpp: evidence-indexed chain plans
   // prefix.cpp: the e_step's leading-missing-run verdict for `version`, valid
   // for T <= pf_T (-1: none below pf_T; -2: not decided, model too large)
   unsigned pf_version = 0;
@@ -174,6 +175,13 @@ long estep_prefix_entries(const Model& m);
 void likelihood_release(nipamd_model* mm);
 // generate.cpp: drop a model's cached generate_data tables (nipamd_model_free)
 void generate_release(const nipamd_model* mm);
+// opchain.cpp: the evidence-indexed interface chain (opchain.h)
+bool op_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int n_query, const int* query,
+                  std::string& why);
+int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T, double* d_joint,
+          long jbs, int jts, int joff, double* d_ll, uint32_t* d_status, void* stream, bool filt, int* K_out,
+          std::string& err);
+void op_release(nipamd_model* mm);
 // jtree_plan.cpp: the general join-tree engine (jtree.h)
 int jt_supported(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
                  const int* query, std::string& why);

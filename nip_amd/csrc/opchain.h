@@ -1,0 +1,56 @@
+// opchain.h -- the evidence-indexed interface chain (opchain.cpp, opchain.hip).
+//
+// Any DBN time slice maps the previous interface's distribution to the
+// current one linearly: with I_{t-1} = x and I_t = y the joint interface
+// states (K = prod of the outgoing variables' cardinalities),
+//   alpha_t(y) = sum_x alpha_{t-1}(x) T_{c_t}(x, y),
+//   T_c(x, y)  = sum over the slice's other variables of the product of its
+//                CPTs, the priors entered every slice and the evidence
+//                indicators of combination c,
+// where c indexes the step's evidence row (each observed variable missing or
+// one of its states).  When K <= 16 and the slice is small enough to
+// enumerate, the operators T_c are built once per model version and request
+// on the host, and forward-backward runs as a chain over K states whose
+// transition is chosen per step by the evidence row -- the slices the
+// interface-chain plan rejects (evidence on a hidden parent or a non-leaf
+// variable, interfaces that do not factorise) then run as chains too instead
+// of on the general join-tree engine.
+#pragma once
+
+#include <cstdint>
+#include <hip/hip_runtime.h>
+
+namespace nipamd {
+
+constexpr int kOpMaxObs = 8;
+
+struct OpArgs {
+  const int32_t* obs;      // [B][T][n_obs]
+  long obs_bstride;
+  int obs_tstride;
+  int nobs;                // observed columns used
+  int col[kOpMaxObs];      // their columns in obs
+  int card[kOpMaxObs];     // their cardinalities
+  int cstride[kOpMaxObs];  // combination radix: prod_{j<i} (card_j + 1)
+  long B;
+  int T, H, K;
+  int ncomb;               // combinations; table ncomb is all zeros (an out-of-range state)
+  int filter;              // forward_inference: the forward rows' normalised messages
+  int tlds;                // set by op_fb_launch: the operators fit in LDS
+  const double* Ttab;      // [(ncomb + 1)][K][K], table ncomb all zeros
+  const double* w;         // [K] slice mass without evidence given x (m1 weights)
+  const double* pi;        // [K] prior of the previous interface
+  double* S;               // scratch: op_scratch_bytes(B, T)
+  double* post;            // [B][T][post_tstride], the joint interface marginal at post_off
+  long post_bstride;
+  int post_tstride;
+  int post_off;
+  double* ll;
+  unsigned* status;
+};
+
+size_t op_lds_bytes(int K, int ncomb, int T, bool tables);
+size_t op_scratch_bytes(long B, int T);
+int op_fb_launch(const OpArgs& a, hipStream_t stream);
+
+}  // namespace nipamd

@@ -1,0 +1,249 @@
+// opchain.hip -- forward-backward over an evidence-indexed interface chain
+// (opchain.h): the two-filter recursion of chain_kernels.hip with the
+// transition chosen per step from LDS-resident operators T_c (evidence folded
+// in) instead of a fixed transition times an evidence column.
+//
+// Block = 8 sequences, 4 waves; a 16-lane row per (sequence, direction),
+// lane y owns joint interface state y (y < K): rows 0-1 of a wave run the
+// forward filter of two sequences, rows 2-3 the backward filter of the same
+// two.  Per step a lane reads its column (forward) or row (backward) of
+// T_{c_t} from LDS and does the K-term mat-vec with DPP row broadcasts; sums
+// over the row are DPP butterflies (bit-identical in every lane).
+//   forward:  alpha_t = T_{c_t}^T alpha_{t-1}, alpha_{-1} = prior of the previous interface
+//   backward: beta_t  = T_{c_{t+1}} beta_{t+1},  beta_{T-1} = 1
+//   posterior_t = normalise(alpha_t o beta_t)
+//   ll = sum over steps with evidence of log m2_t - log m1_t, m2_t = sum alpha_t,
+//        m1_t = alpha_{t-1} . w (the mass the step would have without its
+//        evidence); a step without evidence adds nothing, as the general
+//        engine's filter (jtree.hip) and the reference (nip.c:1458-1474)
+// Messages carry their scale as exact powers of two (the ratio m2 / m1 is
+// taken at one scale).  Phase A / barrier / phase B with the scratch holding
+// alpha_t (t < H) and beta_t (t >= H), as chain_kernel<false>.
+#include <cfloat>
+
+#include "chain_kernels.h"
+#include "opchain.h"
+#include "diag.h"
+
+namespace nipamd {
+namespace {
+
+constexpr int kOpSeqs = 8;
+constexpr int kOpThreads = 256;
+constexpr int kOpGuard = 1;
+
+template <int K>
+__device__ __forceinline__ double ror(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int rl = __builtin_amdgcn_mov_dpp(lo, 0x120 + K, 0xF, 0xF, true);
+  const int rh = __builtin_amdgcn_mov_dpp(hi, 0x120 + K, 0xF, 0xF, true);
+  return __hiloint2double(rh, rl);
+}
+
+__device__ __forceinline__ double rsum(double x) {
+  asm("" : "+v"(x));                       // one rounded value per lane (no fma contraction)
+  x += ror<8>(x);
+  x += ror<4>(x);
+  x += ror<2>(x);
+  x += ror<1>(x);
+  return x;
+}
+
+template <int J, bool NOP>
+__device__ __forceinline__ void fbc(double& acc, double v, double c) {
+  if (NOP)
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(v), "v"(c), "n"(J));
+  else
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(v), "v"(c), "n"(J));
+}
+
+// sum_k x[lane k] * c[k] over the row (c[k] = 0 for k >= K)
+__device__ __forceinline__ double dot16(double x, const double (&c)[16]) {
+  double a0 = 0.0, a1 = 0.0;
+  fbc<0, true>(a0, x, c[0]);   fbc<1, false>(a1, x, c[1]);
+  fbc<2, false>(a0, x, c[2]);  fbc<3, false>(a1, x, c[3]);
+  fbc<4, false>(a0, x, c[4]);  fbc<5, false>(a1, x, c[5]);
+  fbc<6, false>(a0, x, c[6]);  fbc<7, false>(a1, x, c[7]);
+  fbc<8, false>(a0, x, c[8]);  fbc<9, false>(a1, x, c[9]);
+  fbc<10, false>(a0, x, c[10]); fbc<11, false>(a1, x, c[11]);
+  fbc<12, false>(a0, x, c[12]); fbc<13, false>(a1, x, c[13]);
+  fbc<14, false>(a0, x, c[14]); fbc<15, false>(a1, x, c[15]);
+  return a0 + a1;
+}
+
+__device__ __forceinline__ double div_or_keep(double x, double c) { return c != 0.0 ? x / c : x; }
+
+__host__ __device__ __forceinline__ int op_row(int T) { return T + 2 * kOpGuard; }
+
+}  // namespace
+
+__global__ __launch_bounds__(kOpThreads, 2)
+void op_fb_kernel(OpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int K = a.K, KK = K * K;
+  // operators in LDS when they fit (a.tlds), else read through the caches
+  const bool tl = a.tlds != 0;
+  double* Tl = reinterpret_cast<double*>(smem);                          // [(ncomb+1)][K][K] (tlds)
+  uint16_t* codes = reinterpret_cast<uint16_t*>(smem + (tl ? (size_t)(a.ncomb + 1) * KK * sizeof(double) : 0));
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int y = lane & 15, row = lane >> 4;
+  const bool fwd = row < 2;
+  const int seq = wave * 2 + (row & 1);
+  const long b0 = (long)blockIdx.x * kOpSeqs;
+  const long b = b0 + seq;
+  const bool active = b < a.B;
+  const int T = a.T, H = a.H;
+
+  if (tl)
+    for (int i = tid; i < (a.ncomb + 1) * KK; i += kOpThreads) Tl[i] = a.Ttab[i];
+  const int nseq = (int)((a.B - b0) < kOpSeqs ? (a.B - b0) : kOpSeqs);
+  for (int i = tid; i < kOpSeqs * T; i += kOpThreads) {
+    const int s = i / T, t = i - s * T;
+    int c = 0;
+    if (s < nseq && a.obs) {
+      const int32_t* o = a.obs + (b0 + s) * a.obs_bstride + (long)t * a.obs_tstride;
+      for (int k = 0; k < a.nobs; k++) {
+        const int v = o[a.col[k]];
+        if (v >= a.card[k]) { c = a.ncomb; break; }            // all-zero evidence: the zero table
+        if (v >= 0) c += (v + 1) * a.cstride[k];
+      }
+    }
+    codes[s * T + t] = (uint16_t)c;
+  }
+  __syncthreads();
+
+  const uint16_t* cd = codes + seq * T;
+  const double* const Tsrc = tl ? Tl : a.Ttab;
+  const bool ys = y < K;
+  const double wy = ys ? a.w[y] : 0.0;
+  double* const sink = a.S + (size_t)(a.B + 1) * op_row(T) * 16 + y;
+  double* const Srow = a.S + ((size_t)(active ? b : 0) * op_row(T) + kOpGuard) * 16 + y;
+  double* const Sst = active ? Srow : sink;
+  const long sst = active ? 16 : 0;
+  const bool pst = active && ys && a.post;
+  double* const Pst = pst ? a.post + (size_t)b * a.post_bstride + a.post_off + y : sink;
+  const long pstr = pst ? a.post_tstride : 0;
+
+  // this lane's column (forward) / row (backward) of T_c
+  auto coef = [&](int c, double (&C)[16]) {
+    const double* t = Tsrc + (size_t)c * KK;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      C[k] = (k < K && ys) ? (fwd ? t[k * K + y] : t[y * K + k]) : 0.0;
+  };
+
+  double x;                      // forward: alpha^_{t-1}; backward: beta^_{t+1}
+  int sc = 0;
+  double m2 = 1.0, m1 = 1.0;
+  int e2 = 0, e1 = 0;
+  bool dead = false;
+  if (fwd) {
+    x = ys ? a.pi[y] : 0.0;
+  } else {
+    x = ys ? 1.0 : 0.0;                                 // beta_{T-1}
+    if (!a.filter) Sst[(long)(T - 1) * sst] = x;
+  }
+
+  // One step of either direction, branch-free (the rows of a wave differ only
+  // in data): j-th step of the phase, t per direction; a row whose phase is
+  // shorter idles through its last steps (valid = false: state kept, stores
+  // to the sink).  combine: phase B (the posterior from the other
+  // direction's message).
+  // operator of the step at t (forward: c_t; backward: c_{t+1}), clamped
+  auto code_at = [&](int t) {
+    const int tc = t < 0 ? 0 : (t > T - 1 ? T - 1 : t);
+    return (int)cd[fwd ? tc : (tc + 1 < T ? tc + 1 : T - 1)];
+  };
+  double Cn[16];                 // the next step's coefficients, loaded one step ahead
+  auto step = [&](int t, int tnext, bool valid, bool combine) {
+    const int tc = t < 0 ? 0 : (t > T - 1 ? T - 1 : t);
+    const int c = code_at(t);
+    double C[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) C[k] = Cn[k];
+    coef(code_at(tnext), Cn);
+    const double m1v = rsum(x * wy);
+    const double u = __builtin_ldexp(dot16(x, C), sc);
+    const double z = rsum(u);
+    if (fwd && valid && c != 0) {                       // a forward step with evidence
+      m2 *= z;
+      m1 *= __builtin_ldexp(m1v, sc);
+      const int k2 = m2 != 0.0 ? __builtin_amdgcn_frexp_exp(m2) : 0;
+      const int k1 = m1 != 0.0 ? __builtin_amdgcn_frexp_exp(m1) : 0;
+      m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+      m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+    }
+    if (fwd && valid) dead |= z == 0.0;
+    if (a.filter) {
+      if (fwd) (valid ? Pst : sink)[(long)tc * (valid ? pstr : 0)] = div_or_keep(u, z);
+    } else if (!combine) {
+      (valid ? Sst : sink)[(long)tc * (valid ? sst : 0)] = u;
+    } else {
+      const double o = Srow[(long)tc * 16];
+      const double pr = u * o;
+      const double q = div_or_keep(pr, rsum(pr));
+      (valid ? Pst : sink)[(long)tc * (valid ? pstr : 0)] = q;
+    }
+    if (valid) {
+      sc = z != 0.0 ? -__builtin_amdgcn_frexp_exp(z) : 0;
+      x = u;
+    }
+  };
+
+  if (a.filter) {
+    coef(code_at(0), Cn);
+    for (int t = 0; t < T; t++) step(t, t + 1, fwd, false);
+  } else {
+    // phase A: forward t = 0..H-1, backward t = T-2..H
+    const int nA = H > T - 1 - H ? H : T - 1 - H;
+    const int dir = fwd ? 1 : -1;
+    coef(code_at(fwd ? 0 : T - 2), Cn);
+    for (int j = 0; j < nA; j++) {
+      const int t = fwd ? j : T - 2 - j;
+      step(t, t + dir, fwd ? j < H : t >= H, false);
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // phase B: forward t = H..T-1 with beta_t, backward t = H-1..0 with alpha_t
+    const int nB = T - H > H ? T - H : H;
+    coef(code_at(fwd ? H : H - 1), Cn);
+    for (int j = 0; j < nB; j++) {
+      const int t = fwd ? H + j : H - 1 - j;
+      step(t, t + dir, fwd ? t < T : t >= 0, true);
+    }
+  }
+  if (fwd && active && y == 0) {
+    double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 1u : 0u;        // NIPAMD_STATUS_ZERO_MASS
+  }
+}
+
+size_t op_lds_bytes(int K, int ncomb, int T, bool tables) {
+  return (tables ? (size_t)(ncomb + 1) * K * K * sizeof(double) : 0) + (size_t)kOpSeqs * T * sizeof(uint16_t);
+}
+
+size_t op_scratch_bytes(long B, int T) { return (size_t)(B + 2) * op_row(T) * 16 * sizeof(double); }
+
+int op_fb_launch(const OpArgs& a, hipStream_t stream) {
+  if (a.B <= 0) return 0;
+  OpArgs b = a;
+  // operators in LDS while two blocks still fit a CU (80 KB each); the
+  // diagnostics build can force either (NIPAMD_OP_TLDS=0/1)
+  b.tlds = op_lds_bytes(a.K, a.ncomb, a.T, true) <= 80 * 1024 ? 1 : 0;
+  if (const char* e = diag_env("NIPAMD_OP_TLDS")) b.tlds = (e[0] == '1' && op_lds_bytes(a.K, a.ncomb, a.T, true) <= 150 * 1024) ? 1 : 0;
+  const size_t lds = (op_lds_bytes(a.K, a.ncomb, a.T, b.tlds != 0) + 15) & ~(size_t)15;
+  if (lds > 160 * 1024 || a.K > 16 || a.ncomb > 65534) return -2;
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_fb_kernel), lds, lds_set)) return -1;
+  const int blocks = (int)((a.B + kOpSeqs - 1) / kOpSeqs);
+  hipLaunchKernelGGL(op_fb_kernel, dim3(blocks), dim3(kOpThreads), lds, stream, b);
+  g_last_kernel = "op_fb_kernel";
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace nipamd
