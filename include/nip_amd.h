@@ -123,8 +123,11 @@ int nipamd_model_gpu_supported(const nipamd_model* m, int n_obs,
 /*
  * Engine selection for a model (not part of the reference API).
  *   NIPAMD_ENGINE_AUTO   the interface-chain kernels where the slice is an
- *                        interface chain and they fit, else the general
- *                        join-tree engine (jtree.hip)
+ *                        interface chain and they fit, else (fb / filter
+ *                        of current-interface variables, <= 16 joint
+ *                        interface states) the evidence-indexed chain
+ *                        (opchain.hip), else the general join-tree engine
+ *                        (jtree.hip)
  *   NIPAMD_ENGINE_CHAIN  interface-chain kernels only (UNSUPPORTED otherwise)
  *   NIPAMD_ENGINE_JTREE  the general join-tree engine for every request
  * Both run on the GPU; there is no CPU path.  Returns the previous value.

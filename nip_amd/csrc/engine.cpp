@@ -528,7 +528,7 @@ int nipamd_model_gpu_supported(const nipamd_model* mm, int n_obs, const int* obs
   if (!mm) return 0;
   Route r; std::string why;
   if (mm->engine != NIPAMD_ENGINE_JTREE && route_request(mm, n_obs, obs_vars, n_query, query, r, why)) return 1;
-  if (mm->engine != NIPAMD_ENGINE_JTREE &&
+  if (mm->engine == NIPAMD_ENGINE_AUTO &&
       nipamd::op_supported(const_cast<nipamd_model*>(mm), n_obs, obs_vars, n_query, query, why))
     return 1;
   return mm->engine != NIPAMD_ENGINE_CHAIN && nipamd::jt_supported(mm, n_obs, obs_vars, n_query, query, why);
@@ -962,11 +962,14 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
       if (query_kind(mm->m.chain, query[i]) >= 1000 && pick_kernel(mm, r, rt, T, true) == kNoChain) kk = kNoChain;
     if (kk == kNoChain) why = "sequence too long for the interface-chain kernels' LDS-resident codes";
   }
-  if (kk == kNoChain && mm->engine != NIPAMD_ENGINE_JTREE) {
+  if (kk == kNoChain && mm->engine == NIPAMD_ENGINE_AUTO) {
     // the evidence-indexed interface chain (opchain.h): the slice as one K x K
     // operator per evidence combination, K <= 16 joint interface states
+    // (automatic engine choice only: NIPAMD_ENGINE_CHAIN is the chain plan's
+    // kernels, NIPAMD_ENGINE_JTREE the general engine)
     std::string why2;
-    if (nipamd::op_supported(mm, n_obs, obs_vars, n_query, query, why2)) {
+    if (nipamd::op_supported(mm, n_obs, obs_vars, n_query, query, why2) &&
+        nipamd::op_fits(mm, n_obs, obs_vars, T)) {
       if (int rc = ensure_device(mm)) return rc;
       const auto& out = mm->m.outgoing;
       std::string err;

@@ -181,6 +181,7 @@ bool op_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
 int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T, double* d_joint,
           long jbs, int jts, int joff, double* d_ll, uint32_t* d_status, void* stream, bool filt, int* K_out,
           std::string& err);
+bool op_fits(nipamd_model* mm, int n_obs, const int* obs_vars, int T);
 void op_release(nipamd_model* mm);
 // jtree_plan.cpp: the general join-tree engine (jtree.h)
 int jt_supported(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,

@@ -183,6 +183,12 @@ bool op_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
   return true;
 }
 
+// The kernel stages the block's evidence codes in LDS: does T fit?
+bool op_fits(nipamd_model* mm, int n_obs, const int* obs_vars, int T) {
+  OpPlan* P = plan_for(mm, n_obs, obs_vars);
+  return P->ok && op_lds_bytes(P->K, P->ncomb, T, false) <= 150 * 1024;
+}
+
 // The joint interface's posterior (or filtered) marginals into d_joint
 // [B][T][K] (or straight into the caller's rows when jts == K), ll, status.
 int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T, double* d_joint,

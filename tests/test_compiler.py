@@ -87,7 +87,8 @@ def test_chain_plan_recognition():
     assert d.gpu_supported([d.variable("B1")], [d.variable("C1")])
     # every variable of the slice can be queried (derived marginals: prev, hidden parent, children)
     assert d.gpu_supported([d.variable("A1")], [d.variable(v) for v in ("D1", "C0", "B1", "A1")])
-    # evidence on a folded parent: outside the chain plan, served by the general engine
+    # evidence on a folded parent: outside the chain plan; the automatic choice
+    # serves it on the evidence-indexed chain (opchain.cpp)
     d.set_engine(nip_amd.ENGINE_CHAIN)
     assert not d.gpu_supported([d.variable("D1")], [d.variable("C1")])
     d.set_engine(nip_amd.ENGINE_AUTO)
