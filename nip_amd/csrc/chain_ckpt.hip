@@ -423,6 +423,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   double* Et = zr + kZD;                             // [(M+2)][kEtStride]
   uint8_t* codes = reinterpret_cast<uint8_t*>(Et + (a.M + 2) * kEtStride);   // [16][Tr]
   auto nozero = [] {};
+  const unsigned long long t_entry = NIPAMD_WAIT_TIMES ? __builtin_readcyclecounter() : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -494,6 +495,9 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   else filter_wave<false, false, true, 1>(a, c, Et, Sw, lane, true, b0 + j, nchA, nchB, nullptr);
   barrier_lds();
   dg.tb = dg.ta = dg.t0;                             // the filters: total only (slot 2)
+  dg.x2 = dg.t0 - t_entry;                           // and the prologue (staging) in slot 1
+  dg.rc = true;
+  dg.x1 = 0;
   dg.write(a, wave, lane);
 }
 
