@@ -45,6 +45,12 @@ struct ChainArgs {
   unsigned* status;      // [B] or nullptr
   double* counts;        // E-step only: per-sequence slabs [B][chain_estep_slab(M)]
   unsigned long long* diag;   // diagnostics builds only: per-block wall-clock stamps, else null
+  // chain_estep16_kernel, one evidence table per leaf child of the plan
+  // (ChainPlan::emits, at most 4): its column in obs (-1: never observed, the
+  // code is always "missing"), cardinality and first row in Etab / the count
+  // tables (rows M_k + 2 each; a.M + 2 = their sum)
+  int ne;
+  int ecol[4], eM[4], erow[4];
   // chain_fb_ckpt_kernel, joint interface: write the marginals of up to four of
   // its variables instead of the joint posterior (post_tstride = their summed
   // cardinalities).  proj_digit[j][i]: variable j's value at joint state i (-1
@@ -233,7 +239,7 @@ int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
 // sequences per block, direction-uniform waves, analytic phase-B normalisation;
 // its scratch holds the messages plus one exponent per (sequence, step)
 int chain_estep16_launch(const ChainArgs& a, hipStream_t stream);
-size_t chain_estep16_lds_bytes(int M, int T);
+size_t chain_estep16_lds_bytes(int M, int T, int ne);
 size_t chain_estep16_scratch_bytes(long B, int T);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);

@@ -505,39 +505,47 @@ namespace {
 
 __host__ __device__ inline long estep16_xrow(int T) { return (long)T + 2 * kGuard; }
 
+template <int NE>
 struct E16Ctx {
-  const double* Et;        // LDS evidence table, this lane's column (Et + y)
-  const uint8_t* codes;    // LDS codes of this sequence; codes[-kGuard .. T+kGuard)
+  const double* Et;        // LDS evidence tables, this lane's column (Et + y)
+  const uint8_t* codes[NE];   // LDS codes of this sequence per leaf child; codes[k][-kGuard .. T+kGuard)
+  int erow16[NE];          // first row of child k's table, times 16
   const double* Sload;     // scratch message row of this sequence (+y)
   double* Sstore;          // same, or a sink
   long Sstride;            // 16, or 0 for the sink
   const int* Xload;        // scratch exponent row of this sequence
 };
 
-template <int KC>
+template <int KC, int NE>
 struct Prefetch16 {
-  double e[KC];
+  double e[KC];            // the step's evidence column: product over the children
   double s[KC];
-  int c[KC];
+  int c[KC][NE];           // count-table rows (child k's first row + its code)
   int x[KC];
 };
 
-template <int KC>
-__device__ __forceinline__ void load_chunk16(const E16Ctx& c, Prefetch16<KC>& p, int t0, int dir, bool with_s) {
-  int code[KC];
+template <int KC, int NE>
+__device__ __forceinline__ void load_chunk16(const E16Ctx<NE>& c, Prefetch16<KC, NE>& p, int t0, int dir,
+                                             bool with_s) {
 #pragma unroll
   for (int j = 0; j < KC; j++) {
     const int t = t0 + dir * j;
-    code[j] = c.codes[t];
+#pragma unroll
+    for (int k = 0; k < NE; k++) p.c[j][k] = c.erow16[k] + c.codes[k][t] * 16;
     if (with_s) { p.s[j] = c.Sload[(long)t * 16]; p.x[j] = c.Xload[t]; }
   }
 #pragma unroll
-  for (int j = 0; j < KC; j++) { p.e[j] = c.Et[code[j] * 16]; p.c[j] = code[j]; }
+  for (int j = 0; j < KC; j++) {
+    double e = c.Et[p.c[j][0]];
+#pragma unroll
+    for (int k = 1; k < NE; k++) e *= c.Et[p.c[j][k]];
+    p.e[j] = e;
+  }
 }
 
-template <int KC, typename Step>
-__device__ __forceinline__ void run_phase16(const E16Ctx& c, int n, int t0, int dir, bool with_s, Step&& step) {
-  Prefetch16<KC> pa, pb;
+template <int KC, int NE, typename Step>
+__device__ __forceinline__ void run_phase16(const E16Ctx<NE>& c, int n, int t0, int dir, bool with_s, Step&& step) {
+  Prefetch16<KC, NE> pa, pb;
   if (n <= 0) return;
   load_chunk16(c, pa, t0, dir, with_s);
   for (int base = 0; base < n; base += 2 * KC) {
@@ -570,9 +578,9 @@ __device__ __forceinline__ double dot2_bcast(double x, const double (&c)[16]) {
 }
 
 // One direction's rows of a block (FWD: waves 0-3, backward: waves 4-7).
-template <bool FWD, int KC>
+template <bool FWD, int KC, int NE>
 __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* Et, const uint8_t* codes,
-                                             double* Htab, double* m1x, int lane, int grp, long b0) {
+                                             double* Htab, double* m1x, int lane, int grp, long b0, int nseqb) {
   const int y = lane & 15, row = lane >> 4;
   const int seq = grp * 4 + row;                    // within the block
   const long b = b0 + seq;
@@ -583,12 +591,20 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   double C[16];   // forward: column y of A (C[k] = A[k][y]); backward: row y (A[y][k])
 #pragma unroll
   for (int k = 0; k < 16; k++) C[k] = FWD ? a.A[k * 16 + y] : a.A[y * 16 + k];
-  const double s_y = Et[M * 16 + y];
+  // s(y): the product of the children's missing rows (each child's row
+  // sums; the factor of a step that observes nothing)
+  auto s_of = [&](int j) {
+    double v = Et[(a.erow[0] + a.eM[0]) * 16 + j];
+#pragma unroll
+    for (int k = 1; k < NE; k++) v *= Et[(a.erow[k] + a.eM[k]) * 16 + j];
+    return v;
+  };
+  const double s_y = s_of(y);
   // backward rows: (A s)(x) for lane x -- the phase-A steps' m1 (below)
   double As = 0.0;
   if (!FWD) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) As = __builtin_fma(C[k], Et[M * 16 + k], As);
+    for (int k = 0; k < 16; k++) As = __builtin_fma(C[k], s_of(k), As);
   }
 
   const long nrow = (a.B + kE16RowMul - 1) / kE16RowMul * kE16RowMul;
@@ -596,9 +612,13 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   double* const Srow = a.S + (size_t)(active ? b : 0) * chain_scratch_row(T) + (size_t)kGuard * 16 + y;
   int* const X = reinterpret_cast<int*>(a.S + (size_t)(nrow + 2) * chain_scratch_row(T));
   int* const Xrow = X + (size_t)(active ? b : 0) * estep16_xrow(T) + kGuard;
-  E16Ctx cx;
+  E16Ctx<NE> cx;
   cx.Et = Et + y;
-  cx.codes = codes + seq * Tr + kGuard;
+#pragma unroll
+  for (int k = 0; k < NE; k++) {
+    cx.codes[k] = codes + ((size_t)k * nseqb + seq) * Tr + kGuard;
+    cx.erow16[k] = a.erow[k] * 16;
+  }
   cx.Sload = Srow;
   cx.Sstore = active ? Srow : sink;
   cx.Sstride = active ? 16 : 0;
@@ -626,7 +646,10 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     const double beta = (active && y < a.N) ? 1.0 : 0.0;
     cx.Sstore[(long)(T - 1) * cx.Sstride] = beta;     // beta_{T-1} = 1, exponent 0
     if (xw) Xrow[T - 1] = 0;
-    x = Et[cx.codes[T - 1] * 16 + y] * beta;
+    double e0 = Et[cx.erow16[0] + cx.codes[0][T - 1] * 16 + y];
+#pragma unroll
+    for (int k = 1; k < NE; k++) e0 *= Et[cx.erow16[k] + cx.codes[k][T - 1] * 16 + y];
+    x = e0 * beta;
     sc = -exp2_of(row_sum(x));
   }
 
@@ -641,14 +664,18 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   int E0 = 0;                 //          and that step's exponent sum
 
   // one step; combine: phase B (posterior, M1 count, xi), first: its first step
-  auto step = [&](int t, double e, double other, int xo, int code, bool combine, bool first, int j) {
-    // phase B: this step's M1 count cell, read before the step's arithmetic
-    // so the LDS latency overlaps it (the previous step's write to the same
-    // cell precedes it in the wave's LDS order)
-    double hv = 0.0;
-    if (combine) {
-      hv = Hrow[code * 16];
-      asm volatile("" : "+v"(hv));                   // keep the read here
+  auto step = [&](int t, double e, double other, int xo, const int (&code)[NE], bool combine, bool first, int j) {
+    // phase B: this step's count cells (one per child), read before the
+    // step's arithmetic so the LDS latency overlaps it (the previous step's
+    // write to the same cell precedes it in the wave's LDS order)
+    double hv[NE];
+#pragma unroll
+    for (int k = 0; k < NE; k++) {
+      hv[k] = 0.0;
+      if (combine) {
+        hv[k] = Hrow[code[k]];
+        asm volatile("" : "+v"(hv[k]));              // keep the read here
+      }
     }
     const double u = __builtin_ldexp(dot2_bcast(x, C), sc);
     const int eu = ex + sc;                          // exponent of u (and of p)
@@ -674,7 +701,8 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
         E0 = eu + xo;
       }
       const double q = __builtin_ldexp(pr * rc0, E0 - (eu + xo));
-      Hrow[code * 16] = hv + q;
+#pragma unroll
+      for (int k = 0; k < NE; k++) Hrow[code[k]] = hv[k] + q;
       // xi_t (forward, x = alpha^_{t-1}) / xi_{t+1} (backward, x = g_{t+1}, t + 1 < H):
       // x(.) A e_t beta_t / Z resp. alpha_t A g_{t+1} / Z, the A factor applied after the reduction
       const double f = __builtin_ldexp(rc0, E0 - (ex + xo));
@@ -702,8 +730,10 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   unsigned long long st[4] = {0, 0, 0, 0};
   if (NIPAMD_WAIT_TIMES) st[0] = __builtin_readcyclecounter();
   // phase A: forward t = 0..H-1; backward t = T-2..H
-  run_phase16<KC>(cx, FWD ? H : T - 1 - H, FWD ? 0 : T - 2, dir, false,
-                  [&](int t, double e, double o, int xo, int c, int j) { step(t, e, o, xo, c, false, false, j); });
+  run_phase16<KC, NE>(cx, FWD ? H : T - 1 - H, FWD ? 0 : T - 2, dir, false,
+                      [&](int t, double e, double o, int xo, const int (&c)[NE], int j) {
+                        step(t, e, o, xo, c, false, false, j);
+                      });
   const int efa = ex;                                // forward: Ef_{H-1}, the phase-A m1 exponents' sum
   if (NIPAMD_WAIT_TIMES) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); st[1] = __builtin_readcyclecounter(); }
   __syncthreads();
@@ -714,9 +744,17 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     const int n = FWD ? T - H : H;
     const int t0 = FWD ? H : H - 1;
     if (n > 0) {
-      step(t0, cx.Et[cx.codes[t0] * 16], cx.Sload[(long)t0 * 16], cx.Xload[t0], cx.codes[t0], true, true, 3);
-      run_phase16<KC>(cx, n - 1, t0 + dir, dir, true,
-                      [&](int t, double e, double o, int xo, int c, int j) { step(t, e, o, xo, c, true, false, j); });
+      int c0[NE];
+#pragma unroll
+      for (int k = 0; k < NE; k++) c0[k] = cx.erow16[k] + cx.codes[k][t0] * 16;
+      double e0 = cx.Et[c0[0]];
+#pragma unroll
+      for (int k = 1; k < NE; k++) e0 *= cx.Et[c0[k]];
+      step(t0, e0, cx.Sload[(long)t0 * 16], cx.Xload[t0], c0, true, true, 3);
+      run_phase16<KC, NE>(cx, n - 1, t0 + dir, dir, true,
+                          [&](int t, double e, double o, int xo, const int (&c)[NE], int j) {
+                            step(t, e, o, xo, c, true, false, j);
+                          });
     }
   }
   if (NIPAMD_WAIT_TIMES) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); st[3] = __builtin_readcyclecounter(); }
@@ -787,15 +825,16 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
 
 }  // namespace
 
-template <int NSEQ, int KC>
+template <int NSEQ, int KC, int NE>
 __global__ __launch_bounds__(NSEQ * 32, 1)
 void chain_estep16_kernel(ChainArgs a) {
   constexpr int kE16Seqs = NSEQ, kE16Threads = NSEQ * 32, G = NSEQ / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* Et = reinterpret_cast<double*>(smem);                         // [(M+2)][16]
-  uint8_t* codes = smem + (size_t)(a.M + 2) * 16 * sizeof(double);      // [16][Tr]
+  const int R = a.M + 2;                                                // table rows, all children
+  double* Et = reinterpret_cast<double*>(smem);                         // [R][16]
+  uint8_t* codes = smem + (size_t)R * 16 * sizeof(double);              // [NE][NSEQ][Tr]
   double* Htab = reinterpret_cast<double*>(
-      codes + (((size_t)kE16Seqs * chain_codes_row(a.T) + 15) & ~(size_t)15));   // [NSEQ][2][(M+2)][16]
+      codes + (((size_t)NE * kE16Seqs * chain_codes_row(a.T) + 15) & ~(size_t)15));   // [NSEQ][2][R][16]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const long b0 = (long)blockIdx.x * kE16Seqs;
@@ -803,13 +842,17 @@ void chain_estep16_kernel(ChainArgs a) {
   const int Tr = chain_codes_row(T);
   const unsigned long long t_entry = NIPAMD_WAIT_TIMES ? __builtin_readcyclecounter() : 0;
 
-  for (int i = tid; i < (a.M + 2) * 16; i += kE16Threads) Et[i] = a.Etab[i];
+  for (int i = tid; i < R * 16; i += kE16Threads) Et[i] = a.Etab[i];
   const int nseq = (int)((a.B - b0) < kE16Seqs ? (a.B - b0) : kE16Seqs);
-  auto code_of = [&](int o) -> int { return o < 0 ? a.M : (o < a.M ? o : a.M + 1); };
-  for (int i = tid; i < kE16Seqs * Tr; i += kE16Threads) codes[i] = (uint8_t)a.M;   // missing / guard
-  for (int i = tid; i < kE16Seqs * 2 * (a.M + 2) * 16; i += kE16Threads) Htab[i] = 0.0;
+  // child k's code: its state, eM[k] missing, eM[k] + 1 out of range (an all-zero row)
+  auto code_of = [&](int k, int o) -> int { return o < 0 ? a.eM[k] : (o < a.eM[k] ? o : a.eM[k] + 1); };
+#pragma unroll
+  for (int k = 0; k < NE; k++)
+    for (int i = tid; i < kE16Seqs * Tr; i += kE16Threads) codes[(size_t)k * kE16Seqs * Tr + i] = (uint8_t)a.eM[k];
+  for (int i = tid; i < kE16Seqs * 2 * R * 16; i += kE16Threads) Htab[i] = 0.0;
   __syncthreads();
-  if (a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 && nseq == kE16Seqs) {
+  if (NE == 1 && a.ecol[0] >= 0 && a.obs && a.obs_tstride == 1 && a.obs_bstride == T && (T & 3) == 0 &&
+      nseq == kE16Seqs) {
     const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * (long)T);
     const int n4 = (kE16Seqs * T) >> 2;
     for (int i0 = tid; i0 < n4; i0 += kE16Threads * 8) {
@@ -821,8 +864,8 @@ void chain_estep16_kernel(ChainArgs a) {
         const int i4 = i0 + k * kE16Threads;
         if (i4 < n4) {
           const int i = i4 << 2, c = i / T, t = i - c * T;
-          const uint32_t packed = (uint32_t)code_of(r[k].x) | ((uint32_t)code_of(r[k].y) << 8) |
-                                  ((uint32_t)code_of(r[k].z) << 16) | ((uint32_t)code_of(r[k].w) << 24);
+          const uint32_t packed = (uint32_t)code_of(0, r[k].x) | ((uint32_t)code_of(0, r[k].y) << 8) |
+                                  ((uint32_t)code_of(0, r[k].z) << 16) | ((uint32_t)code_of(0, r[k].w) << 24);
           *reinterpret_cast<uint32_t*>(codes + c * Tr + kGuard + t) = packed;
         }
       }
@@ -830,17 +873,19 @@ void chain_estep16_kernel(ChainArgs a) {
   } else if (a.obs) {
     for (int i = tid; i < nseq * T; i += kE16Threads) {
       const int c = i / T, t = i - c * T;
-      codes[c * Tr + kGuard + t] =
-          (uint8_t)code_of(a.obs[(b0 + c) * a.obs_bstride + (long)t * a.obs_tstride + a.obs_col]);
+      const int* o = a.obs + (b0 + c) * a.obs_bstride + (long)t * a.obs_tstride;
+#pragma unroll
+      for (int k = 0; k < NE; k++)
+        if (a.ecol[k] >= 0) codes[((size_t)k * kE16Seqs + c) * Tr + kGuard + t] = (uint8_t)code_of(k, o[a.ecol[k]]);
     }
   }
   __syncthreads();
-  double* m1x = Htab + kE16Seqs * 2 * (a.M + 2) * 16;                   // [NSEQ][4]
-  if (wave < G) estep16_rows<true, KC>(a, Et, codes, Htab, m1x, lane, wave, b0);
-  else estep16_rows<false, KC>(a, Et, codes, Htab, m1x, lane, wave - G, b0);
+  double* m1x = Htab + kE16Seqs * 2 * R * 16;                           // [NSEQ][4]
+  if (wave < G) estep16_rows<true, KC, NE>(a, Et, codes, Htab, m1x, lane, wave, b0, kE16Seqs);
+  else estep16_rows<false, KC, NE>(a, Et, codes, Htab, m1x, lane, wave - G, b0, kE16Seqs);
   __syncthreads();
-  for (int i = tid; i < kE16Seqs * 2 * (a.M + 2) * 16; i += kE16Threads) {
-    const int sq = i / (2 * (a.M + 2) * 16), r = i - sq * 2 * (a.M + 2) * 16;
+  for (int i = tid; i < kE16Seqs * 2 * R * 16; i += kE16Threads) {
+    const int sq = i / (2 * R * 16), r = i - sq * 2 * R * 16;
     if (b0 + sq < a.B) a.counts[(size_t)(b0 + sq) * chain_estep_slab(a.M) + kSlabH + r] = Htab[i];
   }
   if (NIPAMD_WAIT_TIMES && a.diag && lane == 0) {
@@ -858,12 +903,18 @@ static int estep16_seqs() {
   return n;
 }
 
-static size_t estep16_lds(int nseq, int M, int T) {
-  const size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)nseq * chain_codes_row(T);
+static size_t estep16_lds(int nseq, int M, int T, int ne) {
+  const size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)ne * nseq * chain_codes_row(T);
   return ((n + 15) & ~(size_t)15) + (size_t)nseq * 2 * (M + 2) * 16 * sizeof(double) + (size_t)nseq * 4 * sizeof(double);
 }
 
-size_t chain_estep16_lds_bytes(int M, int T) { return estep16_lds(estep16_seqs(), M, T); }
+// sequences per block: 16, or 8 when the children's count tables of 16 do not fit
+static int estep16_nseq(int M, int T, int ne) {
+  if (ne == 1) return estep16_seqs();
+  return estep16_lds(16, M, T, ne) <= 160 * 1024 ? 16 : 8;
+}
+
+size_t chain_estep16_lds_bytes(int M, int T, int ne) { return estep16_lds(estep16_nseq(M, T, ne), M, T, ne); }
 
 size_t chain_estep16_scratch_bytes(long B, int T) {
   const long nrow = (B + kE16RowMul - 1) / kE16RowMul * kE16RowMul;
@@ -871,21 +922,28 @@ size_t chain_estep16_scratch_bytes(long B, int T) {
          (size_t)(nrow + 2) * estep16_xrow(T) * sizeof(int);
 }
 
-template <int NSEQ, int KC>
+template <int NSEQ, int KC, int NE>
 static int estep16_launch(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC>), lds, lds_set)) return -1;
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC, NE>), lds, lds_set)) return -1;
   const int blocks = (int)((a.B + NSEQ - 1) / NSEQ);
-  hipLaunchKernelGGL((chain_estep16_kernel<NSEQ, KC>), dim3(blocks), dim3(NSEQ * 32), lds, stream, a);
+  hipLaunchKernelGGL((chain_estep16_kernel<NSEQ, KC, NE>), dim3(blocks), dim3(NSEQ * 32), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int chain_estep16_launch(const ChainArgs& a, hipStream_t stream) {
-  const int nseq = estep16_seqs();
-  const size_t lds = (estep16_lds(nseq, a.M, a.T) + 15) & ~(size_t)15;
+  if (a.ne < 1 || a.ne > 3) return -2;                           // four children spill: general engine
+  const int nseq = estep16_nseq(a.M, a.T, a.ne);
+  const size_t lds = (estep16_lds(nseq, a.M, a.T, a.ne) + 15) & ~(size_t)15;
   if (lds > 160 * 1024 || a.N > 16 || !a.counts) return -2;
   g_last_kernel = "chain_estep16_kernel";
-  return nseq == 24 ? estep16_launch<24, 4>(a, lds, stream) : estep16_launch<16, NIPAMD_ESTEP_CHUNK>(a, lds, stream);
+  constexpr int KC = NIPAMD_ESTEP_CHUNK;
+  switch (a.ne) {
+    case 1: return nseq == 24 ? estep16_launch<24, 4, 1>(a, lds, stream) : estep16_launch<16, KC, 1>(a, lds, stream);
+    case 2: return nseq == 8 ? estep16_launch<8, KC, 2>(a, lds, stream) : estep16_launch<16, KC, 2>(a, lds, stream);
+    default:                                                       // 4-step prefetch: no spills
+      return nseq == 8 ? estep16_launch<8, 4, 3>(a, lds, stream) : estep16_launch<16, 4, 3>(a, lds, stream);
+  }
 }
 
 size_t chain_lds_bytes(int M, int T, bool estep) {

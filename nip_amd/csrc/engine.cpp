@@ -81,6 +81,9 @@ struct DevState {
   int* jm_idx = nullptr;
   double* jm_coef = nullptr;
   int jm_n = 0;
+  // general chain e_step (several leaf children, hidden parents): every
+  // child's table, rows M_k + 2 each (E, the row sums, zeros), 16 columns
+  double* etab_all = nullptr;
 };
 
 DevState* dev_of(nipamd_model* mm) {
@@ -103,6 +106,8 @@ void free_tables(DevState* d) {
   d->G.clear();
   (void)hipFree(d->jm_ptr); (void)hipFree(d->jm_idx); (void)hipFree(d->jm_coef);
   d->jm_ptr = nullptr; d->jm_idx = nullptr; d->jm_coef = nullptr; d->jm_n = 0;
+  (void)hipFree(d->etab_all);
+  d->etab_all = nullptr;
 }
 
 void dev_release(DevState* d) {
@@ -1177,10 +1182,27 @@ int nipamd_filter_host(nipamd_model* mm, const int32_t* obs, int n_obs, const in
 // layout -- so partials of different routes (another T, another engine
 // setting, another rank) that were combined are detected by the finalize
 // instead of being summed silently.
+// A chain plan the general chain e_step takes: one interface variable of at
+// most 16 states, 1..3 leaf children, hidden independent parents (their
+// families follow from the xi sums, ensure_chain_map).
+static bool estep_general_plan(const nipamd::ChainPlan& P) {
+  return P.valid && !P.joint && !P.hmm && P.N <= 16 && !P.emits.empty() && P.emits.size() <= 3 &&
+         !P.fold_gpu;
+}
+// the count-table rows of every child: sum_k (M_k + 2)
+static int estep_rows(const nipamd::ChainPlan& P) {
+  int R = 0;
+  for (const auto& e : P.emits) R += e.M + 2;
+  return R;
+}
+
 static int estep_body_size(const nipamd_model* mm) {
   const int ps = nipamd::param_size(mm->m);
-  if (mm->engine != NIPAMD_ENGINE_JTREE && mm->m.chain.valid && (mm->m.chain.hmm || mm->m.chain.jhmm))
-    return std::max(ps, nipamd::chain_estep_slab(mm->m.chain.emits[0].M));
+  const auto& P = mm->m.chain;
+  if (mm->engine != NIPAMD_ENGINE_JTREE && P.valid && (P.hmm || P.jhmm))
+    return std::max(ps, nipamd::chain_estep_slab(P.emits[0].M));
+  if (mm->engine != NIPAMD_ENGINE_JTREE && estep_general_plan(P))
+    return std::max(ps, nipamd::chain_estep_slab(estep_rows(P) - 2));
   return mm->engine == NIPAMD_ENGINE_CHAIN ? -1 : ps;
 }
 
@@ -1198,21 +1220,28 @@ int nipamd_estep_partial_size(const nipamd_model* mm) {
 // Measured on config 4.
 static int chain_estep_kernel(const nipamd_model* mm, int T) {
   const auto& P = mm->m.chain;
+  if (estep_general_plan(P))                       // only chain_estep16_kernel takes several children
+    return nipamd::chain_estep16_lds_bytes(estep_rows(P) - 2, T, (int)P.emits.size()) <= 160 * 1024 ? 3 : 0;
   const int M = P.emits[0].M;
   const char* ek = nipamd::diag_env("NIPAMD_ESTEP_KERNEL");
   const std::string want = ek ? ek : "";
   if (want == "mfma" && P.N <= 16 && M <= 16 && nipamd::chain_estep_mfma_lds_bytes(M, T) <= 160 * 1024) return 1;
-  if (want != "dpp8" && P.N <= 16 && nipamd::chain_estep16_lds_bytes(M, T) <= 160 * 1024) return 3;
+  if (want != "dpp8" && P.N <= 16 && nipamd::chain_estep16_lds_bytes(M, T, 1) <= 160 * 1024) return 3;
   if (nipamd::chain_lds_bytes(M, T, true) <= 96 * 1024) return 2;
   return 0;
 }
 
 static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r) {
   std::string why;
-  if (mm->engine == NIPAMD_ENGINE_JTREE || !mm->m.chain.valid || !(mm->m.chain.hmm || mm->m.chain.jhmm))
-    return false;
+  const auto& P = mm->m.chain;
+  const bool general = estep_general_plan(P);
+  if (mm->engine == NIPAMD_ENGINE_JTREE || !P.valid || !(P.hmm || P.jhmm || general)) return false;
   if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why)) return false;
-  if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0)) return false;   // evidence on the child only
+  if (general) {                                   // evidence on leaf children only (not on the interface)
+    for (int i = 0; i < r.ncol; i++) if (r.emit[i] >= (int)P.emits.size()) return false;
+  } else if (r.ncol > 1 || (r.ncol == 1 && r.emit[0] != 0)) {
+    return false;                                  // evidence on the child only
+  }
   return chain_estep_kernel(mm, T) != 0;
 }
 
@@ -1238,6 +1267,7 @@ static int prefix_first_bad(nipamd_model* mm, int T) {
 static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                                 int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
                                 void* stream);
+static int ensure_etab_all(nipamd_model* mm);
 
 int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                          int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
@@ -1277,8 +1307,9 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     return 0;
   }
   const auto& P = mm->m.chain;
+  const bool general = estep_general_plan(P);
   const int col = r.pcol;
-  const int Mo = P.emits[0].M;
+  const int Mo = general ? estep_rows(P) - 2 : P.emits[0].M;   // the slab's count-table rows - 2
   const int S = nipamd::chain_estep_slab(Mo);
   const int ek = chain_estep_kernel(mm, T);
   const bool mfma = ek == 1;
@@ -1292,6 +1323,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   rh.primary = 0;
   ReqTables* rt = nullptr;
   if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
+  if (general)
+    if (int rc = ensure_etab_all(mm)) return rc;
   const long chunk = B < kEstepChunk ? B : kEstepChunk;
   const long nchunks = (B + kEstepChunk - 1) / kEstepChunk;
   const long rows = (chunk + per_row - 1) / per_row;
@@ -1310,14 +1343,24 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     const long b0 = c * kEstepChunk;
     const int nb = (int)((B - b0) < kEstepChunk ? (B - b0) : kEstepChunk);
     nipamd::ChainArgs a{};
-    a.obs = col >= 0 ? d_obs + b0 * T * ocols : nullptr;
+    a.obs = (general ? r.ncol > 0 : col >= 0) ? d_obs + b0 * T * ocols : nullptr;
     a.obs_bstride = (long)T * ocols;
     a.obs_tstride = ocols;
     a.obs_col = col;
     a.B = nb; a.T = T; a.H = T / 2; a.N = P.N; a.M = Mo;
     if (const char* hp = nipamd::diag_env("NIPAMD_ESTEP_H"))    // split point in % of T (A/B builds)
       if (ek == 3) a.H = std::min(T - 1, std::max(0, (int)((long)T * std::atoi(hp) / 100)));
-    a.A = d->A; a.Etab = rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
+    a.A = d->A; a.Etab = general ? d->etab_all : rt->Etab16; a.pi = d->pi; a.ts = rt->ts16; a.S = d->S;
+    // chain_estep16_kernel's children: the HMM's one (the primary table), or every leaf child
+    a.ne = general ? (int)P.emits.size() : 1;
+    for (int k = 0, row = 0; k < a.ne; k++) {
+      a.eM[k] = general ? P.emits[k].M : Mo;
+      a.erow[k] = row;
+      row += a.eM[k] + 2;
+      a.ecol[k] = general ? -1 : col;
+      if (general)
+        for (int i = 0; i < r.ncol; i++) if (r.emit[i] == k) a.ecol[k] = r.col[i];
+    }
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.counts = slab;
@@ -1329,9 +1372,10 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 24 * sizeof(unsigned long long), st));
     }
     unsigned long long* e16d = nullptr;              // chain_estep16_kernel's per-wave stamps [block][16][4]
+    const int nblk8 = (nb + 7) / 8;                  // blocks of 8 or 16 sequences: room for either
     if (ek == 3 && times && c == 0) {
-      HIP_OK(hipMalloc(&e16d, (size_t)nblk * 64 * sizeof(unsigned long long)));
-      HIP_OK(hipMemsetAsync(e16d, 0, (size_t)nblk * 64 * sizeof(unsigned long long), st));
+      HIP_OK(hipMalloc(&e16d, (size_t)nblk8 * 64 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(e16d, 0, (size_t)nblk8 * 64 * sizeof(unsigned long long), st));
       a.diag = e16d;
     }
 #endif
@@ -1341,14 +1385,14 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
 #ifdef NIPAMD_DIAGNOSTICS
     if (e16d) {
-      std::vector<unsigned long long> h((size_t)nblk * 64);
+      std::vector<unsigned long long> h((size_t)nblk8 * 64);
       HIP_OK(hipStreamSynchronize(st));
       HIP_OK(hipMemcpy(h.data(), e16d, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
       (void)hipFree(e16d);
       a.diag = nullptr;
       double m[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
       int nw[2] = {0, 0};
-      for (int k = 0; k < nblk; k++)
+      for (int k = 0; k < nblk8; k++)
         for (int w = 0; w < 16; w++) {
           const unsigned long long* r = h.data() + ((size_t)k * 16 + w) * 4;
           if (r[0] + r[2] == 0) continue;
@@ -1490,6 +1534,134 @@ static int ensure_joint_map(nipamd_model* mm) {
   return 0;
 }
 
+// Every leaf child's evidence table for the general chain e_step: rows
+// M_k + 2 per child (E_k[m][y], the row sums, an all-zero row for an
+// out-of-range state), 16 columns, children in plan order.
+static int ensure_etab_all(nipamd_model* mm) {
+  DevState* d = dev_of(mm);
+  if (d->etab_all) return 0;
+  const auto& P = mm->m.chain;
+  std::vector<double> E;
+  for (const auto& em : P.emits) {
+    const size_t base = E.size();
+    E.resize(base + (size_t)(em.M + 2) * 16, 0.0);
+    for (int y = 0; y < P.N; y++) {
+      for (int m = 0; m < em.M; m++) E[base + (size_t)m * 16 + y] = em.E[(size_t)m * 64 + y];
+      E[base + (size_t)em.M * 16 + y] = em.s[y];
+    }
+  }
+  return upload(&d->etab_all, E);
+}
+
+// The general chain e_step's slab (xi sums Kf / Kb without the transition,
+// the children's count tables, the t = 0 posterior P0) projected onto every
+// family of the em_learn layout (nip.c:2101-2128: child first, then its
+// parents in v->parents order), as one fixed-order sum per count (CSR):
+//   previous interface variable: P0
+//   interface variable y | x, hidden parents h: in-clique(x, y, h)
+//       x prod_j prior_j(h_j) x (Kf + Kb)(x, y)   (the joint posterior of the
+//       in-clique's variables is alpha_{t-1}(x) P(y | x, h) prod prior(h)
+//       e_t(y) beta_t(y) / Z; xi holds everything but the first factors)
+//   hidden parent h_j: the same summed over everything but h_j
+//   leaf child o_k | y: its count table, a missing observation split as
+//       E_k(y, o) / s_k(y) (the child's posterior given y)
+static int ensure_chain_map(nipamd_model* mm) {
+  DevState* d = dev_of(mm);
+  if (d->jm_ptr) return 0;
+  const nipamd::Model& m = mm->m;
+  const auto& P = m.chain;
+  const int nv = (int)m.vars.size(), N = P.N, R = estep_rows(P);
+  const int Kb = nipamd::kSlabKb, Hf = nipamd::kSlabH, Hb = nipamd::kSlabH + R * 16;
+  const int p0 = nipamd::chain_slab_p0(R - 2);
+  std::vector<int> off(nv + 1, 0);
+  for (int v = 0; v < nv; v++) {
+    int sz = m.vars[v].card;
+    for (int q : m.vars[v].parents) sz *= m.vars[q].card;
+    off[v + 1] = off[v] + sz;
+  }
+  std::vector<std::vector<std::pair<int, double>>> rows(off[nv]);
+  // the in-clique's entries: (x, y, hidden values) -> coefficient
+  const auto& cin = m.cliques[P.c_trans];
+  std::vector<long> stride(cin.vars.size());
+  long total = 1;
+  for (size_t i = 0; i < cin.vars.size(); i++) { stride[i] = total; total *= m.vars[cin.vars[i]].card; }
+  for (int v : cin.vars)
+    if (v != P.v_prev && v != P.v_cur && std::find(P.hidden.begin(), P.hidden.end(), v) == P.hidden.end())
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: in-clique variable outside the plan");
+  std::vector<int> val(nv, 0);
+  const auto& Vc = m.vars[P.v_cur];
+  for (long i = 0; i < total; i++) {
+    long r = i;
+    for (size_t k = 0; k < cin.vars.size(); k++) {
+      const int v = cin.vars[k];
+      val[v] = (int)(r % m.vars[v].card);
+      r /= m.vars[v].card;
+    }
+    double coef = cin.original[(size_t)i];
+    for (int h : P.hidden) coef *= m.vars[h].prior[val[h]];
+    const int x = val[P.v_prev], y = val[P.v_cur];
+    // the interface variable's family: y first, then its parents in order
+    long idx = y, st = Vc.card;
+    for (int q : Vc.parents) { idx += (long)val[q] * st; st *= m.vars[q].card; }
+    rows[off[P.v_cur] + idx].push_back({x * 16 + y, coef});
+    rows[off[P.v_cur] + idx].push_back({Kb + x * 16 + y, coef});
+    for (int h : P.hidden) {
+      auto& row = rows[off[h] + val[h]];
+      bool merged = false;                       // one coefficient per (x, y): summed in entry order
+      for (auto& e : row)
+        if (e.first == x * 16 + y) { e.second += coef; merged = true; }
+      if (!merged) row.push_back({x * 16 + y, coef});
+    }
+  }
+  for (int h : P.hidden) {
+    for (int d2 = 0; d2 < m.vars[h].card; d2++) {
+      auto& rw = rows[off[h] + d2];
+      const size_t n = rw.size();
+      for (size_t e = 0; e < n; e++) rw.push_back({Kb + rw[e].first, rw[e].second});
+    }
+  }
+  if (!m.vars[P.v_prev].parents.empty()) return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: prev with parents");
+  for (int x = 0; x < N; x++) rows[off[P.v_prev] + x].push_back({p0 + x, 1.0});
+  for (size_t k = 0, row0 = 0; k < P.emits.size(); k++) {
+    const auto& E = P.emits[k];
+    const auto& Vo = m.vars[E.var];
+    if (Vo.parents.size() != 1 || Vo.parents[0] != P.v_cur)
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: a child with parents besides the interface");
+    for (int y = 0; y < N; y++)
+      for (int o = 0; o < E.M; o++) {
+        auto& rw = rows[off[E.var] + o + E.M * y];
+        rw.push_back({Hf + (int)(row0 + o) * 16 + y, 1.0});
+        rw.push_back({Hb + (int)(row0 + o) * 16 + y, 1.0});
+        if (E.s[y] != 0.0) {
+          const double w = E.E[(size_t)o * 64 + y] / E.s[y];
+          rw.push_back({Hf + (int)(row0 + E.M) * 16 + y, w});
+          rw.push_back({Hb + (int)(row0 + E.M) * 16 + y, w});
+        }
+      }
+    row0 += E.M + 2;
+  }
+  // every variable must be one of the plan's
+  for (int v = 0; v < nv; v++) {
+    const bool known = v == P.v_prev || v == P.v_cur ||
+                       std::find(P.hidden.begin(), P.hidden.end(), v) != P.hidden.end() ||
+                       std::any_of(P.emits.begin(), P.emits.end(), [&](const nipamd::ChainEmit& e) { return e.var == v; });
+    if (!known) return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: variable outside the chain plan");
+  }
+  std::vector<int> ptr{0}, idx;
+  std::vector<double> coef;
+  for (const auto& r : rows) {
+    for (const auto& e : r) { idx.push_back(e.first); coef.push_back(e.second); }
+    ptr.push_back((int)idx.size());
+  }
+  HIP_OK(hipMalloc(&d->jm_ptr, ptr.size() * sizeof(int)));
+  HIP_OK(hipMemcpy(d->jm_ptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OK(hipMalloc(&d->jm_idx, std::max<size_t>(1, idx.size()) * sizeof(int)));
+  if (!idx.empty()) HIP_OK(hipMemcpy(d->jm_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (int rc = upload(&d->jm_coef, coef)) return rc;
+  d->jm_n = off[nv];
+  return 0;
+}
+
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   const int body = estep_body_size(mm);
@@ -1503,7 +1675,7 @@ int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_c
                                             "layout) were combined, or the buffer is not an e_step partial");
   if (tag[1] >= 1.0) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
   const auto& P = mm->m.chain;
-  if (!P.valid || !(P.hmm || P.jhmm))
+  if (!P.valid || !(P.hmm || P.jhmm || estep_general_plan(P)))
     return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
   if (int rc = ensure_tables(mm)) return rc;
   Route rh;
@@ -1511,8 +1683,8 @@ int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_c
   ReqTables* rt = nullptr;
   if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
   DevState* d = dev_of(mm);
-  if (P.jhmm) {
-    if (int rc = ensure_joint_map(mm)) return rc;
+  if (P.jhmm || !P.hmm) {
+    if (int rc = P.jhmm ? ensure_joint_map(mm) : ensure_chain_map(mm)) return rc;
     if (nipamd::estep_map_finalize_launch(d_partial, d->jm_n, d->jm_ptr, d->jm_idx, d->jm_coef, d_counts,
                                           (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, "finalize launch failed");

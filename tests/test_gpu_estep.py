@@ -297,3 +297,66 @@ def test_estep_mfma_kernel_in_diagnostics_build():
                        env=dict(os.environ, NIPAMD_LIB=nb.DIAG_LIB), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "all passed" in r.stdout
+
+
+GENERAL_CASES = [
+    # name, spec, observed children: chain plans beyond the HMM (hidden
+    # parents folded into the transition, several leaf children)
+    ("demo1_4_AB", lambda: synth.demo1_spec(4), ["A1", "B1"]),
+    ("demo1_6_B", lambda: synth.demo1_spec(6, seed=3), ["B1"]),
+    ("demo1_16_AB", lambda: synth.demo1_spec(16, seed=5), ["A1", "B1"]),
+    ("demo1_5_none", lambda: synth.demo1_spec(5, seed=7), []),
+    ("wide_8", lambda: synth.wide_spec(8, 5), ["O1"]),
+]
+
+
+@pytest.mark.parametrize("name,spec,osyms", GENERAL_CASES, ids=[c[0] for c in GENERAL_CASES])
+@pytest.mark.parametrize("B,T", [(37, 41), (16, 1), (3, 2)])
+def test_general_chain_estep_vs_oracle_and_general_engine(name, spec, osyms, B, T):
+    """The chain e_step for plans with hidden parents and several children
+    (chain_estep16_kernel with one evidence table per child, ensure_chain_map):
+    counts rel 1e-11 and ll rel 1e-12 against the oracle and the general
+    join-tree engine, BAD_LUCK flags equal, missing and leading-missing data."""
+    m = nip_amd.Model.from_spec(*spec())
+    ov = [m.variable(s) for s in osyms]
+    rng = np.random.default_rng(B * 31 + T + len(name))
+    if ov:
+        obs = np.stack([rng.integers(0, m.card(v), size=(B, T)) for v in ov], axis=2).astype(np.int32)
+        obs[rng.random(obs.shape) < 0.2] = -1
+        obs[0, :2] = -1
+    else:
+        obs = np.zeros((B, T, 0), np.int32)
+    cnt, ll, st = gpu_estep(m, obs, ov)
+    assert nip_amd.last_kernel() == "chain_estep16_kernel", nip_amd.last_kernel()
+    orc = PortOracle(m.desc())
+    rc, rl, rb = orc.estep(obs, ov, np.ones(m.param_size()))
+    assert np.array_equal(st != 0, rb != 0)
+    ok = rb == 0
+    assert close(ll[ok], rl[ok], LL_RTOL)
+    if not ok.all():
+        cnt, _, _ = gpu_estep(m, obs[ok], ov)
+        rc, _, _ = orc.estep(obs[ok], ov, np.ones(m.param_size()))
+    assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
+    m.set_engine(nip_amd.ENGINE_JTREE)
+    cj, lj, sj = gpu_estep(m, obs[ok], ov)
+    m.set_engine(nip_amd.ENGINE_AUTO)
+    assert close(cnt, cj, CNT_RTOL), np.abs(cnt - cj).max()
+
+
+def test_general_chain_em_learn_matches_general_engine():
+    """em_learn on demo1's structure through the chain e_step against the same
+    run on the general engine (curves rel 1e-10)."""
+    nodes, pots = synth.demo1_spec(6, seed=11)
+    obs_np = np.concatenate([synth.observations(64, 50, 6, seed=s) for s in (1, 2)], axis=2)
+    curves = []
+    for engine in (nip_amd.ENGINE_AUTO, nip_amd.ENGINE_JTREE):
+        m = nip_amd.Model.from_spec(nodes, pots)
+        m.set_engine(engine)
+        ov = [m.variable("A1"), m.variable("B1")]
+        curve = []
+        rc = em_learn(m, torch.from_numpy(obs_np).cuda(), ov, 1e-6, curve,
+                      init=synth.uniform01(5, m.param_size()) + 0.05, max_iterations=6)
+        curves.append((rc, curve))
+    assert curves[0][0] == curves[1][0]
+    assert len(curves[0][1]) == len(curves[1][1])
+    assert close(np.array(curves[0][1]), np.array(curves[1][1]), 1e-10)
