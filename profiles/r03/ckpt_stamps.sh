@@ -1,5 +1,6 @@
 #!/bin/bash
-# per-wave cycle stamps of the checkpoint kernel (stamps build).  $1 = tag
+# per-wave cycle stamps of the checkpoint kernels (stamps build: python -c "from nip_amd import build as b;
+# b.build(defines=['NIPAMD_DIAGNOSTICS', 'NIPAMD_WAIT_TIMES=1'], out='nip_amd/_lib/diag/libnip_amd_stamps.so')").  $1 = tag
 set -o pipefail
 tag=${1:-r03c}
 mkdir -p gpurun_out

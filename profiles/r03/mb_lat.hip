@@ -8,6 +8,10 @@
 // V2  config 2's step: 4 MFMAs chained through C, D feeds the next step's B
 // V3  config 3's step (NT = 2): two output tiles, each 8 MFMAs chained
 //     through C, interleaved; D feeds the next step's B operands
+// V4  V2 + the evidence multiply (p = d o e, e from registers)
+// V5  V4 + ldexp by a power of two on every step
+// V6  V4 + the step's two ds_write_b128 of the row + a 16-state sum every
+//     4th step feeding the next step's ldexp (config 2's filter step)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -24,6 +28,9 @@ __global__ __launch_bounds__(64, 1) void k(const double* in, double* out, unsign
   for (int i = 0; i < 8; i++) A[i] = in[l + 64 * i] * 0.01;
   v4d X = {in[l + 512], in[l + 576], in[l + 640], in[l + 704]};
   v4d Y = {in[l + 768], in[l + 832], in[l + 896], in[l + 960]};
+  const v4d E = {in[l + 1024], in[l + 1088], in[l + 1152], in[l + 1216]};
+  __shared__ double lds[8 * 256];
+  int sc = V == 5 ? 0 : 0;
   v4d acc[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) acc[i] = v4d{0, 0, 0, 0};
@@ -43,6 +50,31 @@ __global__ __launch_bounds__(64, 1) void k(const double* in, double* out, unsign
       d = MFMA(A[2], X.z, d);
       d = MFMA(A[3], X.w, d);
       X = d;
+    } else if (V >= 4) {
+      v4d d = {0, 0, 0, 0};
+      d = MFMA(A[0], X.x, d);
+      d = MFMA(A[1], X.y, d);
+      d = MFMA(A[2], X.z, d);
+      d = MFMA(A[3], X.w, d);
+      if (V == 5 || V == 6) {
+        d.x = __builtin_ldexp(d.x, sc); d.y = __builtin_ldexp(d.y, sc);
+        d.z = __builtin_ldexp(d.z, sc); d.w = __builtin_ldexp(d.w, sc);
+      }
+      const v4d e = (i & 1) ? Y : E;
+      X = d * e;
+      if (V == 6) {
+        double* L = lds + (i & 7) * 256 + l * 2;
+        *reinterpret_cast<double2*>(L) = make_double2(X.x, X.y);
+        *reinterpret_cast<double2*>(L + 128) = make_double2(X.z, X.w);
+        if ((i & 3) == 3) {
+          double z = (X.x + X.y) + (X.z + X.w);
+          z += __shfl_xor(z, 32);
+          z += __shfl_xor(z, 16);
+          sc = -__builtin_amdgcn_frexp_exp(z);
+        } else {
+          sc = 0;
+        }
+      }
     } else {
       v4d d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0};
       d0 = MFMA(A[0], X.x, d0); d1 = MFMA(A[4], X.x, d1);
@@ -68,7 +100,7 @@ __global__ __launch_bounds__(64, 1) void k(const double* in, double* out, unsign
 
 template <int V>
 double run(const char* name, double* din, double* dout, unsigned long long* dc, int blocks, double per) {
-  const int n = V == 2 ? 65536 : 4096;
+  const int n = V >= 2 && V != 3 ? 65536 : 4096;
   for (int rep = 0; rep < (V == 2 ? 40 : 2); rep++)      // V2: >= 2 s of back-to-back launches, then stamp
     hipLaunchKernelGGL(k<V>, dim3(blocks), dim3(64), 0, 0, din, dout, dc, n);
   (void)hipDeviceSynchronize();
@@ -91,10 +123,14 @@ int main() {
   (void)hipMalloc(&dc, 2048 * 8);
   std::vector<double> h(4096);
   for (int i = 0; i < 4096; i++) h[i] = 0.5 + (i % 7) * 0.01;
+  for (int i = 1024; i < 1280; i++) h[i] = 1.0;
   (void)hipMemcpy(din, h.data(), 4096 * 8, hipMemcpyHostToDevice);
   run<0>("V0 MFMA f64 16x16x4 chained C->C (4 per iter)", din, dout, dc, 256, 4);
   run<1>("V1 MFMA f64 16x16x4 independent (8 per iter)", din, dout, dc, 256, 8);
   run<2>("V2 config-2 step: 4 chained, D -> next B", din, dout, dc, 256, 4);
   run<3>("V3 config-3 step: 2 x 8 chained, interleaved, D -> next B", din, dout, dc, 256, 16);
+  run<4>("V4 V2 + evidence multiply", din, dout, dc, 256, 4);
+  run<5>("V5 V4 + ldexp every step", din, dout, dc, 256, 4);
+  run<6>("V6 V4 + row writes + sum/ldexp every 4th step", din, dout, dc, 256, 4);
   return 0;
 }
