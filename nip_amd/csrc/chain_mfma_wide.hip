@@ -15,13 +15,21 @@
 // register algebra).  Internal row g + 4r of tile q is state
 // 16q + state_of(g, r), so lane (g = l >> 4, j = l & 15) owns states
 // 16q + {2g, 2g+1, 8+2g, 9+2g} of chain j in every tile q.
-// Block = 16 sequences, four waves, one per SIMD (f64 MFMA and VALU do not
-// co-execute, so the filters keep only the recursion):
-//   wave 0 forward filter, wave 1 backward filter  (MFMA + evidence)
-//   wave 2 forward partner: scratch copy, ll, posteriors of t >= H
-//   wave 3 backward partner: scratch copy, posteriors of t < H
-// LDS rings hold two chunks of CH steps per direction (CH = 8 / NT, a slot is
-// 16 KB); one s_barrier per chunk hands a slot from filter to partner.
+// Block = two groups of 16 sequences, eight waves, two per SIMD: each SIMD
+// runs one group's filter (matrix core) and one group's partner (VALU), so
+// all four matrix pipes carry a filter:
+//   waves 0, 1: group 0 forward / backward filter   (MFMA + evidence)
+//   waves 2, 3: group 1 forward / backward filter
+//   waves 4, 5: group 0 forward / backward partner (scratch copy, ll,
+//               posteriors of t >= H / t < H)
+//   waves 6, 7: group 1 forward / backward partner
+// (a workgroup's waves go to the CU's SIMDs round robin, wave w and w + 4 on
+// one SIMD).  With one group per block (round 2) the filters had two SIMDs
+// to themselves, the 93 KB of LDS allowed one block per CU, and the other two
+// matrix pipes idled.  LDS rings hold two chunks of CH steps per direction
+// and group (CH = 8 / NT, a slot is 16 KB); one s_barrier per chunk hands a
+// slot from filter to partner.  The observation codes are read from HBM by
+// the filters, two chunks ahead, instead of being staged in LDS.
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cstdint>
@@ -38,8 +46,9 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #ifndef NIPAMD_MW_ABLATE
 #define NIPAMD_MW_ABLATE 0     // timing-only builds: 1 partners only keep the barriers,
 #endif                         // 2 filters skip the mat-vec
-constexpr int kWSeq = 16;
-constexpr int kWThreads = 256;
+constexpr int kWSeq = 16;                  // sequences per group
+constexpr int kWGroups = 2;                // groups per block
+constexpr int kWThreads = 512;
 constexpr int kWG = kScratchGuard;
 
 __host__ __device__ constexpr int state_of(int g, int r) { return r < 2 ? 2 * g + r : 6 + 2 * g + r; }
@@ -121,9 +130,10 @@ struct MwDiag {
   __device__ __forceinline__ void phase() {
     if (NIPAMD_WAIT_TIMES) { ta = __builtin_readcyclecounter(); inB = true; }
   }
-  __device__ __forceinline__ void write(unsigned long long* d, int wave, int lane) {
+  // unit: the block's group (blocks of 16 sequences, as the host counts them)
+  __device__ __forceinline__ void write(unsigned long long* d, long unit, int wave, int lane) {
     if (!NIPAMD_WAIT_TIMES || !d || lane != 0) return;
-    unsigned long long* p = d + (size_t)blockIdx.x * 16 + wave * 4;
+    unsigned long long* p = d + (size_t)unit * 16 + wave * 4;
     p[0] = ta - t0; p[1] = wa; p[2] = __builtin_readcyclecounter() - ta; p[3] = wb;
   }
 };
@@ -159,9 +169,12 @@ __host__ __device__ inline long wblock_scratch(int NT, int T) { return (long)(T 
 
 struct WCtx {
   const double* tab;       // LDS tables
-  const uint8_t* codes;    // LDS codes [ncol][16][Tr] + chain j + kWG (t = 0)
+  const int* obs;          // this chain's observations (null: an absent sequence or no observed column)
+  int ots;                 // their time stride
+  int col[4], M[4];        // per observed column: offset within a time step, states
+  int T;
   int tab_off[4];          // per column: LDS offset of its table + 2g
-  int ncol, Tr;
+  int ncol;
   double* out;             // this direction's ring [2][kSlot]
   double* zr;              // forward: z2 ring [2][CH][16]
   int wo[2][2];            // [tile][half] piece offsets of this lane
@@ -178,24 +191,23 @@ struct WChain {
   v4d X[NT];
   int sc = 0;
 
+  // column k's observation at t, raw (-1: missing, also outside 0..T-1)
+  __device__ __forceinline__ int raw(const WCtx& c, int k, int t) const {
+    return (c.obs && t >= 0 && t < c.T) ? c.obs[(long)t * c.ots + c.col[k]] : -1;
+  }
+  // its table row: the state, M (missing) or M + 1 (out of range: all zero)
+  __device__ __forceinline__ int code(const WCtx& c, int k, int o) const {
+    return o < 0 ? c.M[k] : (o < c.M[k] ? o : c.M[k] + 1);
+  }
   __device__ __forceinline__ void evidence(const WCtx& c, int t, v4d (&e)[NT]) const {
-    int code = c.codes[t];
+    int cd[NC];
 #pragma unroll
-    for (int q = 0; q < NT; q++) e[q] = load4(c.tab + c.tab_off[0] + code * G::NPS + 16 * q);
-#pragma unroll
-    for (int k = 1; k < NC; k++) {
-      code = c.codes[k * kWSeq * c.Tr + t];
-#pragma unroll
-      for (int q = 0; q < NT; q++) e[q] *= load4(c.tab + c.tab_off[k] + code * G::NPS + 16 * q);
-    }
+    for (int k = 0; k < NC; k++) cd[k] = code(c, k, raw(c, k, t));
+    v4d r[NC][NT];
+    rows_of(c, cd, r);
+    product(c, r, e);
   }
 
-  // the step's observation codes, one per observed column (read a step
-  // ahead: the table rows they select are loaded while the step's MFMAs run)
-  __device__ __forceinline__ void codes_of(const WCtx& c, int t, int (&cd)[NC]) const {
-#pragma unroll
-    for (int k = 0; k < NC; k++) cd[k] = c.codes[k * kWSeq * c.Tr + t];
-  }
   __device__ __forceinline__ void rows_of(const WCtx& c, const int (&cd)[NC], v4d (&r)[NC][NT]) const {
 #pragma unroll
     for (int k = 0; k < NC; k++) {
@@ -269,40 +281,49 @@ struct WChain {
     sc = -__builtin_amdgcn_frexp_exp(z2);
   }
 
+  // n steps from t0 in nch chunks; the codes of chunk ci + 2 are loaded from
+  // HBM when chunk ci ends (two chunks of latency cover), a step's table rows
+  // from LDS at its start (under its MFMAs)
   __device__ __forceinline__ void run(const WCtx& c, int n, int nch, int t0, int lane, MwDiag& dg) {
     constexpr int dir = FWD ? 1 : -1;
     constexpr int CH = G::CH;
-    int cd[NC];
-    codes_of(c, t0, cd);
-    for (int ci = 0; ci < nch; ci++) {
+    int ca[CH][NC], cb[CH][NC];
+    auto ldc = [&](int ci, int (&cc)[CH][NC]) {
+#pragma unroll
+      for (int k = 0; k < CH; k++)
+#pragma unroll
+        for (int q = 0; q < NC; q++) cc[k][q] = raw(c, q, t0 + dir * (ci * CH + k));
+    };
+    auto chunk = [&](int ci, int (&cc)[CH][NC]) {
       double* slot = c.out + (ci & 1) * G::kSlot;
       double* zs = FWD ? c.zr + (ci & 1) * CH * kWSeq + (lane & 15) : nullptr;
       const int base = ci * CH;
-      if (base + CH <= n) {
-        // per step: the rows its codes (read a step ahead) select, the next
-        // step's codes, then the MFMAs; guards cover the over-run
+      const bool full = base + CH <= n;
 #pragma unroll
-        for (int k = 0; k < CH; k++) {
-          v4d r[NC][NT];
-          rows_of(c, cd, r);
-          codes_of(c, t0 + dir * (base + k + 1), cd);
-          step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
-        }
-      } else {
-        v4d e[CH][NT];
+      for (int k = 0; k < CH; k++) {
+        if (!full && base + k >= n) break;
+        int cd[NC];
 #pragma unroll
-        for (int k = 0; k < CH; k++) evidence(c, t0 + dir * (base + k), e[k]);   // guards cover over-run
-#pragma unroll
-        for (int k = 0; k < CH; k++)
-          if (base + k < n) step(c, slot + k * G::kStep, zs + k * kWSeq, e[k]);
+        for (int q = 0; q < NC; q++) cd[q] = code(c, q, cc[k][q]);
+        v4d r[NC][NT];
+        rows_of(c, cd, r);
+        step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
       }
       barrier_lds(&dg);
+      ldc(ci + 2, cc);
+    };
+    ldc(0, ca);
+    ldc(1, cb);
+    for (int ci = 0; ci < nch; ci += 2) {
+      chunk(ci, ca);
+      if (ci + 1 >= nch) break;
+      chunk(ci + 1, cb);
     }
   }
 };
 
 template <bool FWD, int NT, int NC>
-__device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, double* Sblk, int lane,
+__device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, double* Sblk, int lane, long b0,
                                         int nchA, int nchB) {
   using G = Geo<NT>;
   const int j = lane & 15, g = lane >> 4;
@@ -345,7 +366,7 @@ __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, do
   dg.phase();
   if (FWD) ch.run(c, T - H, nchB, H, lane, dg);
   else ch.run(c, H, nchB, H - 1, lane, dg);
-  dg.write(a.diag, FWD ? 0 : 1, lane);
+  dg.write(a.diag, b0 / kWSeq, FWD ? 0 : 1, lane);
 }
 
 // ll of the forward filter (nip.c:1461-1474), kept by the forward partner:
@@ -535,7 +556,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     if (FWD) ll.write(a, b0, lane);
     return;
   }
-  v2d oa[kWSeq], ob[kWSeq];
+  v2d oa[kWSeq];
   auto load_other = [&](v2d (&o)[kWSeq], int ci) {
     if (NIPAMD_MW_ABLATE == 1) return;
     const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
@@ -551,20 +572,19 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
     emit(slot, kB, tlow(ci) + hi, kB < nk, o);
   };
+  // one buffer (two groups' partners share the register file with the
+  // filters): the next chunk's vectors are requested as soon as this chunk's
+  // posteriors have used them, a chunk of latency ahead
   const int last = nchB > 0 ? nchB - 1 : 0;
   load_other(oa, 0);
-  for (int ci = 0; ci < nchB; ci += 2) {
-    load_other(ob, ci + 1 < last ? ci + 1 : last);
+  for (int ci = 0; ci < nchB; ci++) {
     barrier_lds(&dg);
     drainB(ci, oa);
-    if (ci + 1 >= nchB) break;
-    load_other(oa, ci + 2 < last ? ci + 2 : last);
-    barrier_lds(&dg);
-    drainB(ci + 1, ob);
+    load_other(oa, ci + 1 < last ? ci + 1 : last);
   }
   // the forward side has nchB chunks when T - H > H (odd T): the last one is
   // the forward partner's or the backward partner's by its parity like the rest
-  dg.write(a.diag, FWD ? 2 : 3, lane);
+  dg.write(a.diag, b0 / kWSeq, FWD ? 2 : 3, lane);
   // the forward ring slot the last chunk did not use (its readers passed the last loop barrier)
   double* share = const_cast<double*>(fring) + ((((nchB > 0 ? nchB : 1) - 1) & 1) ^ 1) * G::kSlot;
   if (!FWD) ll.put(share, lane);
@@ -575,80 +595,37 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   }
 }
 
-// FILT: forward_inference (filtering only): waves 0 (filter) and 1 (partner), H = T
+// FILT: forward_inference (filtering only): per group one filter wave and one
+// partner wave (waves 0, 1 the groups' filters, 2, 3 their partners), H = T
 template <int NT, bool FILT, int NC>
 __global__ __launch_bounds__(FILT ? kWThreads / 2 : kWThreads, 1)
 void chain_mfma_wide_kernel(WideMfmaArgs a) {
   constexpr int kThreads = FILT ? kWThreads / 2 : kWThreads;
+  constexpr int F = FILT ? 1 : 2;                           // filter waves per group
   using G = Geo<NT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* out = reinterpret_cast<double*>(smem);            // [2 dirs][2 slots][kSlot]
-  double* zr = out + 4 * G::kSlot;                          // [2 slots][CH][16]
-  double* tab = zr + 2 * G::CH * kWSeq;                     // [sum (M_k + 2)][NP]
-  const int ncol = a.ncol > 0 ? a.ncol : 1;
-  uint8_t* codes = reinterpret_cast<uint8_t*>(tab + a.tab_rows * G::NPS);   // [ncol][16][Tr]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool filter = wave < kWGroups * F;
+  const int role = filter ? wave : wave - kWGroups * F;
+  const int grp = role / F;
+  const bool fwd = FILT || (role % F) == 0;
+  double* out = reinterpret_cast<double*>(smem) + grp * 4 * G::kSlot;   // this group's [2 dirs][2 slots][kSlot]
+  double* zr = reinterpret_cast<double*>(smem) + kWGroups * 4 * G::kSlot + grp * 2 * G::CH * kWSeq;
+  double* tab = reinterpret_cast<double*>(smem) + kWGroups * (4 * G::kSlot + 2 * G::CH * kWSeq);
+  const int ncol = a.ncol > 0 ? a.ncol : 1;
   const int j = lane & 15, g = lane >> 4;
-  const long b0 = (long)blockIdx.x * kWSeq;
-  const int T = a.T, Tr = chain_codes_row(T);
+  const long b0 = (long)blockIdx.x * (kWGroups * kWSeq) + grp * kWSeq;
+  const int T = a.T;
 
   for (int i = tid; i < a.tab_rows * G::NP; i += kThreads) tab[(i / G::NP) * G::NPS + i % G::NP] = a.tab[i];
-  const int nseq = (int)((a.B - b0) < kWSeq ? (a.B - b0) : kWSeq);
-  // the block's 16 sequences are one contiguous [16][T][n_obs] int32 run
-  // (the usual layout): 16-byte loads, all of a thread's issued before any is
-  // unpacked; otherwise (strided views, a partial block) one element at a time
-  const int W = a.obs_tstride;
-  const bool fast = a.ncol > 0 && a.obs_bstride == (long)T * W && nseq == kWSeq;
-  for (int k = 0; k < ncol; k++) {
-    const int M = a.ncol > 0 ? a.M[k] : 0;
-    uint8_t* ck = codes + (size_t)k * kWSeq * Tr;
-    for (int i = tid; i < kWSeq * Tr; i += kThreads) {
-      const int cq = i / Tr, t = i - cq * Tr - kWG;
-      int c = M;                                            // missing / guard / absent sequence
-      if (!fast && a.ncol > 0 && cq < nseq && t >= 0 && t < T) {
-        const int o = a.obs[(b0 + cq) * a.obs_bstride + (long)t * a.obs_tstride + a.col[k]];
-        c = o < 0 ? M : (o < M ? o : M + 1);
-      }
-      ck[i] = (uint8_t)c;
-    }
-  }
-  if (fast) {
-    __syncthreads();                                        // guards before the interior
-    const int4* src = reinterpret_cast<const int4*>(a.obs + b0 * a.obs_bstride);
-    const int n4 = (kWSeq * T * W) >> 2;                    // 16 T W is a multiple of 4
-    constexpr int kU = 8;                                   // loads in flight per thread
-    for (int i0 = tid; i0 < n4; i0 += kThreads * kU) {
-      int4 r[kU];
-#pragma unroll
-      for (int u = 0; u < kU; u++)
-        if (i0 + u * kThreads < n4) r[u] = src[i0 + u * kThreads];
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const int i4 = i0 + u * kThreads;
-        if (i4 >= n4) break;
-        const int v[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const int i = 4 * i4 + e, cq = i / (T * W), rem = i - cq * T * W, t = rem / W, col = rem - t * W;
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            if (k >= a.ncol || a.col[k] != col) continue;
-            const int M = a.M[k], o = v[e];
-            codes[(size_t)k * kWSeq * Tr + cq * Tr + kWG + t] = (uint8_t)(o < 0 ? M : (o < M ? o : M + 1));
-          }
-        }
-      }
-    }
-  }
   __syncthreads();
 
   const int H = a.H;
   const int nA = (H > T - 1 - H ? H : T - 1 - H), nB = (T - H > H ? T - H : H);
   const int nchA = (nA + G::CH - 1) / G::CH, nchB = FILT ? 0 : (nB + G::CH - 1) / G::CH;
-  const bool fwd = FILT || (wave & 1) == 0;
   double* ring = out + (fwd ? 0 : 2 * G::kSlot);
-  double* Sblk = FILT ? nullptr : a.S + (size_t)blockIdx.x * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;
-  if (FILT ? wave == 1 : wave >= 2) {
+  double* Sblk = FILT ? nullptr : a.S + (size_t)(b0 / kWSeq) * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;
+  if (!filter) {
     const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
                       (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
     if (pvec) {
@@ -662,11 +639,16 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   }
   WCtx c;
   c.tab = tab;
-  c.codes = codes + j * Tr + kWG;
+  c.obs = (a.ncol > 0 && b0 + j < a.B) ? a.obs + (b0 + j) * a.obs_bstride : nullptr;
+  c.ots = a.obs_tstride;
+  c.T = T;
   c.ncol = ncol;
-  c.Tr = Tr;
 #pragma unroll
-  for (int k = 0; k < 4; k++) c.tab_off[k] = (k < ncol ? a.tab_off[k] / G::NP * G::NPS : 0) + 2 * g;
+  for (int k = 0; k < 4; k++) {
+    c.col[k] = a.col[k];
+    c.M[k] = a.ncol > 0 ? a.M[k] : 0;              // no observed column: row 0 (the row sums) every step
+    c.tab_off[k] = (k < ncol ? a.tab_off[k] / G::NP * G::NPS : 0) + 2 * g;
+  }
   c.out = ring;
   c.zr = zr;
   c.zw = g == 0;
@@ -675,18 +657,18 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
     c.wo[q][0] = Geo<NT>::piece_off(j, 8 * q + g);
     c.wo[q][1] = Geo<NT>::piece_off(j, 8 * q + 4 + g);
   }
-  if (fwd) wfilter<true, NT, NC>(a, c, Sblk, lane, nchA, nchB);
-  else if (!FILT) wfilter<false, NT, NC>(a, c, Sblk, lane, nchA, nchB);
+  if (fwd) wfilter<true, NT, NC>(a, c, Sblk, lane, b0, nchA, nchB);
+  else if (!FILT) wfilter<false, NT, NC>(a, c, Sblk, lane, b0, nchA, nchB);
   if (!FILT) barrier_lds();                       // the block's closing barrier (wpartner)
 }
 
 }  // namespace
 
 size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T) {
+  (void)ncol; (void)T;                                       // codes are read from HBM
   const size_t slot = 2048;                                  // doubles per ring slot
   const size_t ch = 8 / NT;
-  return (4 * slot + 2 * ch * kWSeq + (size_t)tab_rows * (16 * NT + 2)) * sizeof(double) +
-         (size_t)(ncol > 0 ? ncol : 1) * kWSeq * chain_codes_row(T);
+  return (kWGroups * (4 * slot + 2 * ch * kWSeq) + (size_t)tab_rows * (16 * NT + 2)) * sizeof(double);
 }
 
 size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
@@ -698,7 +680,7 @@ template <int NT, bool FILT, int NC>
 int launch_wide_nc(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
   static size_t set[kMaxDevices] = {};
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT, NC>), lds, set)) return -1;
-  const int blocks = (int)((a.B + kWSeq - 1) / kWSeq);
+  const int blocks = (int)((a.B + kWGroups * kWSeq - 1) / (kWGroups * kWSeq));
   hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT, NC>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
                      lds, stream, a);
   g_last_kernel = NT == 1 ? "chain_mfma_wide_kernel<1>" : "chain_mfma_wide_kernel<2>";
