@@ -247,6 +247,18 @@ int nipamd_estep_finalize(nipamd_model* m, const double* d_partial,
                           double* d_counts, void* stream);
 
 /*
+ * d_out[S] = the fixed-order binary-tree sum of the n rows d_rows[n][S]
+ * (pairs (2i, 2i + 1) level by level, an odd tail paired with 0): the tree
+ * nipamd_estep_partial reduces its count slabs with, so a data-parallel
+ * em_learn sums its per-sequence log-likelihoods in the same shape as its
+ * counts (nip_amd/em.py exchange).  d_work: at least 2 * ceil(n / 64) * S
+ * doubles of device workspace when n > 64 (else may be null).  Queued on
+ * stream, no synchronisation.
+ */
+int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double* d_out,
+                    void* stream);
+
+/*
  * The e_step's verdict on a leading run of missing observations: the first
  * step k < T at which the reference's e_step rejects (BAD_LUCK, nip.c:1836-
  * 1840) a series that observed nothing at steps 0..k -- its running ll of pure

@@ -50,7 +50,7 @@ EXPORTS = [
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error", "nipamd_last_kernel",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
-    "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
+    "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_tree_sum", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
     "nipamd_series_data", "nipamd_series_free", "nipamd_write_uncertainseries",
@@ -104,6 +104,7 @@ def lib():
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
         L.nipamd_estep_prefix_first_bad.argtypes = [vp, C.c_int]
+        L.nipamd_tree_sum.argtypes = [vp, C.c_long, C.c_int, vp, vp, vp]
         L.nipamd_estep_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp]
         L.nipamd_m_step.argtypes = [vp, dp]
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
@@ -543,6 +544,22 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
                                       B, T, C.c_void_p(partial.data_ptr()), C.c_void_p(ll.data_ptr()),
                                       C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
     return partial, ll, status
+
+
+def tree_sum(rows, out=None, stream=None):
+    """Fixed-order binary-tree sum of rows [n, S] (CUDA float64) over dim 0
+    (nipamd_tree_sum): pairs (2i, 2i + 1) level by level, the shape of the
+    e_step's count tree.  Returns out [S]."""
+    import torch
+    x = rows.reshape(rows.shape[0], -1) if rows.dim() > 1 else rows.reshape(-1, 1)
+    x = x.to(torch.float64).contiguous()
+    n, S = int(x.shape[0]), int(x.shape[1])
+    out = _out_buf(out, (S,), torch.float64, x.device, "out")
+    work = torch.empty((2 * ((n + 63) // 64) * S,), dtype=torch.float64, device=x.device) if n > 64 else None
+    _check(lib().nipamd_tree_sum(C.c_void_p(x.data_ptr()), n, S,
+                                 C.c_void_p(work.data_ptr() if work is not None else 0),
+                                 C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return out
 
 
 def estep_finalize(model: Model, partial, counts, stream=None):

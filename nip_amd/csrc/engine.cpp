@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <unordered_map>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -84,7 +85,37 @@ struct DevState {
   // general chain e_step (several leaf children, hidden parents): every
   // child's table, rows M_k + 2 each (E, the row sums, zeros), 16 columns
   double* etab_all = nullptr;
+  // model-table buffers of earlier versions, kept for the next version's
+  // tables of the same sizes (an em_learn iteration re-uploads every table
+  // after its m_step: no hipMalloc / hipFree pair per table and iteration)
+  std::unordered_map<void*, size_t> live;        // pool-managed buffers in use -> bytes
+  std::vector<std::pair<void*, size_t>> pool;     // free ones
 };
+
+void* dalloc(DevState* d, size_t bytes) {
+  for (size_t i = 0; i < d->pool.size(); i++)
+    if (d->pool[i].second == bytes) {
+      void* p = d->pool[i].first;
+      d->pool[i] = d->pool.back();
+      d->pool.pop_back();
+      d->live[p] = bytes;
+      return p;
+    }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  d->live[p] = bytes;
+  return p;
+}
+
+// back to the pool (the caller has synchronised the device), or hipFree for
+// buffers the pool did not hand out
+void dfree(DevState* d, void* p) {
+  if (!p) return;
+  auto it = d->live.find(p);
+  if (it == d->live.end()) { (void)hipFree(p); return; }
+  d->pool.push_back(*it);
+  d->live.erase(it);
+}
 
 DevState* dev_of(nipamd_model* mm) {
   if (!mm->m.dev) mm->m.dev = new DevState();
@@ -92,34 +123,40 @@ DevState* dev_of(nipamd_model* mm) {
 }
 
 void free_tables(DevState* d) {
-  (void)hipFree(d->A); (void)hipFree(d->pi); (void)hipFree(d->A64); (void)hipFree(d->pi64);
-  (void)hipFree(d->sall64);
+  // queued kernels may still read the tables: they return to the pool only
+  // once the device is idle (hipFree synchronised the same way)
+  if (!d->live.empty()) (void)hipDeviceSynchronize();
+  dfree(d, d->A); dfree(d, d->pi); dfree(d, d->A64); dfree(d, d->pi64);
+  dfree(d, d->sall64);
   d->A = d->pi = d->A64 = d->pi64 = d->sall64 = nullptr;
   for (auto& r : d->reqs) {
-    (void)hipFree(r.Etab16); (void)hipFree(r.ts16); (void)hipFree(r.tabw); (void)hipFree(r.ebase);
-    (void)hipFree(r.mtab); (void)hipFree(r.wv);
+    dfree(d, r.Etab16); dfree(d, r.ts16); dfree(d, r.tabw); dfree(d, r.ebase);
+    dfree(d, r.mtab); dfree(d, r.wv);
   }
   d->reqs.clear();
-  for (double* p : d->childE) (void)hipFree(p);
-  for (double* p : d->G) (void)hipFree(p);
+  for (double* p : d->childE) dfree(d, p);
+  for (double* p : d->G) dfree(d, p);
   d->childE.clear();
   d->G.clear();
-  (void)hipFree(d->jm_ptr); (void)hipFree(d->jm_idx); (void)hipFree(d->jm_coef);
+  dfree(d, d->jm_ptr); dfree(d, d->jm_idx); dfree(d, d->jm_coef);
   d->jm_ptr = nullptr; d->jm_idx = nullptr; d->jm_coef = nullptr; d->jm_n = 0;
-  (void)hipFree(d->etab_all);
+  dfree(d, d->etab_all);
   d->etab_all = nullptr;
 }
 
 void dev_release(DevState* d) {
   if (!d) return;
   free_tables(d);
+  for (auto& e : d->pool) (void)hipFree(e.first);
+  d->pool.clear();
   (void)hipFree(d->S); (void)hipFree(d->W); (void)hipFree(d->R); (void)hipFree(d->Q);
   *d = DevState();
 }
 
 template <typename V>
-int upload(double** dst, const V& v) {
-  HIP_OK(hipMalloc(dst, (v.size() ? v.size() : 1) * sizeof(double)));
+int upload(DevState* d, double** dst, const V& v) {
+  *dst = static_cast<double*>(dalloc(d, (v.size() ? v.size() : 1) * sizeof(double)));
+  if (!*dst) return fail(NIPAMD_ERROR_DEVICE, "device allocation failed");
   if (v.size()) HIP_OK(hipMemcpy(*dst, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice));
   return 0;
 }
@@ -166,17 +203,17 @@ int ensure_tables(nipamd_model* mm) {
   const auto& P = mm->m.chain;
   free_tables(d);
   if (P.N <= 16) {
-    if (int rc = upload(&d->A, P.A)) return rc;
-    if (int rc = upload(&d->pi, P.pi)) return rc;
+    if (int rc = upload(d, &d->A, P.A)) return rc;
+    if (int rc = upload(d, &d->pi, P.pi)) return rc;
   }
-  if (int rc = upload(&d->A64, P.A64)) return rc;
-  if (int rc = upload(&d->pi64, P.pi64)) return rc;
-  if (int rc = upload(&d->sall64, P.s_all64)) return rc;
+  if (int rc = upload(d, &d->A64, P.A64)) return rc;
+  if (int rc = upload(d, &d->pi64, P.pi64)) return rc;
+  if (int rc = upload(d, &d->sall64, P.s_all64)) return rc;
   for (const auto& E : P.emits) {
     std::vector<double> t(E.E);
     t.insert(t.end(), E.s.begin(), E.s.end());
     double* p = nullptr;
-    if (int rc = upload(&p, t)) return rc;
+    if (int rc = upload(d, &p, t)) return rc;
     d->childE.push_back(p);
   }
   d->G.assign(P.hidden.size(), nullptr);
@@ -196,7 +233,7 @@ int ensure_hidden(nipamd_model* mm, int j) {
   } else {
     nipamd::hidden_table(mm->m, j, g);
   }
-  return upload(&d->G[j], g);
+  return upload(d, &d->G[j], g);
 }
 
 // A request's routing through the chain plan: which emission child each
@@ -242,8 +279,8 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
       ts[x] = acc;
     }
     t.M0 = M;
-    if (int rc = upload(&t.Etab16, E)) return rc;
-    if (int rc = upload(&t.ts16, ts)) return rc;
+    if (int rc = upload(d, &t.Etab16, E)) return rc;
+    if (int rc = upload(d, &t.ts16, ts)) return rc;
   }
   // wide: one unscaled table per observed child, the unobserved ones in ebase
   std::vector<double> W;
@@ -267,8 +304,8 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
     }
     eb[y] = v;
   }
-  if (int rc = upload(&t.tabw, W)) return rc;
-  if (int rc = upload(&t.ebase, eb)) return rc;
+  if (int rc = upload(d, &t.tabw, W)) return rc;
+  if (int rc = upload(d, &t.ebase, eb)) return rc;
   if (N <= 32) {
     const int NP = N <= 16 ? 16 : 32;
     std::vector<double> MT;
@@ -296,8 +333,8 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
       for (int y = 0; y < N; y++) acc += P.A64[(size_t)x * 64 + y] * P.s_all64[y];
       wv[x] = acc;
     }
-    if (int rc = upload(&t.mtab, MT)) return rc;
-    if (int rc = upload(&t.wv, wv)) return rc;
+    if (int rc = upload(d, &t.mtab, MT)) return rc;
+    if (int rc = upload(d, &t.wv, wv)) return rc;
   }
   d->reqs.push_back(std::move(t));
   *out = &d->reqs.back();
@@ -1285,6 +1322,20 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   return 0;
 }
 
+int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double* d_out, void* stream) {
+  if (n < 0 || S < 1 || !d_out || (n > 0 && !d_rows) || (n > 64 && !d_work))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (n == 0) {
+    HIP_OK(hipMemsetAsync(d_out, 0, (size_t)S * sizeof(double), (hipStream_t)stream));
+    return 0;
+  }
+  double* tA = d_work;
+  double* tB = d_work ? d_work + (size_t)((n + 63) / 64) * S : nullptr;
+  if (reduce_rows(d_rows, n, S, tA, tB, d_out, (hipStream_t)stream))
+    return fail(NIPAMD_ERROR_DEVICE, "tree launch failed");
+  return 0;
+}
+
 int nipamd_estep_prefix_first_bad(nipamd_model* mm, int T) {
   if (!mm || T < 1) { fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments"); return -2; }
   if (nipamd::estep_prefix_entries(mm->m) > kPrefixMaxEntries) return -2;
@@ -1529,7 +1580,7 @@ static int ensure_joint_map(nipamd_model* mm) {
   HIP_OK(hipMemcpy(d->jm_ptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice));
   HIP_OK(hipMalloc(&d->jm_idx, std::max<size_t>(1, idx.size()) * sizeof(int)));
   if (!idx.empty()) HIP_OK(hipMemcpy(d->jm_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
-  if (int rc = upload(&d->jm_coef, coef)) return rc;
+  if (int rc = upload(d, &d->jm_coef, coef)) return rc;
   d->jm_n = off[nv];
   return 0;
 }
@@ -1550,7 +1601,7 @@ static int ensure_etab_all(nipamd_model* mm) {
       E[base + (size_t)em.M * 16 + y] = em.s[y];
     }
   }
-  return upload(&d->etab_all, E);
+  return upload(d, &d->etab_all, E);
 }
 
 // The general chain e_step's slab (xi sums Kf / Kb without the transition,
@@ -1657,7 +1708,7 @@ static int ensure_chain_map(nipamd_model* mm) {
   HIP_OK(hipMemcpy(d->jm_ptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice));
   HIP_OK(hipMalloc(&d->jm_idx, std::max<size_t>(1, idx.size()) * sizeof(int)));
   if (!idx.empty()) HIP_OK(hipMemcpy(d->jm_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
-  if (int rc = upload(&d->jm_coef, coef)) return rc;
+  if (int rc = upload(d, &d->jm_coef, coef)) return rc;
   d->jm_n = off[nv];
   return 0;
 }

@@ -68,7 +68,11 @@ def exchange(partial, ll, status, group=None):
     power-of-two shards both are bit-identical to the 1-GPU run.
     Returns (partial, ll_total (python float), n_bad (int))."""
     import torch
-    ll_part = tree_sum(ll.to(torch.float64).reshape(-1, 1))
+    if ll.is_cuda:                                # one tree kernel per 64x level (nipamd_tree_sum)
+        from . import tree_sum as gpu_tree_sum
+        ll_part = gpu_tree_sum(ll.to(torch.float64))
+    else:
+        ll_part = tree_sum(ll.to(torch.float64).reshape(-1, 1))
     bad = (status != 0).sum().to(torch.float64).reshape(1).to(partial.device)
     packed = torch.cat([partial.reshape(-1), ll_part.reshape(1).to(partial.device), bad])
     comb = combine_partials(packed, group)

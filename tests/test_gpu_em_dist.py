@@ -138,3 +138,15 @@ def test_config4_shard_scale_and_spot_parity():
     c32, _, _ = nip_amd.e_step(m, sub, ov)
     c32 = c32.cpu().numpy()
     assert np.all(np.abs(c32 - rc) <= 1e-11 * np.maximum(1.0, np.abs(rc)))
+
+
+@pytest.mark.parametrize("n,S", [(1, 1), (63, 1), (64, 1), (65, 3), (4097, 1), (131072, 1), (130001, 2)])
+def test_gpu_tree_sum_bit_identical_to_pairwise_tree(n, S):
+    """nipamd_tree_sum (the exchange's ll tree) is the pairwise tree of
+    em.tree_sum, bit for bit, for any n (odd tails paired with 0)."""
+    import torch
+    rng = np.random.default_rng(n + S)
+    x = torch.tensor(rng.standard_normal((n, S)) * 10.0 ** rng.integers(-8, 8, (n, S)), dtype=torch.float64)
+    want = nem.tree_sum(x.clone())
+    got = nip_amd.tree_sum(x.cuda()).cpu()
+    assert torch.equal(got, want.reshape(-1))
