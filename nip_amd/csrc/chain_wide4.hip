@@ -305,8 +305,219 @@ __device__ __forceinline__ void w4_partner(const WideArgs& a, const W4Lds& L, in
   }
 }
 
-__global__ __launch_bounds__(kW4Threads, 1)
+// ---- chain_row64_kernel: one filter wave per direction (round 3) ----
+//
+// chain_wide4_kernel splits a direction's 64-deep contraction over four
+// waves whose partials meet in LDS behind a block barrier every step: ≈ 1.4K
+// cycles per step, all of it LDS round trips and barrier waits on one
+// sequence's dependency chain (profiles/r02/r02h_config5_wide4_stamps.txt).
+// Here one wave does the whole contraction in registers: lane y holds x(y)
+// and column y of A; two lane-swap levels (v_permlane16_swap, then
+// v_permlane32_swap of both results) leave in every lane the four 16-state
+// blocks of x in canonical order (block 0, 2 from the first value's swap, 1,
+// 3 from the second's), and 64 v_fmac_f64_dpp row_newbcast take x(16b + j)
+// from lane j of the row of block b's copy.  No LDS on the recursion's path
+// and one block barrier per 8 steps, when a partner takes the ring's chunk.
+// Block: 4 waves, one per SIMD: forward filter, backward filter, forward
+// partner, backward partner (the partners as in chain_wide4_kernel).
+constexpr int kR64Threads = 256;
+
+template <int K, bool NOP_FIRST>
+__device__ __forceinline__ void fmac_b(double& acc, double v, double c) {
+  if (NOP_FIRST)
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(v), "v"(c), "n"(K));
+  else
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(v), "v"(c), "n"(K));
+}
+
+// acc[j & 3] += x_block(lane j of the row) * Ac[j], j = 0..15 (sixteen
+// accumulators measured slower: 139K vs 128K cycles per block, the extra
+// zeroing and adds cost more issue slots than the shorter chains save; a
+// single wave per SIMD issues f64 VALU work every ~6.3 cycles)
+__device__ __forceinline__ void fmac16(double (&acc)[4], double xb, const double (&Ac)[16]) {
+  fmac_b<0, true>(acc[0], xb, Ac[0]);    fmac_b<1, false>(acc[1], xb, Ac[1]);
+  fmac_b<2, false>(acc[2], xb, Ac[2]);   fmac_b<3, false>(acc[3], xb, Ac[3]);
+  fmac_b<4, false>(acc[0], xb, Ac[4]);   fmac_b<5, false>(acc[1], xb, Ac[5]);
+  fmac_b<6, false>(acc[2], xb, Ac[6]);   fmac_b<7, false>(acc[3], xb, Ac[7]);
+  fmac_b<8, false>(acc[0], xb, Ac[8]);   fmac_b<9, false>(acc[1], xb, Ac[9]);
+  fmac_b<10, false>(acc[2], xb, Ac[10]); fmac_b<11, false>(acc[3], xb, Ac[11]);
+  fmac_b<12, false>(acc[0], xb, Ac[12]); fmac_b<13, false>(acc[1], xb, Ac[13]);
+  fmac_b<14, false>(acc[2], xb, Ac[14]); fmac_b<15, false>(acc[3], xb, Ac[15]);
+}
+
+// the four 16-state blocks of x (lane l holds x(l)) in every lane: xb[b] at
+// lane (row r, i) = x(16 b + i)
+__device__ __forceinline__ void blocks_of(double x, double (&xb)[4]) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);   // [0]: block r & ~1, [1]: r | 1
+  const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto q0l = __builtin_amdgcn_permlane32_swap(pl[0], pl[0], false, false);   // blocks 0, 2
+  const auto q0h = __builtin_amdgcn_permlane32_swap(ph[0], ph[0], false, false);
+  const auto q1l = __builtin_amdgcn_permlane32_swap(pl[1], pl[1], false, false);   // blocks 1, 3
+  const auto q1h = __builtin_amdgcn_permlane32_swap(ph[1], ph[1], false, false);
+  xb[0] = __hiloint2double((int)q0h[0], (int)q0l[0]);
+  xb[2] = __hiloint2double((int)q0h[1], (int)q0l[1]);
+  xb[1] = __hiloint2double((int)q1h[0], (int)q1l[0]);
+  xb[3] = __hiloint2double((int)q1h[1], (int)q1l[1]);
+}
+
+template <bool FWD>
+__device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, int y, int nA, int nAi, int nB,
+                                           int nBi) {
+  const int T = a.T, H = a.H;
+  const int d = FWD ? 0 : 1;
+  double Ac[4][16];                       // A(16 b + j, y) (forward) / A(y, 16 b + j) (backward)
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+#pragma unroll
+    for (int j = 0; j < 16; j++) Ac[b][j] = FWD ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
+  double x;
+  int sc = 0;
+  if (FWD) {
+    x = a.pi[y];
+  } else {
+    x = (nA + nB > 0) ? evidence(a, L, T - 1, y) * (y < a.N ? 1.0 : 0.0) : 0.0;   // e_{T-1} o beta_{T-1}
+    sc = -__builtin_amdgcn_frexp_exp(wave_sum(x));
+  }
+  const bool dg = a.diag != nullptr;
+  const unsigned long long c0 = dg ? __builtin_readcyclecounter() : 0;
+  unsigned long long twait = 0;
+  auto phase = [&](int n, int ni, int t0) {
+    double en = n > 0 ? evidence(a, L, t0, y) : 1.0;
+    for (int c = 0; c < ni; c += 8) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = c + k;
+        if (i < n) {
+          const int t = FWD ? t0 + i : t0 - i;
+          const double e = en;
+          if (i + 1 < n) en = evidence(a, L, FWD ? t + 1 : t - 1, y);     // the next step's
+          double xb[4];
+          blocks_of(x, xb);
+          double acc[4] = {0.0, 0.0, 0.0, 0.0};
+          fmac16(acc, xb[0], Ac[0]);
+          fmac16(acc, xb[1], Ac[1]);
+          fmac16(acc, xb[2], Ac[2]);
+          fmac16(acc, xb[3], Ac[3]);
+          const double u = __builtin_ldexp((acc[0] + acc[1]) + (acc[2] + acc[3]), sc);
+          const double p = u * e;
+          const int slot = i & (kW4Ring - 1);
+          L.ring[(d * kW4Ring + slot) * 64 + y] = FWD ? p : u;
+          if (FWD) L.uring[slot * 64 + y] = u;
+          const bool rs = (i & (kW4Rescale - 1)) == kW4Rescale - 1 || i == n - 1;
+          sc = rs ? -__builtin_amdgcn_frexp_exp(wave_sum(p)) : 0;   // frexp exponent of 0 is 0
+          x = p;
+        }
+      }
+      const unsigned long long tb = dg ? __builtin_readcyclecounter() : 0;
+      block_barrier();                                  // the chunk to the partner
+      if (dg) twait += __builtin_readcyclecounter() - tb;
+    }
+  };
+  // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
+  phase(nA, nAi, FWD ? 0 : T - 2);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
+  phase(nB, nBi, FWD ? H : H - 1);
+  if (dg && y == 0) {
+    a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 0] = __builtin_readcyclecounter() - c0;
+    a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 1] = twait;
+  }
+}
+
+// The partner takes the ring's chunk c (steps 8c..8c+7) after the chunk's
+// barrier, while the filter writes chunk c + 1 into the ring's other half.
+template <bool FWD>
+__device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, int y, long b, int nA, int nAi,
+                                            int nB, int nBi) {
+  const int T = a.T, H = a.H;
+  const int d = FWD ? 0 : 1;
+  double* const Srow = a.S + (size_t)b * chain_scratch_row64(T) + (size_t)kW4G * 64 + y;
+  double* const Prow = (a.post && y < a.N) ? a.post + (size_t)b * a.post_bstride + a.post_off + y : nullptr;
+  const double s = a.s[y];
+  double m2 = 1.0, m1 = 1.0, zmin = 1.0;
+  int e2 = 0, e1 = 0;
+  // forward ll (nip.c:1461-1474): z2 = sum alpha_t, z1 = sum u_t s, both on
+  // the same (power-of-two) scale; mantissas and exponents kept apart
+  auto ll_step = [&](int slot) {
+    double z[2] = {L.ring[slot * 64 + y], L.uring[slot * 64 + y] * s};
+    wave_sum_n<2>(z);
+    zmin = __builtin_fmin(zmin, z[0]);
+    m2 *= __builtin_amdgcn_frexp_mant(z[0]); e2 += __builtin_amdgcn_frexp_exp(z[0]);
+    m1 *= __builtin_amdgcn_frexp_mant(z[1]); e1 += __builtin_amdgcn_frexp_exp(z[1]);
+    const int k2 = __builtin_amdgcn_frexp_exp(m2), k1 = __builtin_amdgcn_frexp_exp(m1);
+    m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+    m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+  };
+  const unsigned long long c0 = a.diag ? __builtin_readcyclecounter() : 0;
+  if (!FWD && !a.filter) Srow[(long)(T - 1) * 64] = y < a.N ? 1.0 : 0.0;   // beta_{T-1}, T-1 >= H
+  // phase A: the interface vectors to the scratch
+  for (int c = 0; c < nAi; c += 8) {
+    block_barrier();
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int j = c + k;
+      if (j < nA) {
+        const int slot = j & (kW4Ring - 1);
+        Srow[(long)(FWD ? j : T - 2 - j) * 64] = L.ring[(d * kW4Ring + slot) * 64 + y];
+        if (FWD) ll_step(slot);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // phase B: posterior = normalise(this o other); the other direction's
+  // vectors come from the scratch one chunk ahead, ping-ponged between two
+  // register sets
+  const int tB = FWD ? H : H - 1;
+  auto tof = [&](int j) { return FWD ? tB + j : tB - j; };
+  const double* const Sld = a.filter ? a.S + y : Srow;   // forward_inference: a valid dummy row
+  const long sstr = a.filter ? 0 : 64;
+  auto load8 = [&](double (&r)[8], int c) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) r[k] = Sld[(long)tof(8 * c + k) * sstr];   // guards cover the over-run
+  };
+  auto chunk = [&](const double (&r)[8], int c) {
+    block_barrier();                                 // the filter's chunk c is in the ring
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int j = 8 * c + k;
+      if (j < nB) {
+        const int slot = j & (kW4Ring - 1);
+        const double pr = L.ring[(d * kW4Ring + slot) * 64 + y] * (a.filter ? 1.0 : r[k]);
+        const double q = pr * recip(wave_sum(pr));   // an all-zero row stays zero
+        if (Prow) Prow[(long)tof(j) * a.post_tstride] = q;
+        if (FWD) ll_step(slot);
+      }
+    }
+  };
+  const int nch = nBi / 8;                           // nBi: a multiple of 8 (kernel)
+  double ra[8], rb[8];
+  load8(ra, 0);
+  for (int c = 0; c < nch; c += 2) {
+    load8(rb, c + 1);
+    chunk(ra, c);
+    if (c + 1 >= nch) break;
+    load8(ra, c + 2);
+    chunk(rb, c + 1);
+  }
+  if (a.diag && y == 0) a.diag[blockIdx.x * 16 + (FWD ? 8 : 12)] = __builtin_readcyclecounter() - c0;
+  if (FWD && y == 0) {
+    double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+    const bool dead = zmin == 0.0;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 1u : 0u;
+  }
+}
+
+// R64: chain_row64_kernel's roles (one filter wave per direction, 4 waves)
+template <bool R64>
+__global__ __launch_bounds__(R64 ? kR64Threads : kW4Threads, 1)
 void chain_wide4_kernel(WideArgs a) {
+  constexpr int kThreads = R64 ? kR64Threads : kW4Threads;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   lds_d* sm = (lds_d*)(smem);
   W4Lds L;
@@ -332,11 +543,11 @@ void chain_wide4_kernel(WideArgs a) {
 #pragma unroll
   for (int k = 0; k < 4; k++)
     if (k < a.ncol)
-      for (int i = tid; i < (a.M[k] + 2) * 64; i += kW4Threads) tab[toff[k] + i] = a.tab[k][i];
-  for (int i = tid; i < 64; i += kW4Threads) tab[L.eoff + i] = a.ebase[i];
+      for (int i = tid; i < (a.M[k] + 2) * 64; i += kThreads) tab[toff[k] + i] = a.tab[k][i];
+  for (int i = tid; i < 64; i += kThreads) tab[L.eoff + i] = a.ebase[i];
   for (int k = 0; k < a.ncol; k++) {
     const int M = a.M[k];
-    for (int i = tid; i < Tr; i += kW4Threads) {
+    for (int i = tid; i < Tr; i += kThreads) {
       const int t = i - kW4G;
       int c = M;                                      // missing / guard
       if (t >= 0 && t < T) {
@@ -355,10 +566,17 @@ void chain_wide4_kernel(WideArgs a) {
   // block-uniform iteration counts, multiples of the partners' 8-step batches
   const int nAi = ((nAf > nAb ? nAf : nAb) + 7) & ~7;
   const int nBi = ((nBf > nBb ? nBf : nBb) + 7) & ~7;
-  if (wave < kQ) w4_filter<true>(a, L, wave, lane, nAf, nAi, nBf, nBi);
-  else if (wave < 2 * kQ) w4_filter<false>(a, L, wave - kQ, lane, nAb, nAi, nBb, nBi);
-  else if (wave == 2 * kQ) w4_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
-  else w4_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
+  if constexpr (R64) {
+    if (wave == 0) r64_filter<true>(a, L, lane, nAf, nAi, nBf, nBi);
+    else if (wave == 1) r64_filter<false>(a, L, lane, nAb, nAi, nBb, nBi);
+    else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
+    else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
+  } else {
+    if (wave < kQ) w4_filter<true>(a, L, wave, lane, nAf, nAi, nBf, nBi);
+    else if (wave < 2 * kQ) w4_filter<false>(a, L, wave - kQ, lane, nAb, nAi, nBb, nBi);
+    else if (wave == 2 * kQ) w4_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
+    else w4_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
+  }
 }
 
 }  // namespace
@@ -371,13 +589,24 @@ size_t chain_wide4_lds_bytes(const WideArgs& a) {
          (size_t)(a.ncol > 0 ? a.ncol : 1) * chain_codes_row(a.T);
 }
 
+#ifndef NIPAMD_R64
+#define NIPAMD_R64 1               // 33..64 states: chain_row64_kernel (0: chain_wide4_kernel, four waves per direction)
+#endif
+
 int chain_wide4_launch(const WideArgs& a, hipStream_t stream) {
   const size_t lds = (chain_wide4_lds_bytes(a) + 15) & ~(size_t)15;
   if (lds > 160 * 1024) return -2;
-  static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel), lds, lds_set)) return -1;
-  hipLaunchKernelGGL(chain_wide4_kernel, dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
-  g_last_kernel = "chain_wide4_kernel";
+  if (NIPAMD_R64) {
+    static size_t lds_set[kMaxDevices] = {};
+    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<true>), lds, lds_set)) return -1;
+    hipLaunchKernelGGL(chain_wide4_kernel<true>, dim3((unsigned)a.B), dim3(kR64Threads), lds, stream, a);
+    g_last_kernel = "chain_row64_kernel";
+  } else {
+    static size_t lds_set[kMaxDevices] = {};
+    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<false>), lds, lds_set)) return -1;
+    hipLaunchKernelGGL(chain_wide4_kernel<false>, dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
+    g_last_kernel = "chain_wide4_kernel";
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -171,7 +171,7 @@ def test_config3_full_size_properties_and_parity():
         assert abs(ll[b].item() - rl) <= 1e-11 * abs(rl)
 
 
-# 33..64 states: chain_wide4_kernel (four filter waves per direction, one
+# 33..64 states: chain_row64_kernel (one filter wave per direction; chain_wide4_kernel, four per direction, one
 # barrier per step, sparse rescaling, partner waves for scratch/posterior/ll)
 @pytest.mark.parametrize("card,B,T", [(48, 3, 21), (40, 2, 2), (64, 2, 9), (33, 3, 1)])
 def test_wide4_demo1_vs_oracle(card, B, T):
