@@ -57,14 +57,17 @@ METRIC = "sequence-timesteps/s fwd-bwd smoothing, 16-state DBN; 1/2/4/8-GPU scal
 HBM_PEAK_GBS = 8000.0            # MI355X spec (MI355X_MICROARCH.md chip table)
 N_CU = 256
 # Dependency-chain floors of the matrix-core filters, measured by
-# profiles/r03/mb_lat.hip (one wave per CU, s_memtime cycles; r03_mb_lat.txt):
+# profiles/r03/mb_lat.hip (one wave per CU, s_memtime cycles; r03x_mb_lat.txt):
 # kernel -> (cycles per filter step, sequences per block, blocks resident per CU)
 LATENCY_STEP = {
-    "chain_fb_ckpt_kernel": (328.0, 16, 1),            # 4 chained v_mfma_f64_16x16x4, D -> next B
-    "chain_fb_ckpt_kernel<proj>": (328.0, 16, 1),
-    "chain_fb_mfma_kernel": (328.0, 16, 1),
-    "chain_mfma_wide_kernel<1>": (328.0, 16, 1),
-    "chain_mfma_wide_kernel<2>": (1136.1, 16, 1),      # 2 x 8 chained, interleaved (93 KB LDS: 1 block/CU)
+    # 4 chained v_mfma_f64_16x16x4 and the step's evidence multiply on the
+    # VALU between them (V4: the recursion's own dependency chain; the MFMAs
+    # alone, V2, take 328)
+    "chain_fb_ckpt_kernel": (464.0, 16, 1),
+    "chain_fb_ckpt_kernel<proj>": (464.0, 16, 1),
+    "chain_fb_mfma_kernel": (464.0, 16, 1),
+    "chain_mfma_wide_kernel<1>": (464.0, 32, 1),       # two groups of 16 per block, concurrently
+    "chain_mfma_wide_kernel<2>": (1136.1, 32, 1),      # 2 x 8 chained MFMAs, interleaved (V3); two groups of 16
 }
 CLOCK_GHZ = 2.39                 # in-kernel clock under the chain loop (s_memtime / s_memrealtime, r03_mb_lat.txt)
 
@@ -81,6 +84,11 @@ def kernel_bytes(kname: str, N: int, n_obs: int, posterior: bool):
                 "obs %d + every 4th interface message as a checkpoint (%d written + %d read) + posterior %d"
                 % (4 * n_obs, ck, ck, 8 * N))
     post = 8 * N if posterior else 0
+    if kname.startswith("chain_mfma_wide_kernel") and posterior:
+        # both filters read the observation codes from HBM (no LDS staging)
+        return (8 * n_obs + 16 * N + post,
+                "obs %d (read by both filters) + interface message written and read back (%d + %d) + posterior %d"
+                % (8 * n_obs, 8 * N, 8 * N, post))
     return (4 * n_obs + 16 * N + post,
             "obs %d + interface message written and read back (%d + %d)%s"
             % (4 * n_obs, 8 * N, 8 * N, " + posterior %d" % post if post else " (counts stay on chip)"))
@@ -381,7 +389,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         roof["latency"] = {"bound": "filter dependency chain", "cycles_per_step": cyc, "steps": T,
                            "block_rounds": rounds, "clock_ghz": CLOCK_GHZ, "floor_ms": floor_ms,
                            "frac": floor_ms / kern_ms,
-                           "source": "profiles/r03/r03_mb_lat.txt (mb_lat.hip: the step's MFMA chain alone)"}
+                           "source": "profiles/r03/r03x_mb_lat.txt (mb_lat.hip: V4 for the 16-state step, V3 for the 32-state step)"}
     rec = {"metric": metric, "value": value, "unit": "sequence-timesteps/s", "n_gpus": world,
            "steps": steps, "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
