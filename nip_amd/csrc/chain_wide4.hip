@@ -363,7 +363,11 @@ __device__ __forceinline__ void blocks_of(double x, double (&xb)[4]) {
   xb[3] = __hiloint2double((int)q1h[1], (int)q1l[1]);
 }
 
-template <bool FWD>
+// NC: observed columns (0..4).  The step's evidence e_t(y) = ebase(y) x one
+// table entry per column: the codes of the next 8 steps are read a chunk
+// ahead and each entry one step ahead, so no LDS load waits on the
+// recursion's path (evidence() did two dependent LDS round trips per step).
+template <bool FWD, int NC>
 __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, int y, int nA, int nAi, int nB,
                                            int nBi) {
   const int T = a.T, H = a.H;
@@ -381,19 +385,35 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
     x = (nA + nB > 0) ? evidence(a, L, T - 1, y) * (y < a.N ? 1.0 : 0.0) : 0.0;   // e_{T-1} o beta_{T-1}
     sc = -__builtin_amdgcn_frexp_exp(wave_sum(x));
   }
+  const double eb = L.tab[L.eoff + y];
+  const int toff[4] = {L.toff0, L.toff1, L.toff2, L.toff3};
+  constexpr int NK = NC > 0 ? NC : 1;
+  auto row = [&](int k, int code) { return L.tab[toff[k] + code * 64 + y]; };
   const bool dg = a.diag != nullptr;
   const unsigned long long c0 = dg ? __builtin_readcyclecounter() : 0;
   unsigned long long twait = 0;
   auto phase = [&](int n, int ni, int t0) {
-    double en = n > 0 ? evidence(a, L, t0, y) : 1.0;
-    for (int c = 0; c < ni; c += 8) {
+    // codes of the chunk's 8 steps from step index c (guards cover the over-run)
+    auto ldc = [&](int c, int (&cd)[NK][8]) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = c + k;
+      for (int k = 0; k < NC; k++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) cd[k][j] = L.codes[k * L.Tr + kW4G + (FWD ? t0 + c + j : t0 - c - j)];
+    };
+    int cc[NK][8], cn[NK][8];
+    double tv[NK];                              // the current step's table entries
+    ldc(0, cc);
+#pragma unroll
+    for (int k = 0; k < NC; k++) tv[k] = row(k, cc[k][0]);
+    for (int c = 0; c < ni; c += 8) {
+      ldc(c + 8, cn);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int i = c + j;
         if (i < n) {
-          const int t = FWD ? t0 + i : t0 - i;
-          const double e = en;
-          if (i + 1 < n) en = evidence(a, L, FWD ? t + 1 : t - 1, y);     // the next step's
+          double tn[NK];                          // the next step's, loaded under this step's FMAs
+#pragma unroll
+          for (int k = 0; k < NC; k++) tn[k] = row(k, j < 7 ? cc[k][j + 1] : cn[k][0]);
           double xb[4];
           blocks_of(x, xb);
           double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -401,6 +421,9 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
           fmac16(acc, xb[1], Ac[1]);
           fmac16(acc, xb[2], Ac[2]);
           fmac16(acc, xb[3], Ac[3]);
+          double e = eb;                          // evidence(): the same products in the same order
+#pragma unroll
+          for (int k = 0; k < NC; k++) e *= tv[k];
           const double u = __builtin_ldexp((acc[0] + acc[1]) + (acc[2] + acc[3]), sc);
           const double p = u * e;
           const int slot = i & (kW4Ring - 1);
@@ -409,8 +432,14 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
           const bool rs = (i & (kW4Rescale - 1)) == kW4Rescale - 1 || i == n - 1;
           sc = rs ? -__builtin_amdgcn_frexp_exp(wave_sum(p)) : 0;   // frexp exponent of 0 is 0
           x = p;
+#pragma unroll
+          for (int k = 0; k < NC; k++) tv[k] = tn[k];
         }
       }
+#pragma unroll
+      for (int k = 0; k < NC; k++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) cc[k][j] = cn[k][j];
       const unsigned long long tb = dg ? __builtin_readcyclecounter() : 0;
       block_barrier();                                  // the chunk to the partner
       if (dg) twait += __builtin_readcyclecounter() - tb;
@@ -513,8 +542,9 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
   }
 }
 
-// R64: chain_row64_kernel's roles (one filter wave per direction, 4 waves)
-template <bool R64>
+// R64: chain_row64_kernel's roles (one filter wave per direction, 4 waves);
+// NC: its observed columns
+template <bool R64, int NC>
 __global__ __launch_bounds__(R64 ? kR64Threads : kW4Threads, 1)
 void chain_wide4_kernel(WideArgs a) {
   constexpr int kThreads = R64 ? kR64Threads : kW4Threads;
@@ -567,8 +597,8 @@ void chain_wide4_kernel(WideArgs a) {
   const int nAi = ((nAf > nAb ? nAf : nAb) + 7) & ~7;
   const int nBi = ((nBf > nBb ? nBf : nBb) + 7) & ~7;
   if constexpr (R64) {
-    if (wave == 0) r64_filter<true>(a, L, lane, nAf, nAi, nBf, nBi);
-    else if (wave == 1) r64_filter<false>(a, L, lane, nAb, nAi, nBb, nBi);
+    if (wave == 0) r64_filter<true, NC>(a, L, lane, nAf, nAi, nBf, nBi);
+    else if (wave == 1) r64_filter<false, NC>(a, L, lane, nAb, nAi, nBb, nBi);
     else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
     else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
   } else {
@@ -593,18 +623,32 @@ size_t chain_wide4_lds_bytes(const WideArgs& a) {
 #define NIPAMD_R64 1               // 33..64 states: chain_row64_kernel (0: chain_wide4_kernel, four waves per direction)
 #endif
 
+namespace {
+template <int NC>
+int launch_r64(const WideArgs& a, size_t lds, hipStream_t stream) {
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<true, NC>), lds, lds_set)) return -1;
+  hipLaunchKernelGGL((chain_wide4_kernel<true, NC>), dim3((unsigned)a.B), dim3(kR64Threads), lds, stream, a);
+  return 0;
+}
+}  // namespace
+
 int chain_wide4_launch(const WideArgs& a, hipStream_t stream) {
   const size_t lds = (chain_wide4_lds_bytes(a) + 15) & ~(size_t)15;
   if (lds > 160 * 1024) return -2;
   if (NIPAMD_R64) {
-    static size_t lds_set[kMaxDevices] = {};
-    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<true>), lds, lds_set)) return -1;
-    hipLaunchKernelGGL(chain_wide4_kernel<true>, dim3((unsigned)a.B), dim3(kR64Threads), lds, stream, a);
+    switch (a.ncol) {
+      case 0: if (launch_r64<0>(a, lds, stream)) return -1; break;
+      case 1: if (launch_r64<1>(a, lds, stream)) return -1; break;
+      case 2: if (launch_r64<2>(a, lds, stream)) return -1; break;
+      case 3: if (launch_r64<3>(a, lds, stream)) return -1; break;
+      default: if (launch_r64<4>(a, lds, stream)) return -1; break;
+    }
     g_last_kernel = "chain_row64_kernel";
   } else {
     static size_t lds_set[kMaxDevices] = {};
-    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<false>), lds, lds_set)) return -1;
-    hipLaunchKernelGGL(chain_wide4_kernel<false>, dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
+    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<false, 0>), lds, lds_set)) return -1;
+    hipLaunchKernelGGL((chain_wide4_kernel<false, 0>), dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
     g_last_kernel = "chain_wide4_kernel";
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
