@@ -220,3 +220,23 @@ def test_wide4_matches_one_wave_kernel_config5():
         outs.append(np.load(path))
     assert np.abs(outs[0]["p"] - outs[1]["p"]).max() <= 1e-12
     assert np.all(np.abs(outs[0]["l"] - outs[1]["l"]) <= 1e-11 * np.maximum(1.0, np.abs(outs[1]["l"])))
+
+
+def _four_child_spec(card=36, m=5, seed=7):
+    """A 36-state chain observed through up to four leaf children (the
+    row-form 33..64-state kernel is instantiated per observed-column count)."""
+    nodes = [("X0", card, "X1"), ("X1", card, None)] + [("O%d" % i, m, None) for i in range(1, 5)]
+    pots = [("X1", ["X0"], synth.cpt(seed, card, card)), ("X0", [], synth.cpt(seed + 1, card, 1))]
+    pots += [("O%d" % i, ["X1"], synth.cpt(seed + 1 + i, m, card)) for i in range(1, 5)]
+    return nodes, pots
+
+
+@pytest.mark.parametrize("cols", [["O1"], ["O2", "O4"], ["O1", "O2", "O3"], ["O4", "O3", "O2", "O1"]])
+def test_row64_observed_columns_vs_oracle(cols):
+    m = nip_amd.Model.from_spec(*_four_child_spec())
+    ov = [m.variable(c) for c in cols]
+    obs = synth.observations(3, 19, 5, seed=len(cols) + 3, n_obs=len(cols))
+    obs[1, ::3, 0] = -1                               # missing values on one child
+    obs[2, 5, -1] = 7                                 # out of range: zero mass from step 5
+    check_vs_oracle(m, obs, ov, [m.variable("X1")], 1e-12, 1e-11)
+    assert nip_amd.last_kernel() == "chain_row64_kernel"
