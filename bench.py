@@ -271,15 +271,18 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         step()
     barrier()
     kname = nip_amd.last_kernel()       # the kernel the engine chose for this request
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # one event pair around the K steps on the launch stream (torch's current
+    # stream, which the engine launches on): per-step event packets would sit
+    # between the kernels and lengthen the very gaps they measure
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for i in range(steps):
-        evs[i][0].record()
         step()
-        evs[i][1].record()
+    ev1.record()
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    kern_ms = ev0.elapsed_time(ev1) / steps
     if name == "em":
         ll.zero_()
         st.zero_()

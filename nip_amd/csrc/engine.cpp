@@ -1233,20 +1233,25 @@ static int estep_rows(const nipamd::ChainPlan& P) {
   return R;
 }
 
+// The body is the larger of the layouts this model's routes can produce,
+// whatever the engine setting, so the tag sits at the same offset for every
+// partial of a model version (a set_engine between partial and finalize
+// cannot move it into the counts).
+static bool has_chain_estep(const nipamd::ChainPlan& P) {
+  return P.valid && (P.hmm || P.jhmm || estep_general_plan(P));
+}
 static int estep_body_size(const nipamd_model* mm) {
   const int ps = nipamd::param_size(mm->m);
   const auto& P = mm->m.chain;
-  if (mm->engine != NIPAMD_ENGINE_JTREE && P.valid && (P.hmm || P.jhmm))
-    return std::max(ps, nipamd::chain_estep_slab(P.emits[0].M));
-  if (mm->engine != NIPAMD_ENGINE_JTREE && estep_general_plan(P))
-    return std::max(ps, nipamd::chain_estep_slab(estep_rows(P) - 2));
-  return mm->engine == NIPAMD_ENGINE_CHAIN ? -1 : ps;
+  if (P.valid && (P.hmm || P.jhmm)) return std::max(ps, nipamd::chain_estep_slab(P.emits[0].M));
+  if (estep_general_plan(P)) return std::max(ps, nipamd::chain_estep_slab(estep_rows(P) - 2));
+  return ps;
 }
 
 int nipamd_estep_partial_size(const nipamd_model* mm) {
   if (!mm) return -1;
-  const int body = estep_body_size(mm);
-  return body < 0 ? -1 : body + 2;
+  if (mm->engine == NIPAMD_ENGINE_CHAIN && !has_chain_estep(mm->m.chain)) return -1;
+  return estep_body_size(mm) + 2;
 }
 
 // e_step kernel of the chain route: 3 = chain_estep16_kernel (16-lane DPP
@@ -1284,13 +1289,17 @@ static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_var
 
 // The reference's verdict on a leading run of missing observations
 // (prefix.cpp), once per model version and T; -1: no step is rejected.
-// Models whose join tree has more than kPrefixMaxEntries table entries are
-// not simulated (-2: their leading missing runs are accepted).
-constexpr long kPrefixMaxEntries = 1L << 20;
+// prefix.cpp bounds its own work (entries x steps); models whose join tree
+// holds more than kPrefixMaxEntries table entries are not simulated at all
+// (-2: their leading missing runs are accepted).
+constexpr long kPrefixMaxEntries = 1L << 26;
 
 static int prefix_first_bad(nipamd_model* mm, int T) {
   const int c = mm->pf_first_bad;
-  const bool hit = mm->pf_version == mm->version && (c == -2 || c >= 0 || T <= mm->pf_T);
+  // -1 holds for every shorter T, a step >= 0 for every T, -2 (the work bound
+  // ran out) for every longer T
+  const bool hit = mm->pf_version == mm->version &&
+                   (c >= 0 || (c == -1 && T <= mm->pf_T) || (c == -2 && T >= mm->pf_T));
   if (!hit) {
     mm->pf_first_bad = nipamd::estep_prefix_entries(mm->m) > kPrefixMaxEntries
                            ? -2 : nipamd::estep_prefix_first_bad(mm->m, T, nullptr);
@@ -1311,6 +1320,12 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
                          void* stream) {
   if (!mm || B < 0 || T < 1 || !d_partial || (n_obs > 0 && (!d_obs || !obs_vars)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  // The reference rejects series whose leading missing run reaches the
+  // model's verdict step (BAD_LUCK): without d_status that verdict could not
+  // be reported, and the partial would include counts the reference drops.
+  if (!d_status && B > 0 && prefix_first_bad(mm, T) >= 0)
+    return fail(NIP_ERROR_INVALID_ARGUMENT,
+                "d_status is required: this model's e_step rejects series with a long leading missing run");
   if (int rc = estep_partial_routes(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
     return rc;
   if (!d_status || B == 0) return 0;
@@ -1716,7 +1731,6 @@ static int ensure_chain_map(nipamd_model* mm) {
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   const int body = estep_body_size(mm);
-  if (body < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "no e_step plan for this model under the selected engine");
   // the route tag (see nipamd_estep_partial_size): one 16-byte read, once per EM iteration
   double tag[2] = {0.0, 0.0};
   HIP_OK(hipMemcpyAsync(tag, d_partial + body, sizeof(tag), hipMemcpyDeviceToHost, (hipStream_t)stream));
@@ -1726,8 +1740,7 @@ int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_c
                                             "layout) were combined, or the buffer is not an e_step partial");
   if (tag[1] >= 1.0) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
   const auto& P = mm->m.chain;
-  if (!P.valid || !(P.hmm || P.jhmm || estep_general_plan(P)))
-    return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
+  if (!has_chain_estep(P)) return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
   if (int rc = ensure_tables(mm)) return rc;
   Route rh;
   rh.primary = 0;

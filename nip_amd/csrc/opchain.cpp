@@ -208,17 +208,16 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
     }
     P->device = dev;
   }
-  const size_t need = op_scratch_bytes(B, T);
-  if (!filt && P->S_bytes < need) {
+  // Smoothing keeps every sequence's rows plus a sink row past them; filter
+  // mode keeps no rows, and its masked lanes (inactive sequences, states
+  // y >= K) write to a sink at the start of S (op_fb_kernel).
+  const size_t need = filt ? op_scratch_bytes(1, 1) : op_scratch_bytes(B, T);
+  if (P->S_bytes < need) {
     (void)hipFree(P->S);
     P->S = nullptr;
     P->S_bytes = 0;
     if (hipMalloc(&P->S, need) != hipSuccess) { err = "scratch"; return NIPAMD_ERROR_DEVICE; }
     P->S_bytes = need;
-  }
-  if (filt && !P->S) {
-    if (hipMalloc(&P->S, op_scratch_bytes(1, 1)) != hipSuccess) { err = "scratch"; return NIPAMD_ERROR_DEVICE; }
-    P->S_bytes = op_scratch_bytes(1, 1);
   }
   OpArgs a{};
   a.obs = d_obs;

@@ -119,7 +119,10 @@ void op_fb_kernel(OpArgs a) {
   const double* const Tsrc = tl ? Tl : a.Ttab;
   const bool ys = y < K;
   const double wy = ys ? a.w[y] : 0.0;
-  double* const sink = a.S + (size_t)(a.B + 1) * op_row(T) * 16 + y;
+  // filter mode keeps no rows in S: its sink is S's first 16 doubles (the
+  // host allocates op_scratch_bytes(1, 1) for it); smoothing puts the sink
+  // row past the last sequence's rows
+  double* const sink = a.filter ? a.S + y : a.S + (size_t)(a.B + 1) * op_row(T) * 16 + y;
   double* const Srow = a.S + ((size_t)(active ? b : 0) * op_row(T) + kOpGuard) * 16 + y;
   double* const Sst = active ? Srow : sink;
   const long sst = active ? 16 : 0;

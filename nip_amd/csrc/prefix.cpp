@@ -234,14 +234,23 @@ struct Sim {
   }
 };
 
-constexpr int kMaxPeriod = 8;
+constexpr int kMaxPeriod = 32;
+// Work bound: table entries x propagated steps.  A chain whose forward message
+// has not repeated (bit for bit, period <= kMaxPeriod) within this budget is
+// not simulated further (-2: its leading missing runs are accepted), so the
+// host work per model version stays within about a second whatever T, the
+// chain's mixing time or its period.
+constexpr long kPrefixWork = 1L << 29;
 
 }  // namespace
 
 // First step k < T at which the reference's e_step would reject a series that
-// has observed nothing at steps 0..k; -1 if there is none.  `steps` (if not
-// null) receives the number of steps actually propagated.
+// has observed nothing at steps 0..k; -1 if there is none; -2 if the work
+// bound ran out first.  `steps` (if not null) receives the number of steps
+// actually propagated.
 int estep_prefix_first_bad(const Model& m, int T, int* steps) {
+  const long entries = std::max(1L, estep_prefix_entries(m));
+  const long budget = std::max(16L, kPrefixWork / entries);
   Sim S(m);
   S.reset();
   S.use_priors(false);
@@ -251,6 +260,7 @@ int estep_prefix_first_bad(const Model& m, int T, int* steps) {
   std::vector<double> inc;                // the increment of every step so far
   int t = 0;
   for (; t < T; t++) {
+    if (t >= budget) { if (steps) *steps = t; return -2; }
     if (t > 0) S.finish(alpha);
     S.make_consistent();
     const double m1 = S.mass();

@@ -118,3 +118,40 @@ def test_prefix_verdict_independent_of_T():
         k0 = min(first)
         for T, k in ks.items():
             assert k == (k0 if T > k0 else -1)
+
+
+def test_prefix_work_is_bounded_on_a_long_period_chain():
+    """A chain whose forward message cycles with a period above the repeat
+    check's window never repeats within it: the simulation stops at its work
+    bound instead of propagating T steps, and answers -2 (not
+    simulated) or a verdict it reached before the bound."""
+    import time
+    N, M = 40, 3
+    nodes = [("P0", N, "P1"), ("P1", N, None), ("M1", M, None)]
+    trans = np.zeros((N, N))
+    trans[np.arange(N), (np.arange(N) + 1) % N] = 1.0        # P1 = P0 + 1 (mod 40)
+    prior = synth.cpt(7, N, 1)
+    pots = [("M1", ["P1"], synth.cpt(3, M, N)), ("P1", ["P0"], trans.ravel()), ("P0", [], prior)]
+    m = nip_amd.Model.from_spec(nodes, pots)
+    t0 = time.time()
+    k = m.estep_prefix_first_bad(20_000_000)
+    assert time.time() - t0 < 60
+    assert k >= -2
+    # a short T within the bound is simulated to the end, as before
+    k_short = m.estep_prefix_first_bad(200)
+    assert k_short >= -1
+    if k >= 0:
+        assert k_short == (k if k < 200 else -1)
+
+
+def test_prefix_verdict_on_a_wide_clique_model():
+    """Config 5's structure (in-clique card^4 entries) is simulated too (it was
+    skipped above 2^20 entries before round 4): at 64 states the reference's
+    e_step rejects a series whose leading missing run reaches the step this
+    returns.  The 16.7M-entry join tree takes about a second on the host."""
+    import time
+    m = nip_amd.Model.from_spec(*synth.wide_spec(64, 16))
+    t0 = time.time()
+    k = m.estep_prefix_first_bad(128)
+    assert time.time() - t0 < 30
+    assert k >= -1                          # simulated, not skipped (-2)

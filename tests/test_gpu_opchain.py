@@ -96,6 +96,22 @@ def test_zero_mass_and_ragged_batch():
     assert (st == 0).sum() == 1001
 
 
+def test_filter_first_on_a_fresh_model():
+    """forward_inference before any smoothing call (filter mode's
+    masked lanes wrote to a sink sized for the first request only), with a
+    ragged B and K < 16; then smoothing and filtering with larger B and T than
+    any earlier call, each against the general engine."""
+    m = nip_amd.Model.from_net(os.path.join(GOLD, "demo1.net"))
+    ov = [m.variable(s) for s in ("A1", "B1", "D1")]
+    q = [m.variable("C1")]
+    rng = np.random.default_rng(11)
+    for B, T, filt in ((13, 17, True), (5, 9, False), (301, 90, True), (517, 130, False), (900, 200, True)):
+        obs = np.stack([rng.integers(-1, m.card(v), size=(B, T)) for v in ov], axis=2).astype(np.int32)
+        post, ll, st, _ = both(m, obs, ov, q, filt)
+        assert not st.any()
+        assert np.abs(post.sum(-1) - 1).max() < 1e-12
+
+
 def interface_queries(m, query):
     out = m.desc()["outgoing"]
     return [v for v in query if v in out]
