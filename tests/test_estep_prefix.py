@@ -155,3 +155,14 @@ def test_prefix_verdict_on_a_wide_clique_model():
     k = m.estep_prefix_first_bad(128)
     assert time.time() - t0 < 30
     assert k >= -1                          # simulated, not skipped (-2)
+
+
+def test_prefix_verdict_matches_wide64_golden():
+    """Config 5's structure at 64 states (16.8M join-tree entries, skipped by
+    the simulation before round 4): the predicted BAD_LUCK flags equal the
+    reference's own e_step flags on gappy series (tests/golden/
+    wide64_prefix.npz, made by make_golden_wide_prefix.py from oracle/_ref)."""
+    z = np.load(os.path.join(GOLD, "wide64_prefix.npz"))
+    m = nip_amd.Model.from_spec(*synth.wide_spec(64, 16))
+    assert np.array_equal(predicted(m, z["obs"]), z["bad"] != 0)
+    assert (z["bad"] != 0).any()            # the reference does reject some of them
