@@ -234,10 +234,14 @@ int nipamd_estep_host(nipamd_model* m, const int32_t* obs, int n_obs,
  *                         the whole batch.
  *   nipamd_estep_finalize d_counts += the e_step families of a partial
  *                         (synchronises the stream to read the route tag).
- * A partial ends in two tag slots counting the partials summed into it per
- * kernel route (the route depends on the engine setting and on T); the
- * finalize fails with NIP_ERROR_INVALID_ARGUMENT on partials of different
- * routes combined, instead of summing mismatched layouts.
+ * A partial ends in three tag slots counting the partials summed into it per
+ * kernel route (16-state chain slab, em_learn layout, wide chain slab; the
+ * route depends on the engine setting and on T); the finalize fails with
+ * NIP_ERROR_INVALID_ARGUMENT on partials of different routes combined,
+ * instead of summing mismatched layouts.  nipamd_estep_partial requires
+ * d_status (NIP_ERROR_INVALID_ARGUMENT otherwise) when the model's e_step
+ * rejects series with a long leading missing run
+ * (nipamd_estep_prefix_first_bad >= 0): the verdict is reported there.
  */
 int nipamd_estep_partial_size(const nipamd_model* m);
 int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,

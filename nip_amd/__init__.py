@@ -231,7 +231,7 @@ class Model:
 
     def partial_size(self) -> int:
         """Doubles in an e_step partial (nipamd_estep_partial_size): the count
-        body plus the 2-slot route tag; -1 without an e_step plan."""
+        body plus the 3-slot route tag; -1 without an e_step plan."""
         return lib().nipamd_estep_partial_size(self._h)
 
     def estep_prefix_first_bad(self, T: int) -> int:

@@ -221,6 +221,46 @@ int generate_launch(const GenArgs& a, hipStream_t stream);
 // win [B][31] from qd_base = {x^D mod (x^31 - x^28 - 1) [31], r[313..373] [61]}
 int rand_window_launch(int B, const uint32_t* qd_base, uint32_t* win, hipStream_t stream);
 
+// e_step of interface chains up to 64 states (estep_wide.hip): the two
+// filters store every message (chain_msgs_kernel), then the xi sums, the
+// children's count tables and P0 per 16-sequence block on the matrix cores
+// (chain_stats_kernel), one slab row per block:
+//   K [NP][NP] (xi sums without the transition factor), H [R][NP] (every
+//   plan child's rows M_k + 2, concatenated), P0 [NP];  NP = 16, 32 or 64
+struct EWideArgs {
+  const int* obs;        // int32 observations [B][T][n_obs]
+  long obs_bstride;
+  int obs_tstride;
+  int ncol;              // observed children (their evidence)
+  int col[4];            // their columns in obs
+  int M[4];
+  const double* tab;     // [(M_k + 2)][64] per observed child, concatenated
+  int tab_off[4];        // doubles: child column k's table within tab
+  const double* ebase;   // [64] the unobserved children's row sums
+  const double* s;       // [64] m1 weights: every child's row sum
+  const double* A;       // [64][64]
+  const double* pi;      // [64]
+  long B;
+  int T, N;
+  double* Sa;            // [B][T][NP] alpha^_t
+  double* Sb;            // [B][T + 1][NP] beta^_{t-1} at row t
+  int* Ea;               // [B][T] exponent of alpha^_t
+  double* ll;
+  unsigned* status;
+  double* slab;          // [ceil(B / 16)][slab_size]
+  int slab_size;
+  int R;                 // count-table rows: sum over the plan's children of M_k + 2
+  int nchild;            // the plan's leaf children (count tables)
+  int ccol[4];           // their columns in obs, or -1 (never observed: always missing)
+  int cM[4];
+  int erow[4];           // first count-table row of each
+};
+int estep_wide_np(int N);
+int estep_wide_slab(int N, int R);
+bool estep_wide_fits(int N, int R);
+size_t estep_wide_scratch_bytes(int N, long B, int T);
+int estep_wide_launch(const EWideArgs& a, hipStream_t stream);
+
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 4-wave block
@@ -243,8 +283,8 @@ size_t chain_estep16_lds_bytes(int M, int T, int ne);
 size_t chain_estep16_scratch_bytes(long B, int T);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
-// the e_step partial's route tag: tag[0] = a, tag[1] = b
-int estep_tag_launch(double* tag, double a, double b, hipStream_t stream);
+// the e_step partial's route tag: tag[0] = a, tag[1] = b, tag[2] = c
+int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stream);
 // BAD_LUCK for sequences missing every observation at steps 0..first_bad (prefix.cpp)
 int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, uint32_t* status,
                              hipStream_t stream);

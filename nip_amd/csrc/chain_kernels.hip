@@ -963,12 +963,12 @@ int estep_map_finalize_launch(const double* R, int n, const int* ptr, const int*
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-__global__ void estep_tag_kernel(double* tag, double a, double b) {
-  if (threadIdx.x == 0) { tag[0] = a; tag[1] = b; }
+__global__ void estep_tag_kernel(double* tag, double a, double b, double c) {
+  if (threadIdx.x == 0) { tag[0] = a; tag[1] = b; tag[2] = c; }
 }
 
-int estep_tag_launch(double* tag, double a, double b, hipStream_t stream) {
-  hipLaunchKernelGGL(estep_tag_kernel, dim3(1), dim3(64), 0, stream, tag, a, b);
+int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stream) {
+  hipLaunchKernelGGL(estep_tag_kernel, dim3(1), dim3(64), 0, stream, tag, a, b, c);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -82,6 +82,7 @@ struct DevState {
   int* jm_idx = nullptr;
   double* jm_coef = nullptr;
   int jm_n = 0;
+  int jm_kind = 0;                // 1 joint map, 2 16-state chain slab, 3 wide chain slab
   // general chain e_step (several leaf children, hidden parents): every
   // child's table, rows M_k + 2 each (E, the row sums, zeros), 16 columns
   double* etab_all = nullptr;
@@ -139,7 +140,7 @@ void free_tables(DevState* d) {
   d->childE.clear();
   d->G.clear();
   dfree(d, d->jm_ptr); dfree(d, d->jm_idx); dfree(d, d->jm_coef);
-  d->jm_ptr = nullptr; d->jm_idx = nullptr; d->jm_coef = nullptr; d->jm_n = 0;
+  d->jm_ptr = nullptr; d->jm_idx = nullptr; d->jm_coef = nullptr; d->jm_n = 0; d->jm_kind = 0;
   dfree(d, d->etab_all);
   d->etab_all = nullptr;
 }
@@ -1211,17 +1212,18 @@ int nipamd_filter_host(nipamd_model* mm, const int32_t* obs, int n_obs, const in
   return fb_host_impl(mm, obs, n_obs, obs_vars, B, T, n_query, query, post, ll, status, true);
 }
 
-// The chain e_step kernel serves the HMM slice with evidence on its child
-// only; every other e_step runs on the general engine, whose partial is the
-// em_learn layout itself.  The partial is [body | route tag]: the body holds
-// either layout (the larger of the two sizes), the two tag slots count the
-// partials summed into it per route -- (1, 0) chain slab, (0, 1) em_learn
-// layout -- so partials of different routes (another T, another engine
-// setting, another rank) that were combined are detected by the finalize
-// instead of being summed silently.
-// A chain plan the general chain e_step takes: one interface variable of at
-// most 16 states, 1..3 leaf children, hidden independent parents (their
-// families follow from the xi sums, ensure_chain_map).
+// The chain e_step kernels serve interface chains with evidence on their
+// leaf children; every other e_step runs on the general engine, whose partial
+// is the em_learn layout itself.  The partial is [body | route tag]: the body
+// holds any layout the model's routes produce (the largest of the sizes), the
+// three tag slots count the partials summed into it per route -- (1, 0, 0)
+// the 16-state chain slab, (0, 1, 0) em_learn layout, (0, 0, 1) the wide
+// chain slab (estep_wide.hip) -- so partials of different routes (another T,
+// another engine setting, another rank) that were combined are detected by
+// the finalize instead of being summed silently.
+// A chain plan the general 16-state chain e_step takes: one interface
+// variable of at most 16 states, 1..3 leaf children, hidden independent
+// parents (their families follow from the xi sums, ensure_chain_map).
 static bool estep_general_plan(const nipamd::ChainPlan& P) {
   return P.valid && !P.joint && !P.hmm && P.N <= 16 && !P.emits.empty() && P.emits.size() <= 3 &&
          !P.fold_gpu;
@@ -1232,26 +1234,38 @@ static int estep_rows(const nipamd::ChainPlan& P) {
   for (const auto& e : P.emits) R += e.M + 2;
   return R;
 }
+static bool chain_map_supported(const nipamd::Model& m);
+// A chain plan the wide chain e_step takes (estep_wide.hip): one interface
+// variable of at most 64 states, 1..4 leaf children, hidden independent
+// parents, in-cliques folded on the GPU (config 3's and config 5's models).
+static bool estep_wide_plan(const nipamd::Model& m) {
+  const auto& P = m.chain;
+  return P.valid && !P.joint && !P.emits.empty() && P.emits.size() <= 4 &&
+         nipamd::estep_wide_fits(P.N, estep_rows(P)) && chain_map_supported(m);
+}
+constexpr int kTagSlots = 3;
 
 // The body is the larger of the layouts this model's routes can produce,
 // whatever the engine setting, so the tag sits at the same offset for every
 // partial of a model version (a set_engine between partial and finalize
 // cannot move it into the counts).
-static bool has_chain_estep(const nipamd::ChainPlan& P) {
-  return P.valid && (P.hmm || P.jhmm || estep_general_plan(P));
+static bool has_chain_estep(const nipamd::Model& m) {
+  const auto& P = m.chain;
+  return P.valid && (P.hmm || P.jhmm || estep_general_plan(P) || estep_wide_plan(m));
 }
 static int estep_body_size(const nipamd_model* mm) {
-  const int ps = nipamd::param_size(mm->m);
+  int body = nipamd::param_size(mm->m);
   const auto& P = mm->m.chain;
-  if (P.valid && (P.hmm || P.jhmm)) return std::max(ps, nipamd::chain_estep_slab(P.emits[0].M));
-  if (estep_general_plan(P)) return std::max(ps, nipamd::chain_estep_slab(estep_rows(P) - 2));
-  return ps;
+  if (P.valid && (P.hmm || P.jhmm)) body = std::max(body, nipamd::chain_estep_slab(P.emits[0].M));
+  if (estep_general_plan(P)) body = std::max(body, nipamd::chain_estep_slab(estep_rows(P) - 2));
+  if (estep_wide_plan(mm->m)) body = std::max(body, nipamd::estep_wide_slab(P.N, estep_rows(P)));
+  return body;
 }
 
 int nipamd_estep_partial_size(const nipamd_model* mm) {
   if (!mm) return -1;
-  if (mm->engine == NIPAMD_ENGINE_CHAIN && !has_chain_estep(mm->m.chain)) return -1;
-  return estep_body_size(mm) + 2;
+  if (mm->engine == NIPAMD_ENGINE_CHAIN && !has_chain_estep(mm->m)) return -1;
+  return estep_body_size(mm) + kTagSlots;
 }
 
 // e_step kernel of the chain route: 3 = chain_estep16_kernel (16-lane DPP
@@ -1285,6 +1299,16 @@ static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_var
     return false;                                  // evidence on the child only
   }
   return chain_estep_kernel(mm, T) != 0;
+}
+
+// the wide chain e_step: evidence on leaf children only
+static bool wide_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, Route& r) {
+  std::string why;
+  const auto& P = mm->m.chain;
+  if (mm->engine == NIPAMD_ENGINE_JTREE || !estep_wide_plan(mm->m)) return false;
+  if (!route_request(mm, n_obs, obs_vars, 0, nullptr, r, why)) return false;
+  for (int i = 0; i < r.ncol; i++) if (r.emit[i] >= (int)P.emits.size()) return false;
+  return true;
 }
 
 // The reference's verdict on a leading run of missing observations
@@ -1357,18 +1381,96 @@ int nipamd_estep_prefix_first_bad(nipamd_model* mm, int T) {
   return prefix_first_bad(mm, T);
 }
 
+// The wide chain e_step (estep_wide.hip): the filters store every message of
+// a chunk of sequences, the statistics kernel writes one slab row per 16
+// sequences, and the fixed-order tree sums the rows (per chunk, then over
+// the chunks) into the partial.
+static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d_obs, int n_obs, int B, int T,
+                              double* d_partial, double* d_ll, uint32_t* d_status, void* stream) {
+  const auto& P = mm->m.chain;
+  const int R = estep_rows(P);
+  const int S = nipamd::estep_wide_slab(P.N, R);
+  hipStream_t st = (hipStream_t)stream;
+  if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 0.0, 1.0, st))
+    return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
+  if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
+  if (int rc = ensure_tables(mm)) return rc;
+  ReqTables* rt = nullptr;
+  if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
+  // sequences per launch: the messages of a chunk stay within ~4 GB of HBM
+  const size_t per_seq = nipamd::estep_wide_scratch_bytes(P.N, 1, T);
+  long chunk = (long)std::min<size_t>(kEstepChunk, std::max<size_t>(16, ((size_t)4 << 30) / per_seq));
+  chunk = std::max(16L, chunk / 16 * 16);
+  if (B < chunk) chunk = B;
+  const long nchunks = (B + chunk - 1) / chunk;
+  const long rows = (chunk + 15) / 16;
+  const long lvl = (rows + 63) / 64;
+  const size_t work = ((size_t)rows + 2 * lvl + nchunks + 64) * S * sizeof(double);
+  if (int rc = ensure_scratch(mm, nipamd::estep_wide_scratch_bytes(P.N, chunk, T))) return rc;
+  if (int rc = ensure_work(mm, work)) return rc;
+  DevState* d = dev_of(mm);
+  const int NP = nipamd::estep_wide_np(P.N);
+  double* slab = d->W;
+  double* tA = slab + (size_t)rows * S;
+  double* tB = tA + (size_t)lvl * S;
+  double* cres = tB + (size_t)lvl * S;
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  for (long c = 0; c < nchunks; c++) {
+    const long b0 = c * chunk;
+    const long nb = (B - b0) < chunk ? (B - b0) : chunk;
+    nipamd::EWideArgs a{};
+    a.obs = d_obs ? d_obs + b0 * T * ocols : nullptr;
+    a.obs_bstride = (long)T * ocols;
+    a.obs_tstride = (int)ocols;
+    a.ncol = r.ncol;
+    for (int i = 0; i < r.ncol; i++) {
+      a.col[i] = r.col[i];
+      a.M[i] = P.emit(r.emit[i]).M;
+      a.tab_off[i] = (int)rt->tabw_off[i];
+    }
+    a.tab = rt->tabw; a.ebase = rt->ebase; a.s = d->sall64; a.A = d->A64; a.pi = d->pi64;
+    a.B = nb; a.T = T; a.N = P.N;
+    a.Sa = d->S;
+    a.Sb = a.Sa + (size_t)chunk * T * NP;
+    a.Ea = reinterpret_cast<int*>(a.Sb + (size_t)chunk * (T + 1) * NP);
+    a.ll = d_ll ? d_ll + b0 : nullptr;
+    a.status = d_status ? d_status + b0 : nullptr;
+    a.slab = slab; a.slab_size = S; a.R = R;
+    a.nchild = (int)P.emits.size();
+    for (int k = 0, row = 0; k < a.nchild; k++) {
+      a.ccol[k] = -1;
+      for (int i = 0; i < r.ncol; i++) if (r.emit[i] == k) a.ccol[k] = r.col[i];
+      a.cM[k] = P.emits[k].M;
+      a.erow[k] = row;
+      row += P.emits[k].M + 2;
+    }
+    const int lrc = nipamd::estep_wide_launch(a, st);
+    if (lrc == -2) return fail(NIPAMD_ERROR_UNSUPPORTED, "wide chain e_step: the count tables do not fit the kernel");
+    if (lrc) return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
+    if (reduce_rows(slab, (nb + 15) / 16, S, tA, tB, out, st))
+      return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
+  }
+  if (nchunks > 1 && reduce_rows(cres, nchunks, S, tA, tB, d_partial, st))
+    return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
+  return 0;
+}
+
 static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                                 int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
                                 void* stream) {
   Route r;
   if (!chain_estep_ok(mm, n_obs, obs_vars, T, r)) {
+    Route rw;
+    if (wide_estep_ok(mm, n_obs, obs_vars, rw))
+      return estep_wide_partial(mm, rw, d_obs, n_obs, B, T, d_partial, d_ll, d_status, stream);
     if (mm->engine == NIPAMD_ENGINE_CHAIN)
-      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step covers the HMM slice with evidence on its child");
+      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step covers interface chains with evidence on their children");
     std::string why;
     if (!nipamd::jt_supported(mm, n_obs, obs_vars, 0, nullptr, why)) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
     if (int rc = nipamd::jt_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
       return rc;
-    if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 1.0, (hipStream_t)stream))
+    if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 1.0, 0.0, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
     return 0;
   }
@@ -1381,7 +1483,7 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   const bool mfma = ek == 1;
   const int per_row = mfma ? 16 : 1;            // sequences per slab row
   hipStream_t st = (hipStream_t)stream;
-  if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, st))
+  if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, 0.0, st))
     return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   if (int rc = ensure_tables(mm)) return rc;
@@ -1619,136 +1721,213 @@ static int ensure_etab_all(nipamd_model* mm) {
   return upload(d, &d->etab_all, E);
 }
 
-// The general chain e_step's slab (xi sums Kf / Kb without the transition,
-// the children's count tables, the t = 0 posterior P0) projected onto every
+// The general chain e_step's slab (xi sums without the transition, the
+// children's count tables, the t = 0 posterior P0) projected onto every
 // family of the em_learn layout (nip.c:2101-2128: child first, then its
 // parents in v->parents order), as one fixed-order sum per count (CSR):
 //   previous interface variable: P0
 //   interface variable y | x, hidden parents h: in-clique(x, y, h)
-//       x prod_j prior_j(h_j) x (Kf + Kb)(x, y)   (the joint posterior of the
+//       x prod_j prior_j(h_j) x K(x, y)   (the joint posterior of the
 //       in-clique's variables is alpha_{t-1}(x) P(y | x, h) prod prior(h)
-//       e_t(y) beta_t(y) / Z; xi holds everything but the first factors)
+//       e_t(y) beta_t(y) / Z; the xi sums K hold everything but the first factors)
 //   hidden parent h_j: the same summed over everything but h_j
 //   leaf child o_k | y: its count table, a missing observation split as
 //       E_k(y, o) / s_k(y) (the child's posterior given y)
-static int ensure_chain_map(nipamd_model* mm) {
+// Two slab layouts: the 16-state kernels' (Kf and Kb, two count tables, row
+// stride 16) and estep_wide.hip's (one K, one table, row stride NP).  Built
+// as (row, slab index, coefficient) triples in a fixed generation order, then
+// grouped by row with a stable counting sort: the in-clique of config 5 has
+// 16.7M entries, one CSR row each.
+// the cached slab -> em_learn map serves one slab layout: drop it when a
+// partial of another layout comes to be finalized
+static int ensure_map_kind(nipamd_model* mm, int kind) {
+  DevState* d = dev_of(mm);
+  if (d->jm_ptr && d->jm_kind != kind) {
+    HIP_OK(hipDeviceSynchronize());
+    dfree(d, d->jm_ptr); dfree(d, d->jm_idx); dfree(d, d->jm_coef);
+    d->jm_ptr = nullptr; d->jm_idx = nullptr; d->jm_coef = nullptr; d->jm_n = 0;
+  }
+  d->jm_kind = kind;
+  return 0;
+}
+
+struct SlabLayout {
+  int ns;          // row stride of K and H
+  int kf, kb;      // K sums (kb < 0: one sum)
+  int hf, hb;      // count tables (hb < 0: one table)
+  int p0;
+};
+
+// the projection's structural preconditions (ensure_chain_map's checks)
+static bool chain_map_supported(const nipamd::Model& m) {
+  const auto& P = m.chain;
+  if (!P.valid || P.joint || P.c_trans < 0) return false;
+  for (int v : m.cliques[P.c_trans].vars)
+    if (v != P.v_prev && v != P.v_cur && std::find(P.hidden.begin(), P.hidden.end(), v) == P.hidden.end())
+      return false;
+  if (!m.vars[P.v_prev].parents.empty()) return false;
+  for (const auto& E : P.emits) {
+    const auto& Vo = m.vars[E.var];
+    if (Vo.parents.size() != 1 || Vo.parents[0] != P.v_cur) return false;
+  }
+  for (int v = 0; v < (int)m.vars.size(); v++) {
+    const bool known = v == P.v_prev || v == P.v_cur ||
+                       std::find(P.hidden.begin(), P.hidden.end(), v) != P.hidden.end() ||
+                       std::any_of(P.emits.begin(), P.emits.end(), [&](const nipamd::ChainEmit& e) { return e.var == v; });
+    if (!known) return false;
+  }
+  return true;
+}
+
+static int ensure_chain_map(nipamd_model* mm, const SlabLayout& L) {
   DevState* d = dev_of(mm);
   if (d->jm_ptr) return 0;
   const nipamd::Model& m = mm->m;
+  if (!chain_map_supported(m)) return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: slice outside the chain plan");
   const auto& P = m.chain;
-  const int nv = (int)m.vars.size(), N = P.N, R = estep_rows(P);
-  const int Kb = nipamd::kSlabKb, Hf = nipamd::kSlabH, Hb = nipamd::kSlabH + R * 16;
-  const int p0 = nipamd::chain_slab_p0(R - 2);
-  std::vector<int> off(nv + 1, 0);
+  const int nv = (int)m.vars.size(), N = P.N;
+  std::vector<long> off(nv + 1, 0);
   for (int v = 0; v < nv; v++) {
-    int sz = m.vars[v].card;
+    long sz = m.vars[v].card;
     for (int q : m.vars[v].parents) sz *= m.vars[q].card;
     off[v + 1] = off[v] + sz;
   }
-  std::vector<std::vector<std::pair<int, double>>> rows(off[nv]);
+  struct Ent { long row; int idx; double coef; };
+  std::vector<Ent> ents;
+  auto kidx = [&](int base, int x, int y) { return base + x * L.ns + y; };
   // the in-clique's entries: (x, y, hidden values) -> coefficient
   const auto& cin = m.cliques[P.c_trans];
-  std::vector<long> stride(cin.vars.size());
+  const size_t nc = cin.vars.size();
   long total = 1;
-  for (size_t i = 0; i < cin.vars.size(); i++) { stride[i] = total; total *= m.vars[cin.vars[i]].card; }
-  for (int v : cin.vars)
-    if (v != P.v_prev && v != P.v_cur && std::find(P.hidden.begin(), P.hidden.end(), v) == P.hidden.end())
-      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: in-clique variable outside the plan");
+  for (size_t i = 0; i < nc; i++) total *= m.vars[cin.vars[i]].card;
+  ents.reserve((size_t)total * (L.kb >= 0 ? 2 : 1) + 4096);
+  const int nh = (int)P.hidden.size();
+  // hidden parent j, value d: sum over the in-clique entries of each (x, y),
+  // in entry order, and the order in which the (x, y) first occur
+  std::vector<std::vector<double>> hacc(nh);
+  std::vector<std::vector<char>> hseen(nh);
+  std::vector<std::vector<std::vector<int>>> horder(nh);
+  for (int j = 0; j < nh; j++) {
+    const int c = m.vars[P.hidden[j]].card;
+    hacc[j].assign((size_t)c * N * N, 0.0);
+    hseen[j].assign((size_t)c * N * N, 0);
+    horder[j].resize(c);
+  }
   std::vector<int> val(nv, 0);
   const auto& Vc = m.vars[P.v_cur];
+  std::vector<int> cardc(nc);
+  for (size_t k = 0; k < nc; k++) cardc[k] = m.vars[cin.vars[k]].card;
+  std::vector<int> digit(nc, 0);
   for (long i = 0; i < total; i++) {
-    long r = i;
-    for (size_t k = 0; k < cin.vars.size(); k++) {
-      const int v = cin.vars[k];
-      val[v] = (int)(r % m.vars[v].card);
-      r /= m.vars[v].card;
-    }
+    for (size_t k = 0; k < nc; k++) val[cin.vars[k]] = digit[k];
     double coef = cin.original[(size_t)i];
     for (int h : P.hidden) coef *= m.vars[h].prior[val[h]];
     const int x = val[P.v_prev], y = val[P.v_cur];
     // the interface variable's family: y first, then its parents in order
     long idx = y, st = Vc.card;
     for (int q : Vc.parents) { idx += (long)val[q] * st; st *= m.vars[q].card; }
-    rows[off[P.v_cur] + idx].push_back({x * 16 + y, coef});
-    rows[off[P.v_cur] + idx].push_back({Kb + x * 16 + y, coef});
-    for (int h : P.hidden) {
-      auto& row = rows[off[h] + val[h]];
-      bool merged = false;                       // one coefficient per (x, y): summed in entry order
-      for (auto& e : row)
-        if (e.first == x * 16 + y) { e.second += coef; merged = true; }
-      if (!merged) row.push_back({x * 16 + y, coef});
+    ents.push_back({off[P.v_cur] + idx, kidx(L.kf, x, y), coef});
+    if (L.kb >= 0) ents.push_back({off[P.v_cur] + idx, kidx(L.kb, x, y), coef});
+    for (int j = 0; j < nh; j++) {
+      const int dv = val[P.hidden[j]];
+      const size_t c = ((size_t)dv * N + x) * N + y;
+      if (!hseen[j][c]) { hseen[j][c] = 1; horder[j][dv].push_back(x * N + y); }
+      hacc[j][c] += coef;
+    }
+    for (size_t k = 0; k < nc; k++) {                     // odometer, dimension 0 fastest
+      if (++digit[k] < cardc[k]) break;
+      digit[k] = 0;
     }
   }
-  for (int h : P.hidden) {
-    for (int d2 = 0; d2 < m.vars[h].card; d2++) {
-      auto& rw = rows[off[h] + d2];
-      const size_t n = rw.size();
-      for (size_t e = 0; e < n; e++) rw.push_back({Kb + rw[e].first, rw[e].second});
+  for (int j = 0; j < nh; j++) {
+    const int h = P.hidden[j];
+    for (int dv = 0; dv < m.vars[h].card; dv++) {
+      for (int xy : horder[j][dv])
+        ents.push_back({off[h] + dv, kidx(L.kf, xy / N, xy % N), hacc[j][((size_t)dv * N) * N + xy]});
+      if (L.kb >= 0)
+        for (int xy : horder[j][dv])
+          ents.push_back({off[h] + dv, kidx(L.kb, xy / N, xy % N), hacc[j][((size_t)dv * N) * N + xy]});
     }
   }
-  if (!m.vars[P.v_prev].parents.empty()) return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: prev with parents");
-  for (int x = 0; x < N; x++) rows[off[P.v_prev] + x].push_back({p0 + x, 1.0});
+  for (int x = 0; x < N; x++) ents.push_back({off[P.v_prev] + x, L.p0 + x, 1.0});
   for (size_t k = 0, row0 = 0; k < P.emits.size(); k++) {
     const auto& E = P.emits[k];
-    const auto& Vo = m.vars[E.var];
-    if (Vo.parents.size() != 1 || Vo.parents[0] != P.v_cur)
-      return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: a child with parents besides the interface");
     for (int y = 0; y < N; y++)
       for (int o = 0; o < E.M; o++) {
-        auto& rw = rows[off[E.var] + o + E.M * y];
-        rw.push_back({Hf + (int)(row0 + o) * 16 + y, 1.0});
-        rw.push_back({Hb + (int)(row0 + o) * 16 + y, 1.0});
-        if (E.s[y] != 0.0) {
+        const long r = off[E.var] + o + (long)E.M * y;
+        ents.push_back({r, L.hf + (int)(row0 + o) * L.ns + y, 1.0});
+        if (L.hb >= 0) ents.push_back({r, L.hb + (int)(row0 + o) * L.ns + y, 1.0});
+        if (E.s[y] != 0.0) {                   // missing observations, split as E(y, o) / s(y)
           const double w = E.E[(size_t)o * 64 + y] / E.s[y];
-          rw.push_back({Hf + (int)(row0 + E.M) * 16 + y, w});
-          rw.push_back({Hb + (int)(row0 + E.M) * 16 + y, w});
+          ents.push_back({r, L.hf + (int)(row0 + E.M) * L.ns + y, w});
+          if (L.hb >= 0) ents.push_back({r, L.hb + (int)(row0 + E.M) * L.ns + y, w});
         }
       }
     row0 += E.M + 2;
   }
-  // every variable must be one of the plan's
-  for (int v = 0; v < nv; v++) {
-    const bool known = v == P.v_prev || v == P.v_cur ||
-                       std::find(P.hidden.begin(), P.hidden.end(), v) != P.hidden.end() ||
-                       std::any_of(P.emits.begin(), P.emits.end(), [&](const nipamd::ChainEmit& e) { return e.var == v; });
-    if (!known) return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: variable outside the chain plan");
-  }
-  std::vector<int> ptr{0}, idx;
-  std::vector<double> coef;
-  for (const auto& r : rows) {
-    for (const auto& e : r) { idx.push_back(e.first); coef.push_back(e.second); }
-    ptr.push_back((int)idx.size());
+  // CSR by a stable counting sort on the row
+  const long nrows = off[nv];
+  if ((long)ents.size() >= (1L << 31) || nrows >= (1L << 31))
+    return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step: projection beyond 2^31 entries");
+  std::vector<int> ptr((size_t)nrows + 1, 0);
+  for (const Ent& e : ents) ptr[(size_t)e.row + 1]++;
+  for (long r = 0; r < nrows; r++) ptr[(size_t)r + 1] += ptr[(size_t)r];
+  std::vector<int> fill(ptr.begin(), ptr.end() - 1), idx(ents.size());
+  std::vector<double> coef(ents.size());
+  for (const Ent& e : ents) {
+    const int q = fill[(size_t)e.row]++;
+    idx[(size_t)q] = e.idx;
+    coef[(size_t)q] = e.coef;
   }
   HIP_OK(hipMalloc(&d->jm_ptr, ptr.size() * sizeof(int)));
   HIP_OK(hipMemcpy(d->jm_ptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice));
   HIP_OK(hipMalloc(&d->jm_idx, std::max<size_t>(1, idx.size()) * sizeof(int)));
   if (!idx.empty()) HIP_OK(hipMemcpy(d->jm_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
   if (int rc = upload(d, &d->jm_coef, coef)) return rc;
-  d->jm_n = off[nv];
+  d->jm_n = (int)nrows;
   return 0;
 }
 
 int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_counts, void* stream) {
   if (!mm || !d_partial || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   const int body = estep_body_size(mm);
-  // the route tag (see nipamd_estep_partial_size): one 16-byte read, once per EM iteration
-  double tag[2] = {0.0, 0.0};
+  // the route tag (see nipamd_estep_partial_size): one 24-byte read, once per EM iteration
+  double tag[kTagSlots] = {0.0, 0.0, 0.0};
   HIP_OK(hipMemcpyAsync(tag, d_partial + body, sizeof(tag), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_OK(hipStreamSynchronize((hipStream_t)stream));
-  if (!(tag[0] >= 1.0 && tag[1] == 0.0) && !(tag[1] >= 1.0 && tag[0] == 0.0))
+  int route = -1, nz = 0;
+  for (int k = 0; k < kTagSlots; k++)
+    if (tag[k] != 0.0) { nz++; if (tag[k] >= 1.0) route = k; }
+  if (nz != 1 || route < 0)
     return fail(NIP_ERROR_INVALID_ARGUMENT, "e_step partial: partials of different routes (chain slab / em_learn "
-                                            "layout) were combined, or the buffer is not an e_step partial");
-  if (tag[1] >= 1.0) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
+                                            "layout / wide chain slab) were combined, or the buffer is not an "
+                                            "e_step partial");
+  if (route == 1) return nipamd::jt_estep_finalize(mm, d_partial, d_counts, stream);
   const auto& P = mm->m.chain;
-  if (!has_chain_estep(P)) return fail(NIPAMD_ERROR_UNSUPPORTED, "batched e_step GPU plan covers the HMM slice");
+  if (!has_chain_estep(mm->m)) return fail(NIPAMD_ERROR_UNSUPPORTED, "no chain e_step plan for this model");
   if (int rc = ensure_tables(mm)) return rc;
+  DevState* d = dev_of(mm);
+  if (route == 2) {
+    if (!estep_wide_plan(mm->m)) return fail(NIPAMD_ERROR_UNSUPPORTED, "no wide chain e_step plan for this model");
+    const int NP = nipamd::estep_wide_np(P.N), R = estep_rows(P);
+    const SlabLayout L{NP, 0, -1, NP * NP, -1, NP * NP + R * NP};
+    if (int rc = ensure_map_kind(mm, 3)) return rc;
+    if (int rc = ensure_chain_map(mm, L)) return rc;
+    if (nipamd::estep_map_finalize_launch(d_partial, d->jm_n, d->jm_ptr, d->jm_idx, d->jm_coef, d_counts,
+                                          (hipStream_t)stream))
+      return fail(NIPAMD_ERROR_DEVICE, "finalize launch failed");
+    return 0;
+  }
   Route rh;
   rh.primary = 0;
   ReqTables* rt = nullptr;
   if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
-  DevState* d = dev_of(mm);
   if (P.jhmm || !P.hmm) {
-    if (int rc = P.jhmm ? ensure_joint_map(mm) : ensure_chain_map(mm)) return rc;
+    const int R = estep_rows(P);
+    const SlabLayout L{16, nipamd::kSlabKf, nipamd::kSlabKb, nipamd::kSlabH, nipamd::kSlabH + R * 16,
+                       nipamd::chain_slab_p0(R - 2)};
+    if (int rc = ensure_map_kind(mm, P.jhmm ? 1 : 2)) return rc;
+    if (int rc = P.jhmm ? ensure_joint_map(mm) : ensure_chain_map(mm, L)) return rc;
     if (nipamd::estep_map_finalize_launch(d_partial, d->jm_n, d->jm_ptr, d->jm_idx, d->jm_coef, d_counts,
                                           (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, "finalize launch failed");

@@ -1,0 +1,409 @@
+// estep_wide.hip -- e_step for interface chains of up to 64 states (the chain
+// plans of SURVEY 8(d) configs 3 and 5: demo1's structure at 32 states, the
+// 64^4 wide clique after its GPU fold), any number of hidden independent
+// parents, up to four leaf children.
+//
+// The reference's e_step (src/nip.c:1708-2007, families nip.c:1925-1967)
+// sums, per sequence and step, the normalised family marginals of every
+// variable.  For an interface chain they all follow from three sums
+// (the general chain e_step):
+//   K(x, y)   = sum_t alpha_{t-1}(x) e_t(y) beta_t(y) / Z_t   (the in-clique's
+//               joint posterior without its table factor; alpha_{-1} = prior)
+//   H[r][y]   = sum_t [r = row of child k's code at t] gamma_t(y)   (the
+//               children's count tables, one row per state + missing + zero)
+//   P0(x)     = gamma_{-1}(x) = prior(x) beta_{-1}(x) / Z   (the previous
+//               interface at t = 0; OLD_OUTGOING is skipped at t > 0)
+// and the finalize projects them onto the em_learn layout (a CSR map built
+// once per model version, engine.cpp ensure_chain_map).
+//
+// Two kernels:
+//  * chain_msgs_kernel<NP>: the two filters, every message stored.  One wave
+//    per direction holds 64 / NP sequences, lane = state; the mat-vec reads
+//    the input by LDS broadcast against the lane's column (forward) or row
+//    (backward) of A in registers.  alpha^_t = alpha_t 2^Ef_t (Ef_t stored,
+//    one int per step) and beta^_t (t = -1 .. T-1, scale free for the
+//    statistics) go to HBM; the forward wave keeps the ll (m2 / m1 per step,
+//    nip.c:1461-1474) as chain_wide.hip does.
+//  * chain_stats_kernel<NT, HR>: the three sums on the matrix cores.  With
+//    c_t = sum_y alpha^_t(y) beta^_t(y) and w_t(y) = e_t(y) beta^_t(y)
+//    2^(Ef_t - Ef_{t-1}) / c_t (the 2^Ef factors cancel the scales of the
+//    stored messages), K = sum_t alpha^_{t-1} (x) w_t is a GEMM whose inner
+//    dimension is time: one v_mfma_f64_16x16x4 per 16x16 tile and four steps
+//    (lane l: step l >> 4, state 16 tile + (l & 15)).  H is the same GEMM with
+//    a one-hot A operand (row = child code) against gamma_t = alpha^ beta^ / c.
+//    A block of four waves owns 16 sequences (four per wave, one after
+//    another); the waves' sums meet in LDS in a fixed order and the block
+//    writes one slab row, which tree64_kernel reduces like every e_step slab.
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cstdint>
+
+#include "chain_kernels.h"
+
+namespace nipamd {
+
+namespace {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+constexpr int kMsgWaves = 8;                 // 4 forward + 4 backward
+constexpr int kMsgChunk = 8;                 // steps of evidence prefetched ahead
+constexpr int kStatSeqs = 16;                // sequences per stats block (one slab row)
+constexpr int kStatWaves = 4;
+
+template <int K>
+__device__ __forceinline__ double rorK(double v) {     // row_ror:K of a double (16-lane rows)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x120 + K, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x120 + K, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double swap16(double x) {   // x[l ^ 16] + x[l] in both lanes: the pair's sum
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+__device__ __forceinline__ double swap32(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+// sum over aligned groups of L lanes (16, 32 or 64); every level pairs equal
+// partial sums, so all L lanes end with the same bits
+template <int L>
+__device__ __forceinline__ double group_sum(double x) {
+  asm("" : "+v"(x));       // one rounded value per lane: no fma contraction into the first add
+  x += rorK<8>(x);
+  x += rorK<4>(x);
+  x += rorK<2>(x);
+  x += rorK<1>(x);
+  if (L >= 32) x = swap16(x);
+  if (L >= 64) x = swap32(x);
+  return x;
+}
+
+__device__ __forceinline__ double recip(double c) {
+  double r = __builtin_amdgcn_rcp(c);
+  r = __builtin_fma(r, __builtin_fma(-c, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-c, r, 1.0), r);
+  return c != 0.0 ? r : 0.0;
+}
+
+// child c's code at step t: its state, M missing, M + 1 out of range
+__device__ __forceinline__ int code_of(int o, int M) { return o < 0 ? M : (o < M ? o : M + 1); }
+
+// the step's evidence e_t(y): the unobserved children's row sums times each
+// observed child's table row
+__device__ __forceinline__ double evidence(const EWideArgs& a, const int* o, int y) {
+  double e = a.ebase[y];
+  for (int c = 0; c < a.ncol; c++) e *= a.tab[a.tab_off[c] + code_of(o[a.col[c]], a.M[c]) * 64 + y];
+  return e;
+}
+
+template <int NP>
+__global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a) {
+  constexpr int SPW = 64 / NP;                        // sequences per wave
+  __shared__ __attribute__((aligned(16))) double xbuf[kMsgWaves][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool fwd = wave < 4;
+  const int s = lane / NP, y = lane % NP;
+  const long b = (long)blockIdx.x * (4 * SPW) + (wave & 3) * SPW + s;
+  const bool active = b < a.B;
+  const long bb = active ? b : 0;
+  const int T = a.T, N = a.N;
+  double* const xb = xbuf[wave];
+  double Acol[NP];
+#pragma unroll
+  for (int x = 0; x < NP; x++) Acol[x] = (x < N && y < N) ? (fwd ? a.A[x * 64 + y] : a.A[y * 64 + x]) : 0.0;
+  const int* obs = a.obs + bb * a.obs_bstride;
+  auto ev = [&](int t) {
+    if (!active || y >= N) return 0.0;
+    return evidence(a, obs + (long)t * a.obs_tstride, y);
+  };
+  // u = sum_x Acol[x] xb[x] over this sequence's NP lanes of the LDS buffer
+  auto matvec = [&](double v) {
+    xb[lane] = v;
+    __builtin_amdgcn_wave_barrier();
+    const double* q = xb + s * NP;
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int x = 0; x < NP; x += 2) {
+      const double2 w = *reinterpret_cast<const double2*>(q + x);
+      a0 = __builtin_fma(Acol[x], w.x, a0);
+      a1 = __builtin_fma(Acol[x + 1], w.y, a1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return a0 + a1;
+  };
+  double e[kMsgChunk], en[kMsgChunk];
+  if (fwd) {
+    double* Sa = a.Sa + (size_t)bb * T * NP + y;
+    int* Ea = a.Ea + (size_t)bb * T;
+    double x = (active && y < N) ? a.pi[y] : 0.0;
+    const double sy = y < N ? a.s[y] : 0.0;
+    int sc = 0, E = 0;
+    double m2 = 1.0, m1 = 1.0, zmin = 1.0;
+    int e2 = 0, e1 = 0;
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) e[k] = k < T ? ev(k) : 0.0;
+    for (int t0 = 0; t0 < T; t0 += kMsgChunk) {
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) en[k] = t0 + kMsgChunk + k < T ? ev(t0 + kMsgChunk + k) : 0.0;
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) {
+        const int t = t0 + k;
+        if (t >= T) break;
+        const double u = __builtin_ldexp(matvec(x), sc);
+        const double p = u * e[k];
+        const double z2 = group_sum<NP>(p);
+        const double z1 = group_sum<NP>(u * sy);
+        E += sc;
+        if (active) {
+          Sa[(size_t)t * NP] = p;
+          if (y == 0) Ea[t] = E;
+        }
+        zmin = __builtin_fmin(zmin, z2);
+        m2 *= z2; m1 *= z1;
+        if ((k & 3) == 3) {
+          const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+          const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+        }
+        sc = z2 != 0.0 ? -__builtin_amdgcn_frexp_exp(z2) : 0;
+        x = p;
+      }
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) e[k] = en[k];
+    }
+    if (active && y == 0) {
+      double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+      const bool dead = zmin == 0.0;
+      if (dead) ll = -DBL_MAX;
+      if (a.ll) a.ll[b] = ll;
+      // e_step's BAD_LUCK (m1 <= 0 || m2 <= 0, nip.c:1827-1854): a zero mass
+      if (a.status) a.status[b] = dead ? 3u : 0u;
+    }
+  } else {
+    // beta^_{T-1} = 1 at row T, then beta^_{t-1} = A (e_t o beta^_t) 2^sc at row t
+    double* Sb = a.Sb + (size_t)bb * (T + 1) * NP + y;
+    double xbeta = (active && y < N) ? 1.0 : 0.0;
+    if (active) Sb[(size_t)T * NP] = xbeta;
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) e[k] = T - 1 - k >= 0 ? ev(T - 1 - k) : 0.0;
+    for (int j0 = 0; j0 < T; j0 += kMsgChunk) {
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) {
+        const int t = T - 1 - (j0 + kMsgChunk + k);
+        en[k] = t >= 0 ? ev(t) : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) {
+        const int t = T - 1 - (j0 + k);
+        if (t < 0) break;
+        const double g = e[k] * xbeta;
+        const double z = group_sum<NP>(g);
+        const int sc = z != 0.0 ? -__builtin_amdgcn_frexp_exp(z) : 0;
+        const double u = __builtin_ldexp(matvec(g), sc);
+        if (active) Sb[(size_t)t * NP] = u;
+        xbeta = u;
+      }
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) e[k] = en[k];
+    }
+  }
+}
+
+// One 16x16x4 f64 MFMA: D += A (16 x 4) B (4 x 16); lane l supplies
+// A[l & 15][l >> 4] and B[l >> 4][l & 15], and holds D[(l >> 4) + 4 r][l & 15].
+__device__ __forceinline__ v4d mfma(double a, double b, v4d d) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
+}
+
+template <int NT, int HR>
+__global__ __launch_bounds__(kStatWaves * 64, 1) void chain_stats_kernel(EWideArgs a) {
+  constexpr int NP = 16 * NT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* red = reinterpret_cast<double*>(smem);     // [2][NT*NT + HR*NT][4][64]: the waves' sums
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k4 = lane >> 4, i = lane & 15;
+  const int T = a.T, N = a.N;
+  constexpr int NK = NT * NT, NH = HR * NT;
+  v4d K[NK], Hc[NH];
+#pragma unroll
+  for (int q = 0; q < NK; q++) K[q] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < NH; q++) Hc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+  double p0 = 0.0;                                   // P0 of state `lane` (lane < NP)
+  const int hr = (a.R + 15) >> 4;                    // row tiles in use (<= HR)
+
+  for (int sq = 0; sq < kStatSeqs / kStatWaves; sq++) {
+    const long b = (long)blockIdx.x * kStatSeqs + wave * (kStatSeqs / kStatWaves) + sq;
+    if (b >= a.B) break;                             // wave-uniform
+    const double* Sa = a.Sa + (size_t)b * T * NP;
+    const double* Sb = a.Sb + (size_t)b * (T + 1) * NP;
+    const int* Ea = a.Ea + (size_t)b * T;
+    const int* obs = a.obs + b * a.obs_bstride;
+    // P0: gamma_{-1} = prior o beta^_{-1} / its sum (lanes 0 .. NP-1: state = lane)
+    {
+      const int x = lane < NP ? lane : 0;
+      const double v = (lane < NP && x < N) ? a.pi[x] * Sb[x] : 0.0;
+      const double z = group_sum<64>(v);
+      p0 += v * recip(z);
+    }
+    for (int t0 = 0; t0 < T; t0 += 4) {
+      const int t = t0 + k4;
+      const bool ok = t < T;
+      const int tc = ok ? t : T - 1;
+      // operands of this lane's step: alpha^_{t-1} (A of K), alpha^_t, beta^_t
+      double ap[NT], al[NT], be[NT], ev[NT];
+#pragma unroll
+      for (int q = 0; q < NT; q++) {
+        const int st = 16 * q + i;
+        ap[q] = tc >= 1 ? Sa[(size_t)(tc - 1) * NP + st] : (st < N ? a.pi[st] : 0.0);
+        al[q] = Sa[(size_t)tc * NP + st];
+        be[q] = Sb[(size_t)(tc + 1) * NP + st];
+      }
+      const int ef = Ea[tc] - (tc >= 1 ? Ea[tc - 1] : 0);
+      const int* o = obs + (long)tc * a.obs_tstride;
+#pragma unroll
+      for (int q = 0; q < NT; q++) {
+        const int st = 16 * q + i;
+        ev[q] = st < N ? evidence(a, o, st) : 0.0;
+      }
+      // the one-hot rows of the children's codes at t
+      int row[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        row[c] = c < a.nchild ? a.erow[c] + (a.ccol[c] >= 0 ? code_of(o[a.ccol[c]], a.cM[c]) : a.cM[c]) : -1;
+      double pr[NT];
+      double zz = 0.0;
+#pragma unroll
+      for (int q = 0; q < NT; q++) { pr[q] = al[q] * be[q]; zz += pr[q]; }
+      const double c = group_sum<16>(zz);
+      const double rc = ok ? recip(c) : 0.0;
+      const double f = __builtin_ldexp(rc, ef);
+      double w[NT], g[NT];
+#pragma unroll
+      for (int q = 0; q < NT; q++) { w[q] = ev[q] * be[q] * f; g[q] = pr[q] * rc; }
+#pragma unroll
+      for (int xi = 0; xi < NT; xi++)
+#pragma unroll
+        for (int yj = 0; yj < NT; yj++) K[xi * NT + yj] = mfma(ap[xi], w[yj], K[xi * NT + yj]);
+#pragma unroll
+      for (int mi = 0; mi < HR; mi++) {
+        if (mi >= hr) break;
+        const int r = 16 * mi + i;
+        const double oh = (r == row[0] || r == row[1] || r == row[2] || r == row[3]) ? 1.0 : 0.0;
+#pragma unroll
+        for (int yj = 0; yj < NT; yj++) Hc[mi * NT + yj] = mfma(oh, g[yj], Hc[mi * NT + yj]);
+      }
+    }
+  }
+  // the waves' sums in a fixed order: (w0 + w2) + (w1 + w3)
+  constexpr int NA = NK + NH;
+  auto put = [&](int slot) {
+    double* d = red + (size_t)slot * NA * 256;
+#pragma unroll
+    for (int q = 0; q < NK; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) d[(q * 4 + r) * 64 + lane] = K[q][r];
+#pragma unroll
+    for (int q = 0; q < NH; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) d[((NK + q) * 4 + r) * 64 + lane] = Hc[q][r];
+  };
+  auto add = [&](int slot) {
+    const double* d = red + (size_t)slot * NA * 256;
+#pragma unroll
+    for (int q = 0; q < NK; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) K[q][r] += d[(q * 4 + r) * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < NH; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) Hc[q][r] += d[((NK + q) * 4 + r) * 64 + lane];
+  };
+  double* p0s = red + (size_t)2 * NA * 256;          // [4][64]
+  p0s[wave * 64 + lane] = p0;
+  if (wave >= 2) put(wave - 2);
+  __syncthreads();
+  if (wave < 2) add(wave);
+  __syncthreads();
+  if (wave == 1) put(0);
+  __syncthreads();
+  if (wave != 0) return;
+  add(0);
+  const double pz = (p0s[lane] + p0s[128 + lane]) + (p0s[64 + lane] + p0s[192 + lane]);
+  double* slab = a.slab + (size_t)blockIdx.x * a.slab_size;
+  // K[x][y]: tile (xi, yj), D[(l >> 4) + 4r][l & 15]
+#pragma unroll
+  for (int xi = 0; xi < NT; xi++)
+#pragma unroll
+    for (int yj = 0; yj < NT; yj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        slab[(size_t)(16 * xi + k4 + 4 * r) * NP + 16 * yj + i] = K[xi * NT + yj][r];
+  double* Hs = slab + NP * NP;
+#pragma unroll
+  for (int mi = 0; mi < HR; mi++)
+#pragma unroll
+    for (int yj = 0; yj < NT; yj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 16 * mi + k4 + 4 * r;
+        if (row < a.R) Hs[(size_t)row * NP + 16 * yj + i] = Hc[mi * NT + yj][r];
+      }
+  if (lane < NP) slab[(size_t)NP * NP + (size_t)a.R * NP + lane] = pz;
+}
+
+template <int NT, int HR>
+int stats_launch(const EWideArgs& a, hipStream_t stream) {
+  constexpr int NA = NT * NT + HR * NT;
+  const size_t lds = (size_t)2 * NA * 256 * sizeof(double) + 4 * 64 * sizeof(double);
+  static size_t set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_stats_kernel<NT, HR>), lds, set)) return -1;
+  const int blocks = (int)((a.B + kStatSeqs - 1) / kStatSeqs);
+  hipLaunchKernelGGL((chain_stats_kernel<NT, HR>), dim3(blocks), dim3(kStatWaves * 64), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace
+
+int estep_wide_np(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 0; }
+
+// the slab row's size (doubles): K [NP][NP], H [R][NP], P0 [NP]
+int estep_wide_slab(int N, int R) {
+  const int NP = estep_wide_np(N);
+  return NP * NP + R * NP + NP;
+}
+
+bool estep_wide_fits(int N, int R) {
+  const int NP = estep_wide_np(N);
+  const int hr = (R + 15) / 16;
+  return NP != 0 && (NP <= 32 ? hr <= 8 : hr <= 2);
+}
+
+size_t estep_wide_scratch_bytes(int N, long B, int T) {
+  const int NP = estep_wide_np(N);
+  return (size_t)B * (2 * (size_t)T + 1) * NP * sizeof(double) + (size_t)B * T * sizeof(int) + 256;
+}
+
+int estep_wide_launch(const EWideArgs& a, hipStream_t stream) {
+  if (a.B <= 0) return 0;
+  const int NP = estep_wide_np(a.N);
+  if (!estep_wide_fits(a.N, a.R) || a.nchild > 4 || a.ncol > 4) return -2;
+  {
+    const int spb = 4 * (64 / NP);
+    const int blocks = (int)((a.B + spb - 1) / spb);
+    if (NP == 16) hipLaunchKernelGGL(chain_msgs_kernel<16>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
+    else if (NP == 32) hipLaunchKernelGGL(chain_msgs_kernel<32>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
+    else hipLaunchKernelGGL(chain_msgs_kernel<64>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
+    if (hipGetLastError() != hipSuccess) return -1;
+  }
+  g_last_kernel = "chain_msgs_kernel + chain_stats_kernel";
+  if (NP == 16) return stats_launch<1, 8>(a, stream);
+  if (NP == 32) return stats_launch<2, 8>(a, stream);
+  return stats_launch<4, 2>(a, stream);
+}
+
+}  // namespace nipamd

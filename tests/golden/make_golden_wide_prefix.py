@@ -9,7 +9,7 @@ Output tests/golden/wide64_prefix.npz:
   obs      int32 [B, T, 1]: series 0..T with leading missing runs of length
            L = 0..T, one with a missing step in the middle
   ll, bad  the reference's e_step per-series ll and BAD_LUCK flags
-  idx, cnt every e_step count outside the big family X1 | X0 Y1 Z1 and a
+  idx, cnt the e_step counts of the accepted series (bad == 0): every count outside the big family X1 | X0 Y1 Z1 and a
            fixed random sample of 8192 of its 16.8M entries (big_off,
            big_len locate it); cnt_sum = the sum of all counts
 Pins nipamd_estep_prefix_first_bad above 2^20 entries (simulated since
@@ -41,7 +41,9 @@ def main():
         obs[L, :L] = -1
     obs[T + 1, 2] = -1
     ps = orc.param_size()
-    cnt, ll, bad = orc.estep(obs, [4], np.ones(ps))
+    _, ll, bad = orc.estep(obs, [4], np.ones(ps))
+    cnt, _, bad_ok = orc.estep(obs[bad == 0], [4], np.ones(ps))     # counts of the accepted series
+    assert not bad_ok.any()
     # em_learn layout: one block per variable in declaration order (X0, Y1, Z1
     # priors, X1 | X0 Y1 Z1, O1 | X1), card x prod(parent cards) each
     big_off, big_len = 3 * 64, 64 ** 4

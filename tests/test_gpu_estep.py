@@ -186,15 +186,16 @@ def test_partial_is_shard_invariant_and_reproducible():
         p, _, _ = nip_amd.estep_partial(m, obs[k * 64:(k + 1) * 64].contiguous(), ov)
         parts.append(p.clone())
     comb = tree_sum(torch.stack(parts))
-    assert torch.equal(comb[:-2], whole[:-2])             # the body, bit for bit
-    assert comb[-2:].tolist() == [4.0, 0.0] and whole[-2:].tolist() == [1.0, 0.0]   # route tag counts
+    assert torch.equal(comb[:-3], whole[:-3])             # the body, bit for bit
+    assert comb[-3:].tolist() == [4.0, 0.0, 0.0] and whole[-3:].tolist() == [1.0, 0.0, 0.0]   # route tag counts
 
 
 def test_partials_of_different_routes_are_refused():
-    """The e_step route depends on T (a chain kernel's LDS must hold the
-    sequence; beyond it the general engine runs): partials of the two
-    layouts have the same size, and combining them must fail in the
-    finalize, not sum mismatched layouts."""
+    """The e_step route depends on T (the 16-state kernel's LDS must hold the
+    sequence; beyond it the wide chain e_step runs) and on the engine setting
+    (the general engine): partials of the layouts have the same size, and
+    combining them must fail in the finalize, not sum mismatched layouts
+    (ADVICE r02)."""
     m = nip_amd.Model.from_spec(*synth.hmm_spec(4, 4, seed=3))
     ov = [m.variable("M1")]
     short = torch.from_numpy(synth.observations(2, 16, 4, seed=1)).cuda()
@@ -203,11 +204,17 @@ def test_partials_of_different_routes_are_refused():
     a = a.clone()
     b, _, _ = nip_amd.estep_partial(m, long_, ov)
     b = b.clone()
-    assert a[-2:].tolist() == [1.0, 0.0] and b[-2:].tolist() == [0.0, 1.0]
-    nip_amd.estep_finalize(m, a, None)                   # each alone is fine
-    nip_amd.estep_finalize(m, b, None)
-    with pytest.raises(nip_amd.NipError):
-        nip_amd.estep_finalize(m, tree_sum(torch.stack([a, b])), None)
+    m.set_engine(nip_amd.ENGINE_JTREE)
+    c, _, _ = nip_amd.estep_partial(m, short, ov)
+    c = c.clone()
+    m.set_engine(nip_amd.ENGINE_AUTO)
+    assert a[-3:].tolist() == [1.0, 0.0, 0.0] and b[-3:].tolist() == [0.0, 0.0, 1.0]
+    assert c[-3:].tolist() == [0.0, 1.0, 0.0]
+    for p in (a, b, c):
+        nip_amd.estep_finalize(m, p, None)               # each alone is fine
+    for x, y in ((a, b), (a, c), (b, c)):
+        with pytest.raises(nip_amd.NipError):
+            nip_amd.estep_finalize(m, tree_sum(torch.stack([x, y])), None)
 
 
 def test_chunked_batch_matches_tree():
@@ -222,7 +229,7 @@ def test_chunked_batch_matches_tree():
     a, _, _ = nip_amd.estep_partial(m, obs[:16384].contiguous(), ov)
     a = a.clone()
     b, _, _ = nip_amd.estep_partial(m, obs[16384:].contiguous(), ov)
-    assert torch.equal(tree_sum(torch.stack([a, b.clone()]))[:-2], whole[:-2])
+    assert torch.equal(tree_sum(torch.stack([a, b.clone()]))[:-3], whole[:-3])
 
 
 @pytest.mark.parametrize("path", chain_fixtures(), ids=lambda p: os.path.basename(p))
