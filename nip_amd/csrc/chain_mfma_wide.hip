@@ -166,13 +166,6 @@ struct Geo {
 };
 
 __host__ __device__ inline long wblock_scratch(int NT, int T) { return (long)(T + 2 * kWG) * kWSeq * 16 * NT; }
-// the exponents of the scratch vectors (phase A's messages), one int per
-// (step, chain), after the message rows of every block and the sink block
-__device__ inline int* wblock_exps(const WideMfmaArgs& a, int NT, long blk) {
-  const long nb = (a.B + kWSeq - 1) / kWSeq + 1;
-  return reinterpret_cast<int*>(a.S + (size_t)nb * wblock_scratch(NT, a.T)) + (size_t)blk * (a.T + 2 * kWG) * kWSeq +
-         kWG * kWSeq;
-}
 
 struct WCtx {
   const double* tab;       // LDS tables
@@ -184,7 +177,6 @@ struct WCtx {
   int ncol;
   double* out;             // this direction's ring [2][kSlot]
   double* zr;              // forward: z2 ring [2][CH][16]
-  int* er;                 // this direction's exponent ring [2][CH][16]: E_t of each ring vector
   int wo[2][2];            // [tile][half] piece offsets of this lane
   bool zw;
 };
@@ -198,7 +190,6 @@ struct WChain {
   double Aop[NT][NT][4];
   v4d X[NT];
   int sc = 0;
-  int E = 0;      // the stored vector's exponent: alpha^_t = alpha_t 2^E (beta^_t likewise)
 
   // column k's observation at t, raw (-1: missing, also outside 0..T-1)
   __device__ __forceinline__ int raw(const WCtx& c, int k, int t) const {
@@ -236,12 +227,18 @@ struct WChain {
 
   // one step with the evidence rows loaded at its start: the MFMAs first, the
   // evidence product after them (its LDS loads complete under the MFMAs)
-  __device__ __forceinline__ void step_rows(const WCtx& c, double* L, double* Z, int* Er, const v4d (&r)[NC][NT]) {
+  __device__ __forceinline__ void step_rows(const WCtx& c, double* L, double* Z, const v4d (&r)[NC][NT]) {
     v4d d[NT];
     matvec(d);
     v4d e[NT];
     product(c, r, e);
-    finish(c, L, Z, Er, d, e);
+    finish(c, L, Z, d, e);
+  }
+
+  __device__ __forceinline__ void step(const WCtx& c, double* L, double* Z, const v4d (&e)[NT]) {
+    v4d d[NT];
+    matvec(d);
+    finish(c, L, Z, d, e);
   }
 
   __device__ __forceinline__ void matvec(v4d (&d)[NT]) {
@@ -266,10 +263,8 @@ struct WChain {
     }
   }
 
-  __device__ __forceinline__ void finish(const WCtx& c, double* L, double* Z, int* Er, const v4d (&d)[NT],
+  __device__ __forceinline__ void finish(const WCtx& c, double* L, double* Z, const v4d (&d)[NT],
                                          const v4d (&e)[NT]) {
-    E += sc;
-    if (c.zw) *Er = E;
     double part = 0.0;
 #pragma unroll
     for (int q = 0; q < NT; q++) {
@@ -302,7 +297,6 @@ struct WChain {
     auto chunk = [&](int ci, int (&cc)[CH][NC]) {
       double* slot = c.out + (ci & 1) * G::kSlot;
       double* zs = FWD ? c.zr + (ci & 1) * CH * kWSeq + (lane & 15) : nullptr;
-      int* es = c.er + (ci & 1) * CH * kWSeq + (lane & 15);
       const int base = ci * CH;
       const bool full = base + CH <= n;
 #pragma unroll
@@ -313,7 +307,7 @@ struct WChain {
         for (int q = 0; q < NC; q++) cd[q] = code(c, q, cc[k][q]);
         v4d r[NC][NT];
         rows_of(c, cd, r);
-        step_rows(c, slot + k * G::kStep, zs + k * kWSeq, es + k * kWSeq, r);
+        step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
       }
       barrier_lds(&dg);
       ldc(ci + 2, cc);
@@ -363,7 +357,6 @@ __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, do
       part += (ch.X[q].x + ch.X[q].y) + (ch.X[q].z + ch.X[q].w);
     }
     ch.sc = -__builtin_amdgcn_frexp_exp(swap16_sum(swap32_sum(part)));
-    if (g == 0) wblock_exps(a, NT, b0 / kWSeq)[(long)(T - 1) * kWSeq + j] = 0;   // beta_{T-1} = 1 exactly
   }
   MwDiag dg;
   dg.start();
@@ -450,20 +443,9 @@ struct WLL {
 // even chunks, the backward partner (which has no ll of its own and waits at
 // the barriers otherwise) the odd ones; its partial products join the forward
 // partner's through LDS after the block's closing barrier.
-//
-// Phase-B normalisation (round 4): sum_y alpha_t(y) beta_t(y) = Z for every t
-// (the sequence's likelihood), and the filters carry their vectors' scales as
-// exact powers of two (ring exponents; phase A's travel with the scratch
-// rows), so c_t = Z 2^(E_t + E'_t).  An anchor chunk (the phase's first, then
-// every kAnchor-th) normalises explicitly and records 1 / c and E + E' per
-// chain and lane; every other chunk's posterior is a multiply and an ldexp
-// per element -- no 16-lane sums, no reciprocals.  Drift between anchors is
-// the filters' rounding over kAnchor * CH steps (~1e-14 relative).
-constexpr int kAnchor = 16;
 template <bool FWD, bool PVEC, int NT, bool FILT>
 __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* out, const double* fring,
-                                         const double* zr, const int* er, double* Sblk, int* Xblk, double* anr,
-                                         int lane, long b0, int nchA, int nchB) {
+                                         const double* zr, double* Sblk, int lane, long b0, int nchA, int nchB) {
   using G = Geo<NT>;
   constexpr int NP = G::NP, LPC = G::LPC, CH = G::CH, QN = G::QN;
   const int T = a.T, H = a.H;
@@ -482,75 +464,43 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     const double* slot = fring + (ci & 1) * G::kSlot;
     const double* zs = zr + (ci & 1) * CH * kWSeq;
     const bool full = ci * CH + CH <= n;
-    // two halves of the chunk's steps (register pressure), in step order
-    constexpr int KH = CH > 1 ? CH / 2 : 1;
+    double y[CH * QN];
 #pragma unroll
-    for (int k0 = 0; k0 < CH; k0 += KH) {
-      double y[KH * QN];
+    for (int k = 0; k < CH; k++)
 #pragma unroll
-      for (int k = 0; k < KH; k++)
-#pragma unroll
-        for (int q = 0; q < QN; q++) {
-          const v2d v = *reinterpret_cast<const v2d*>(slot + (k0 + k) * G::kStep + G::piece_off(q * CH + hi, s));
-          y[k * QN + q] = v.x * ll.w0 + v.y * ll.w1;
-        }
-      sumL_n<LPC>(y);
-#pragma unroll
-      for (int k = 0; k < KH; k++) {
-        const int i = ci * CH + k0 + k;
-        if (i >= n) break;
-        const bool last = t0 + i == T - 1;
-#pragma unroll
-        for (int q = 0; q < QN; q++)
-          ll.step(q, y[k * QN + q], zs[(k0 + k) * kWSeq + q * CH + hi], last, !full || ((k0 + k) & 3) == 3);
+      for (int q = 0; q < QN; q++) {
+        const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(q * CH + hi, s));
+        y[k * QN + q] = v.x * ll.w0 + v.y * ll.w1;
       }
+    sumL_n<LPC>(y);
+#pragma unroll
+    for (int k = 0; k < CH; k++) {
+      const int i = ci * CH + k;
+      if (i >= n) break;
+      const bool last = t0 + i == T - 1;
+#pragma unroll
+      for (int q = 0; q < QN; q++)
+        ll.step(q, y[k * QN + q], zs[k * kWSeq + q * CH + hi], last, !full || (k & 3) == 3);
     }
   };
   double* const sink = FILT ? a.S + 2 * s
                             : a.S + (size_t)((a.B + kWSeq - 1) / kWSeq) * wblock_scratch(NT, T) + 2 * s;
   const bool st0 = 2 * s < a.N, st1 = 2 * s + 1 < a.N;
-  // the anchor's 1 / c and E + E' of this lane group's step, per chain, in
-  // LDS (anr: [CH][16] doubles, then [CH][16] ints); a group's 16 lanes read
-  // the same words (broadcast)
-  double* const arz = anr + hi * kWSeq;
-  int* const aez = reinterpret_cast<int*>(anr + CH * kWSeq) + hi * kWSeq;
-  // normalised posteriors of ring step kk (time t) times o, for the 16 chains;
-  // eo: the ring step's exponents (null: explicit normalisation, no anchor),
-  // xo: the other direction's
-  auto emit = [&](const double* slot, int kk, int t, bool ok, const v2d (&o)[kWSeq], const int* eo,
-                  const int (&xo)[kWSeq], bool anchor) {
-    constexpr int QG = 4;                        // chains per pass (register pressure: the partners
-                                                 // share the register file with the filters)
+  // normalised posteriors of ring step kk (time t) times o, for the 16 chains
+  auto emit = [&](const double* slot, int kk, int t, bool ok, const v2d (&o)[kWSeq]) {
 #pragma unroll
-    for (int q0 = 0; q0 < kWSeq; q0 += QG) {
-      double px[QG], py[QG], z[QG], r[QG];
-      int ev[QG];
-      if (eo) {
-        const int4 v = *reinterpret_cast<const int4*>(eo + q0);
-        ev[0] = v.x + xo[q0]; ev[1] = v.y + xo[q0 + 1]; ev[2] = v.z + xo[q0 + 2]; ev[3] = v.w + xo[q0 + 3];
-      }
+    for (int q0 = 0; q0 < kWSeq; q0 += 8) {
+      double px[8], py[8], z[8], r[8];
 #pragma unroll
-      for (int i = 0; i < QG; i++) {
+      for (int i = 0; i < 8; i++) {
         const v2d v = *reinterpret_cast<const v2d*>(slot + kk * G::kStep + G::piece_off(q0 + i, s));
         px[i] = v.x * o[q0 + i].x; py[i] = v.y * o[q0 + i].y;
         z[i] = px[i] + py[i];
       }
-      if (!eo || anchor) {
-        sumL_n<LPC>(z);
-        recip_n(z, r);
-        if (eo && s == 0) {
+      sumL_n<LPC>(z);
+      recip_n(z, r);
 #pragma unroll
-          for (int i = 0; i < QG; i++) { arz[q0 + i] = r[i]; aez[q0 + i] = ev[i]; }
-        }
-      } else {
-        const v2d r01 = *reinterpret_cast<const v2d*>(arz + q0);
-        const v2d r23 = *reinterpret_cast<const v2d*>(arz + q0 + 2);
-        const int4 ez = *reinterpret_cast<const int4*>(aez + q0);
-        r[0] = __builtin_ldexp(r01.x, ez.x - ev[0]); r[1] = __builtin_ldexp(r01.y, ez.y - ev[1]);
-        r[2] = __builtin_ldexp(r23.x, ez.z - ev[2]); r[3] = __builtin_ldexp(r23.y, ez.w - ev[3]);
-      }
-#pragma unroll
-      for (int i = 0; i < QG; i++) {
+      for (int i = 0; i < 8; i++) {
         const long bb = b0 + q0 + i;
         if constexpr (PVEC) {
           double* p = (ok && bb < a.B) ? a.post + (size_t)bb * a.post_bstride + (long)t * NP + a.post_off + 2 * s
@@ -575,21 +525,10 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     if constexpr (FILT) {
       if (!PVEC && !a.post) return;
       v2d ones[kWSeq];
-      int zx[kWSeq];
 #pragma unroll
-      for (int q = 0; q < kWSeq; q++) { ones[q] = v2d{1.0, 1.0}; zx[q] = 0; }
-      emit(slot, hi, ci * CH + hi, ci * CH + hi < nA, ones, nullptr, zx, true);
+      for (int q = 0; q < kWSeq; q++) ones[q] = v2d{1.0, 1.0};
+      emit(slot, hi, ci * CH + hi, ci * CH + hi < nA, ones);
       return;
-    }
-    // the slot's exponents travel with the scratch rows (lanes 0..15: chain = lane)
-    if (lane < kWSeq) {
-      const int* es = er + (ci & 1) * CH * kWSeq + lane;
-#pragma unroll
-      for (int k = 0; k < CH; k++) {
-        const int i = ci * CH + k;
-        if (i >= nA) break;
-        Xblk[(long)(tA + dir * i) * kWSeq + lane] = es[k * kWSeq];
-      }
     }
 #pragma unroll
     for (int k = 0; k < CH; k++) {
@@ -618,38 +557,30 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     return;
   }
   v2d oa[kWSeq];
-  int xa[kWSeq];
-  auto load_other = [&](v2d (&o)[kWSeq], int (&xo)[kWSeq], int ci) {
+  auto load_other = [&](v2d (&o)[kWSeq], int ci) {
     if (NIPAMD_MW_ABLATE == 1) return;
-    const long t = tlow(ci) + hi;
-    const double* q = Sblk + t * G::kStep + 2 * s;
+    const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
 #pragma unroll
     for (int c = 0; c < kWSeq; c++) o[c] = *reinterpret_cast<const v2d*>(q + c * NP);
-    const int* x = Xblk + t * kWSeq;
-#pragma unroll
-    for (int c = 0; c < kWSeq; c += 4) {
-      const int4 v = *reinterpret_cast<const int4*>(x + c);
-      xo[c] = v.x; xo[c + 1] = v.y; xo[c + 2] = v.z; xo[c + 3] = v.w;
-    }
   };
   const int nBf = T - H;                         // the forward side's phase-B steps (from t = H)
-  auto drainB = [&](int ci, const v2d (&o)[kWSeq], const int (&xo)[kWSeq]) {
+  auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {
     if (NIPAMD_MW_ABLATE == 1) return;
     if (FWD == ((ci & 1) == 0) && ci * CH < nBf) ll_chunk(ci, nBf, H);
     if (!PVEC && !a.post) return;
     const double* slot = out + (ci & 1) * G::kSlot;
     const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
-    emit(slot, kB, tlow(ci) + hi, kB < nk, o, er + (ci & 1) * CH * kWSeq + kB * kWSeq, xo, ci % kAnchor == 0);
+    emit(slot, kB, tlow(ci) + hi, kB < nk, o);
   };
   // one buffer (two groups' partners share the register file with the
   // filters): the next chunk's vectors are requested as soon as this chunk's
   // posteriors have used them, a chunk of latency ahead
   const int last = nchB > 0 ? nchB - 1 : 0;
-  load_other(oa, xa, 0);
+  load_other(oa, 0);
   for (int ci = 0; ci < nchB; ci++) {
     barrier_lds(&dg);
-    drainB(ci, oa, xa);
-    load_other(oa, xa, ci + 1 < last ? ci + 1 : last);
+    drainB(ci, oa);
+    load_other(oa, ci + 1 < last ? ci + 1 : last);
   }
   // the forward side has nchB chunks when T - H > H (odd T): the last one is
   // the forward partner's or the backward partner's by its parity like the rest
@@ -680,12 +611,7 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   const bool fwd = FILT || (role % F) == 0;
   double* out = reinterpret_cast<double*>(smem) + grp * 4 * G::kSlot;   // this group's [2 dirs][2 slots][kSlot]
   double* zr = reinterpret_cast<double*>(smem) + kWGroups * 4 * G::kSlot + grp * 2 * G::CH * kWSeq;
-  // exponent rings [group][dir][2 slots][CH][16] (ints)
-  int* ers = reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + kWGroups * (4 * G::kSlot + 2 * G::CH * kWSeq));
-  // the partners' anchors [group][dir]: [CH][16] doubles + [CH][16] ints
-  double* anc = reinterpret_cast<double*>(smem) + kWGroups * (4 * G::kSlot + 2 * G::CH * kWSeq) +
-                kWGroups * 2 * G::CH * kWSeq;       // after the exponent rings (2 CH 16 ints = CH 16 doubles per dir)
-  double* tab = anc + kWGroups * 2 * (G::CH * kWSeq * 3 / 2);
+  double* tab = reinterpret_cast<double*>(smem) + kWGroups * (4 * G::kSlot + 2 * G::CH * kWSeq);
   const int ncol = a.ncol > 0 ? a.ncol : 1;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * (kWGroups * kWSeq) + grp * kWSeq;
@@ -698,19 +624,16 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   const int nA = (H > T - 1 - H ? H : T - 1 - H), nB = (T - H > H ? T - H : H);
   const int nchA = (nA + G::CH - 1) / G::CH, nchB = FILT ? 0 : (nB + G::CH - 1) / G::CH;
   double* ring = out + (fwd ? 0 : 2 * G::kSlot);
-  int* er = ers + (grp * 2 + (fwd ? 0 : 1)) * 2 * G::CH * kWSeq;
   double* Sblk = FILT ? nullptr : a.S + (size_t)(b0 / kWSeq) * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;
-  int* Xblk = FILT ? nullptr : wblock_exps(a, NT, b0 / kWSeq);
-  double* anr = anc + (grp * 2 + (fwd ? 0 : 1)) * (G::CH * kWSeq * 3 / 2);
   if (!filter) {
     const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
                       (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
     if (pvec) {
-      if (fwd) wpartner<true, true, NT, FILT>(a, ring, out, zr, er, Sblk, Xblk, anr, lane, b0, nchA, nchB);
-      else wpartner<false, true, NT, FILT>(a, ring, out, zr, er, Sblk, Xblk, anr, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, true, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, true, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
     } else {
-      if (fwd) wpartner<true, false, NT, FILT>(a, ring, out, zr, er, Sblk, Xblk, anr, lane, b0, nchA, nchB);
-      else wpartner<false, false, NT, FILT>(a, ring, out, zr, er, Sblk, Xblk, anr, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, false, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
+      else wpartner<false, false, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
     }
     return;
   }
@@ -728,7 +651,6 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   }
   c.out = ring;
   c.zr = zr;
-  c.er = er;
   c.zw = g == 0;
 #pragma unroll
   for (int q = 0; q < NT; q++) {
@@ -746,14 +668,11 @@ size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T) {
   (void)ncol; (void)T;                                       // codes are read from HBM
   const size_t slot = 2048;                                  // doubles per ring slot
   const size_t ch = 8 / NT;
-  // rings, z2 rings, exponent rings, anchors, tables
-  return (kWGroups * (4 * slot + 2 * ch * kWSeq) + kWGroups * 2 * ch * kWSeq + kWGroups * 2 * (ch * kWSeq * 3 / 2) +
-          (size_t)tab_rows * (16 * NT + 2)) * sizeof(double);
+  return (kWGroups * (4 * slot + 2 * ch * kWSeq) + (size_t)tab_rows * (16 * NT + 2)) * sizeof(double);
 }
 
 size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
-  const size_t nb = (size_t)((B + kWSeq - 1) / kWSeq + 1);
-  return nb * wblock_scratch(NT, T) * sizeof(double) + nb * (size_t)(T + 2 * kWG) * kWSeq * sizeof(int);
+  return (size_t)((B + kWSeq - 1) / kWSeq + 1) * wblock_scratch(NT, T) * sizeof(double);
 }
 
 namespace {

@@ -1381,6 +1381,15 @@ int nipamd_estep_prefix_first_bad(nipamd_model* mm, int T) {
   return prefix_first_bad(mm, T);
 }
 
+// A route writes the first `written` doubles of the body; the rest (another
+// route's larger layout) is zeroed, so every partial is fully defined and
+// partials of one route combine and compare bit for bit.
+static int zero_tail(nipamd_model* mm, double* d_partial, int written, hipStream_t st) {
+  const int body = estep_body_size(mm);
+  if (written < body) HIP_OK(hipMemsetAsync(d_partial + written, 0, (size_t)(body - written) * sizeof(double), st));
+  return 0;
+}
+
 // The wide chain e_step (estep_wide.hip): the filters store every message of
 // a chunk of sequences, the statistics kernel writes one slab row per 16
 // sequences, and the fixed-order tree sums the rows (per chunk, then over
@@ -1393,6 +1402,7 @@ static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d
   hipStream_t st = (hipStream_t)stream;
   if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 0.0, 1.0, st))
     return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
+  if (int rc = zero_tail(mm, d_partial, S, st)) return rc;
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   if (int rc = ensure_tables(mm)) return rc;
   ReqTables* rt = nullptr;
@@ -1472,7 +1482,7 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       return rc;
     if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 1.0, 0.0, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
-    return 0;
+    return zero_tail(mm, d_partial, nipamd::param_size(mm->m), (hipStream_t)stream);
   }
   const auto& P = mm->m.chain;
   const bool general = estep_general_plan(P);
@@ -1485,6 +1495,7 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   hipStream_t st = (hipStream_t)stream;
   if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, 0.0, st))
     return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
+  if (int rc = zero_tail(mm, d_partial, S, st)) return rc;
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   if (int rc = ensure_tables(mm)) return rc;
   Route rh;

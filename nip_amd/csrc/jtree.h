@@ -112,6 +112,7 @@ struct JtRun {
   int filter;             // forward_inference: no beta, the posterior sweep uses ones
   int estep;              // status BAD_LUCK rules of e_step (nip.c:1827-1854)
   int chunk;              // posterior: time steps per unit
+  int gunits;             // HBM workspace: slots per direction (<= kJtGlobalUnits; wsg holds 2 x gunits)
 };
 
 // launches (jtree.hip); L = lanes per sequence unit (16, 32 or 64)
@@ -119,7 +120,16 @@ int jt_w_launch(const JtRun& r, double* w_out, int L, hipStream_t st);
 int jt_filter_launch(const JtRun& r, int L, bool lds, int dirs, hipStream_t st);
 int jt_post_launch(const JtRun& r, int L, bool lds, hipStream_t st);
 int jt_add_launch(const double* src, double* dst, int n, hipStream_t st);
-// workspace units per launch when the workspace lives in HBM
+// workspace units per launch when the workspace lives in HBM (at most; the
+// host lowers it so that the 2 x units slots stay within kJtGlobalBytes)
 constexpr int kJtGlobalUnits = 4096;
+constexpr size_t kJtGlobalBytes = (size_t)8 << 30;
+inline int jt_global_units(int ws) {
+  const size_t per = (size_t)2 * ws * sizeof(double);
+  size_t u = per ? kJtGlobalBytes / per : kJtGlobalUnits;
+  if (u > (size_t)kJtGlobalUnits) u = kJtGlobalUnits;
+  u = u / 64 * 64;
+  return u < 64 ? 64 : (int)u;
+}
 
 }  // namespace nipamd

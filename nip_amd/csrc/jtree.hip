@@ -126,10 +126,13 @@ __device__ double normalise(double* x, int n, int sub) {
   return s;
 }
 
+// a unit's workspace: in LDS, or its own HBM slot -- per block of the whole
+// grid, blockIdx.y included (the two filter directions run as blockIdx.y = 0
+// and 1 of one launch; the host sizes wsg for 2 x r.gunits slots)
 template <bool LDS>
 __device__ __forceinline__ double* unit_ws(const JtRun& r, double* lds, int u, int U) {
   if (LDS) return lds + (long)u * r.p.ws;
-  return r.wsg + ((long)blockIdx.x * U + u) * r.p.ws;
+  return r.wsg + (((long)blockIdx.y * gridDim.x + blockIdx.x) * U + u) * r.p.ws;
 }
 
 // any evidence entered at this step (a step without any contributes exactly 0
@@ -327,7 +330,7 @@ template <int L, bool LDS>
 int filter_launch(const JtRun& r, int dirs, hipStream_t st) {
   constexpr int U = 64 / L;
   long blocks = (r.B + U - 1) / U;
-  if (!LDS && blocks > kJtGlobalUnits / U) blocks = kJtGlobalUnits / U;
+  if (!LDS && blocks > r.gunits / U) blocks = r.gunits / U;
   const size_t shm = LDS ? (size_t)U * r.p.ws * sizeof(double) : 0;
   const int dir_base = dirs == 2 ? 0 : (dirs == 0 ? 0 : 1);   // dirs: 0 fwd only, 1 bwd only, 2 both
   hipLaunchKernelGGL((jt_filter_kernel<L, LDS>), dim3((unsigned)blocks, dirs == 2 ? 2 : 1), dim3(64),
@@ -340,7 +343,7 @@ int post_launch(const JtRun& r, hipStream_t st) {
   constexpr int U = 64 / L;
   const long nch = (r.T + r.chunk - 1) / r.chunk;
   long blocks = (r.B * nch + U - 1) / U;
-  if (!LDS && blocks > kJtGlobalUnits / U) blocks = kJtGlobalUnits / U;
+  if (!LDS && blocks > r.gunits / U) blocks = r.gunits / U;
   const size_t shm = LDS ? (size_t)U * r.p.ws * sizeof(double) : 0;
   hipLaunchKernelGGL((jt_post_kernel<L, LDS>), dim3((unsigned)blocks), dim3(64), shm, st, r);
   return hipGetLastError() == hipSuccess ? 0 : -1;

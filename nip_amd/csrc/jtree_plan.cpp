@@ -446,6 +446,7 @@ static int get_plan(nipamd_model* mm, int n_obs, const int* obs_vars, int n_quer
   JtRun r{};
   r.p = P.p;
   r.wsg = s->wsg;
+  r.gunits = jt_global_units(P.p.ws);
   if (jt_w_launch(r, P.d_dp + P.p.w_off, P.L, st)) {
     (void)hipFree(P.d_ip); (void)hipFree(P.d_dp);
     return set_error(NIPAMD_ERROR_DEVICE, "jtree: m1-weight launch failed");
@@ -496,7 +497,7 @@ int jt_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
   const long chunk = seq_chunk(B, T, K);
   if (int rc = ensure_buf(&s->msg, &s->msg_bytes, (size_t)2 * chunk * T * K * sizeof(double))) return rc;
   if (!P->lds)
-    if (int rc = ensure_buf(&s->wsg, &s->wsg_bytes, (size_t)kJtGlobalUnits * P->p.ws * sizeof(double))) return rc;
+    if (int rc = ensure_buf(&s->wsg, &s->wsg_bytes, (size_t)2 * jt_global_units(P->p.ws) * P->p.ws * sizeof(double))) return rc;
   const long ocols = n_obs > 0 ? n_obs : 1;
   for (long b0 = 0; b0 < B; b0 += chunk) {
     const long nb = std::min<long>(chunk, B - b0);
@@ -511,6 +512,7 @@ int jt_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
     r.msgA = s->msg;
     r.msgB = s->msg + (size_t)chunk * T * K;
     r.wsg = s->wsg;
+    r.gunits = jt_global_units(P->p.ws);
     r.post = d_post ? d_post + b0 * (long)T * P->stride : nullptr;
     r.post_bstride = (long)T * P->stride;
     r.post_tstride = P->stride;
@@ -545,7 +547,7 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   const long lvl = (chunk + 63) / 64;
   if (int rc = ensure_buf(&s->msg, &s->msg_bytes, (size_t)2 * chunk * T * K * sizeof(double))) return rc;
   if (!P->lds)
-    if (int rc = ensure_buf(&s->wsg, &s->wsg_bytes, (size_t)kJtGlobalUnits * P->p.ws * sizeof(double))) return rc;
+    if (int rc = ensure_buf(&s->wsg, &s->wsg_bytes, (size_t)2 * jt_global_units(P->p.ws) * P->p.ws * sizeof(double))) return rc;
   if (int rc = ensure_buf(&s->work, &s->work_bytes,
                           ((size_t)chunk + 2 * lvl + nchunks + 64) * S * sizeof(double))) return rc;
   double* slab = s->work;
@@ -577,6 +579,7 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     r.msgA = s->msg;
     r.msgB = s->msg + (size_t)chunk * T * K;
     r.wsg = s->wsg;
+    r.gunits = jt_global_units(P->p.ws);
     r.ll = d_ll ? d_ll + b0 : nullptr;
     r.status = d_status ? (unsigned*)d_status + b0 : nullptr;
     r.slabs = slab;

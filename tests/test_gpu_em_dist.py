@@ -150,3 +150,34 @@ def test_gpu_tree_sum_bit_identical_to_pairwise_tree(n, S):
     want = nem.tree_sum(x.clone())
     got = nip_amd.tree_sum(x.cuda()).cpu()
     assert torch.equal(got, want.reshape(-1))
+
+
+def test_config4_full_shard_counts_vs_textbook():
+    """The whole config-4 shard (131072 x 1024) element by element: the
+    e_step counts of the full launch (8 chunks of 16384 sequences, the
+    fixed-order trees) against a textbook e_step in torch fp64 on the same
+    GPU (tests/textbook_util.py hmm_estep_torch, pinned to the reference by
+    test_oracle_textbook.py), counts rel 1e-11, every sequence's ll rel 1e-12."""
+    from textbook_util import chain_tables, hmm_estep_torch
+    nodes, pots = synth.hmm_spec(16, 16)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    B, Tn = 131072, 1024
+    obs = torch.from_numpy(synth.observations(B, Tn, 16, seed=4)).cuda()
+    ov = [m.variable("M1")]
+    counts, ll, st = nip_amd.e_step(m, obs, ov, torch.zeros((m.param_size(),), dtype=torch.float64, device="cuda"))
+    assert not st.any().item()
+    A, pi, Es = chain_tables(m, m.variable("P0"), m.variable("P1"), [m.variable("M1")])
+    tA, tpi, tE = (torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (A, pi, Es[0]))
+    want = torch.zeros_like(counts)
+    wll = torch.empty_like(ll)
+    for b0 in range(0, B, 16384):
+        c, l = hmm_estep_torch(tA, tpi, tE, obs[b0:b0 + 16384, :, 0].long())
+        want += c
+        wll[b0:b0 + 16384] = l
+        del c
+        torch.cuda.empty_cache()
+    got, want = counts.cpu().numpy(), want.cpu().numpy()
+    err = np.abs(got - want) / np.maximum(1.0, np.abs(want))
+    assert err.max() <= 1e-11, err.max()
+    lg, lw = ll.cpu().numpy(), wll.cpu().numpy()
+    assert np.all(np.abs(lg - lw) <= 1e-12 * np.abs(lw)), np.abs(lg - lw).max()

@@ -117,3 +117,25 @@ def test_large_batch_properties():
         rp, rl = orc.fb(obs[b], [m.variable("M1")], [m.variable("P1")])
         assert np.abs(post[b] - rp).max() <= POST_TOL
         assert abs(ll[b] - rl) <= LL_RTOL * abs(rl)
+
+
+def test_config2_all_sequences_vs_textbook():
+    """Config 2 in full (4096 x 1024, the bench's batch and seed): every
+    sequence's posteriors (abs 1e-12) and ll (rel 1e-12) against the textbook
+    smoother in torch fp64 on the same GPU (tests/textbook_util.py
+    smoother_torch, pinned to the reference by test_oracle_textbook.py)."""
+    import torch
+    from textbook_util import chain_tables, smoother_torch
+    nodes, pots = synth.hmm_spec(16, 16)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    B, T = 4096, 1024
+    obs = synth.observations(B, T, 16, seed=1)
+    post, ll, st = gpu_fb(m, obs, [m.variable("M1")], [m.variable("P1")])
+    assert not st.any()
+    A, pi, Es = chain_tables(m, m.variable("P0"), m.variable("P1"), [m.variable("M1")])
+    tA, tpi, tE = (torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (A, pi, Es[0]))
+    tobs = torch.from_numpy(obs[:, :, 0].astype(np.int64)).cuda()
+    wp, wl = smoother_torch(tA, tpi, [tE], [tobs])
+    assert np.abs(post - wp.cpu().numpy()).max() <= POST_TOL
+    wl = wl.cpu().numpy()
+    assert np.all(np.abs(ll - wl) <= LL_RTOL * np.abs(wl)), np.abs(ll - wl).max()

@@ -196,3 +196,31 @@ def test_bad_luck_only_on_leading_missing_runs():
     for b in np.nonzero(ok)[0]:
         _, _, l, _ = textbook(A, pi, [E], [obs[b, :, 0]], E.sum(axis=1))
         assert abs(ll[b] - l) <= 1e-12 * max(1.0, abs(l))
+
+
+@pytest.mark.parametrize("N,M,miss", [(5, 4, 0.0), (16, 16, 0.2)])
+def test_torch_textbook_estep_vs_reference(N, M, miss):
+    """tests/textbook_util.py's torch e_step (the full-shard check of
+    test_gpu_em_dist.py, run there on the GPU) against the reference's own
+    e_step, here on the CPU: counts 1e-11, ll 1e-12."""
+    torch = pytest.importorskip("torch")
+    from textbook_util import hmm_estep_torch, smoother_torch
+    nodes, pots, A, E, pi = hmm_tables(N, M, seed=N * 5 + M)
+    ref = harness(nodes, pots)
+    obs = synth.observations(9, 23, M, seed=N + 1)
+    rng = np.random.default_rng(M + 1)
+    obs[rng.random(obs.shape) < miss] = -1
+    obs[:, 0] = np.where(obs[:, 0] < 0, 0, obs[:, 0])     # no leading missing run
+    cnt, ll, bad = ref.estep(obs, [2], np.zeros(ref.param_size()))
+    assert not bad.any()
+    tA, tE, tpi = (torch.from_numpy(x) for x in (A, E, pi))
+    tobs = torch.from_numpy(obs[:, :, 0].astype(np.int64))
+    got, gll = hmm_estep_torch(tA, tpi, tE, tobs)
+    got = got.numpy()
+    assert np.all(np.abs(got - cnt) <= 1e-11 * np.maximum(1.0, np.abs(cnt))), np.abs(got - cnt).max()
+    assert np.all(np.abs(gll.numpy() - ll) <= 1e-12 * np.maximum(1.0, np.abs(ll)))
+    post, sll = smoother_torch(tA, tpi, [tE], [tobs])
+    for b in range(obs.shape[0]):
+        rp, rl = ref.fb(obs[b], [2], [1])
+        assert np.abs(post[b].numpy() - rp).max() <= 1e-12
+        assert abs(sll[b].item() - rl) <= 1e-12 * max(1.0, abs(rl))

@@ -86,3 +86,106 @@ def smoother(A, pi, Es, cols):
         p = ah[:, t] * b
         post[:, t] = p / p.sum(axis=1, keepdims=True)
     return post, ah, ll
+
+
+# ---------------------------------------------------------------------------
+# The same textbook recursions in torch fp64 on the GPU, for the full-size
+# checks (config 2: 4096 x 1024; config 4: 131072 x 1024), where numpy would
+# take minutes.  Independent of the engine: plain matmuls and elementwise ops
+# over the model's compiled tables (chain_tables).
+
+def _ev_torch(Es, s_list, cols, t):
+    """e_t [B, N] over the children (cols: [B, T] long tensors, -1 missing)."""
+    e = None
+    for E, s, c in zip(Es, s_list, cols):
+        x = c[:, t]
+        ee = E[:, x.clamp(min=0)].T
+        ee = torch_where(x < 0, s, ee)
+        e = ee if e is None else e * ee
+    return e
+
+
+def torch_where(mask, s, ee):
+    import torch
+    return torch.where(mask[:, None], s[None, :].expand_as(ee), ee)
+
+
+def smoother_torch(A, pi, Es, cols):
+    """Smoothed [B, T, N] and ll [B] (torch, on the device of A)."""
+    import torch
+    B, T = cols[0].shape
+    N = A.shape[0]
+    s_list = [E.sum(dim=1) for E in Es]
+    s_all = torch.ones(N, dtype=A.dtype, device=A.device)
+    for s in s_list:
+        s_all = s_all * s
+    ah = torch.empty((B, T, N), dtype=A.dtype, device=A.device)
+    ll = torch.zeros(B, dtype=A.dtype, device=A.device)
+    prev = pi[None, :].expand(B, N)
+    for t in range(T):
+        u = prev @ A
+        al = u * _ev_torch(Es, s_list, cols, t)
+        c = al.sum(dim=1)
+        ll += torch.log(c) - torch.log((u * s_all).sum(dim=1))
+        prev = al / c[:, None]
+        ah[:, t] = prev
+    post = torch.empty_like(ah)
+    post[:, T - 1] = ah[:, T - 1]
+    b = torch.ones((B, N), dtype=A.dtype, device=A.device)
+    for t in range(T - 2, -1, -1):
+        b = (_ev_torch(Es, s_list, cols, t + 1) * b) @ A.T
+        b = b / b.sum(dim=1, keepdim=True)
+        p = ah[:, t] * b
+        post[:, t] = p / p.sum(dim=1, keepdim=True)
+    return post, ll
+
+
+def hmm_estep_torch(A, pi, E, obs):
+    """The e_step of an HMM slice (prev, cur, one child) in the em_learn
+    layout [P0 | P1|P0 (y + N x) | M1|P1 (m + M y)] (nip.c:1925-1967: each
+    family marginal normalised per step, P0 at t = 0 only, a missing
+    observation split as E(y, m) / s(y)), and the per-sequence ll.
+    obs: [B, T] long tensor (-1 missing).  Sums over sequences and steps in
+    torch's order (a check at 1e-11 relative, not a bit-exact one)."""
+    import torch
+    B, T = obs.shape
+    N, M = E.shape
+    s = E.sum(dim=1)
+    dev, dt = A.device, A.dtype
+    # forward: alpha^_t normalised; backward: beta^_t normalised
+    ah = torch.empty((B, T, N), dtype=dt, device=dev)
+    ll = torch.zeros(B, dtype=dt, device=dev)
+    prev = pi[None, :].expand(B, N)
+    for t in range(T):
+        u = prev @ A
+        al = u * _ev_torch([E], [s], [obs], t)
+        c = al.sum(dim=1)
+        ll += torch.log(c) - torch.log((u * s).sum(dim=1))
+        prev = al / c[:, None]
+        ah[:, t] = prev
+    c0 = torch.zeros(N, dtype=dt, device=dev)
+    c1 = torch.zeros((N, N), dtype=dt, device=dev)
+    c2 = torch.zeros((N, M), dtype=dt, device=dev)
+    b = torch.ones((B, N), dtype=dt, device=dev)
+    ar = torch.arange(M, device=dev)
+    for t in range(T - 1, -1, -1):
+        if t < T - 1:
+            b = (_ev_torch([E], [s], [obs], t + 1) * b) @ A.T
+            b = b / b.sum(dim=1, keepdim=True)
+        e = _ev_torch([E], [s], [obs], t)
+        w = e * b
+        pv = ah[:, t - 1] if t > 0 else pi[None, :].expand(B, N)
+        n = ((pv @ A) * w).sum(dim=1)
+        c1 += A * ((pv / n[:, None]).T @ w)
+        g = ah[:, t] * b
+        g = g / g.sum(dim=1, keepdim=True)
+        m = obs[:, t]
+        miss = m < 0
+        oh = (m[:, None] == ar[None, :]).to(dt)
+        c2 += g.T @ oh
+        if bool(miss.any()):
+            c2 += g[miss].sum(dim=0)[:, None] * E / s[:, None]
+        if t == 0:
+            g0 = pi[None, :] * (w @ A.T)
+            c0 += (g0 / g0.sum(dim=1, keepdim=True)).sum(dim=0)
+    return torch.cat([c0, c1.reshape(-1), c2.reshape(-1)]), ll
