@@ -113,13 +113,16 @@ WORKLOADS = {
     # the general join-tree engine as "opchain_jt"
     "opchain": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 20),
     "opchain_jt": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 2),
+    # e_step of config 3's model (demo1 @ 32 states, A1 and B1 observed): the
+    # wide chain e_step (estep_wide.hip)
+    "estep_config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256, 5),
     # e_step of demo1's structure (16 states: hidden parent D1, children A1, B1)
     # on the chain e_step kernel, and on the general engine ("estep_demo1_jt")
     "estep_demo1": ("general", lambda a: synth.demo1_spec(16), ["A1", "B1"], "C1", 16384, 1024, 5),
     "estep_demo1_jt": ("general", lambda a: synth.demo1_spec(16), ["A1", "B1"], "C1", 4096, 1024, 2),
 }
 # the default line: the headline, then these under "secondary" 
-SECONDARY = ["config3", "em", "config5"]
+SECONDARY = ["config3", "em", "config5", "estep_config3"]
 
 
 def host_info():
@@ -158,7 +161,8 @@ def cpu_baselines(workloads, budget):
     """The reference's own code (and the C port) on the host's granted cores,
     one process per core (oracle/cpu_bench.py), run as a child process
     before this process touches the GPU.  -> {workload: record}."""
-    cmap = {"fb": "fb", "config3": "config3", "em": "em", "estep": "em", "config5": "config5"}
+    cmap = {"fb": "fb", "config3": "config3", "em": "em", "estep": "em", "config5": "config5",
+            "estep_config3": "estep_config3"}
     wl = [cmap[w] for w in workloads if w in cmap]
     if not wl:
         return {}
@@ -194,18 +198,73 @@ def cpu_baselines(workloads, budget):
     return out
 
 
+def load_entry(workload: str):
+    """The committed rocprofv3 PMC pass of a workload (profiles/pmc_traffic.json,
+    written by profiles/summarize.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get("entries", {}).get(workload)
+    except Exception:
+        return None
+
+
 def load_traffic(workload: str):
     """HBM bytes per step from the committed rocprofv3 PMC pass (profiles/)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")   # profiles/summarize.py
+    e = load_entry(workload)
+    if e:
+        return e.get("all_kernels_hbm_bytes_per_step", e.get("hbm_bytes_per_step", e.get("hbm_bytes_per_launch")))
+    return None
+
+
+N_SIMD = 4 * N_CU
+VALU_ISSUE_CYC = 4.0      # one wave64 VALU instruction per 4 cycles on a 16-lane SIMD (MI355X_MICROARCH.md)
+MFMA_F64_CYC = 64.0       # v_mfma_f64_16x16x4 occupies its SIMD's matrix pipe 64 cycles (profiles/r03/r03_mb_pipe.txt)
+
+
+def pipe_roof(workload: str, kern_ms: float):
+    """The issue roof of the dominant kernel from its committed PMC pass: its
+    vector instructions at one per 4 cycles and its matrix-core busy cycles,
+    spread over the chip's 1024 SIMDs at the kernel's effective clock, against
+    the measured time per step.  frac near 1: the kernel issues as fast as the
+    SIMDs can; the gap to 1 is dependency stalls and imbalance."""
+    e = load_entry(workload)
+    if not e:
+        return None
+    c = e.get("counters_per_launch", {})
+    valu = c.get("SQ_INSTS_VALU")
+    if valu is None:
+        return None
+    mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
+    clock = e.get("effective_clock_ghz") or CLOCK_GHZ
+    per = e.get("launches_per_step", 1)
+    cyc = (valu * VALU_ISSUE_CYC + (mfma or 0.0)) / N_SIMD
+    floor_ms = per * cyc / (clock * 1e9) * 1e3
+    return {"bound": "SIMD issue (VALU + matrix core)", "valu_insts_per_launch": valu,
+            "mfma_busy_cycles_per_launch": mfma, "launches_per_step": per,
+            "clock_ghz": clock, "floor_ms": floor_ms, "frac": floor_ms / kern_ms,
+            "source": "profiles/pmc_traffic.json tag %s (rocprofv3 --pmc SQ_INSTS_VALU, SQ_VALU_MFMA_BUSY_CYCLES, "
+                      "GRBM_GUI_ACTIVE)" % e.get("tag")}
+
+
+def row64_issue_roof(B: int, T: int, kern_ms: float):
+    """Config 5's filter wave is one sequence's dependency chain on one SIMD:
+    its per-step instruction stream (static count of the gfx950 ISA,
+    profiles/r04/isa_row64_step.json) at the single-wave issue rates (VALU 4
+    cycles, SALU 1, LDS 4) for T steps, one block per CU."""
+    p = os.path.join(ROOT, "profiles", "r04", "isa_row64_step.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get("entries", {}).get(workload)
-        if e:
-            return e.get("hbm_bytes_per_step", e.get("hbm_bytes_per_launch"))
     except Exception:
-        pass
-    return None
+        return None
+    cyc = d["valu_per_step"] * VALU_ISSUE_CYC + d["salu_per_step"] + d["ds_per_step"] * 4.0
+    rounds = -(-B // N_CU)
+    floor_ms = rounds * T * cyc / (CLOCK_GHZ * 1e9) * 1e3
+    return {"bound": "one filter wave's instruction issue", "cycles_per_step": cyc,
+            "valu_per_step": d["valu_per_step"], "salu_per_step": d["salu_per_step"],
+            "ds_per_step": d["ds_per_step"], "steps": T, "block_rounds": rounds, "clock_ghz": CLOCK_GHZ,
+            "floor_ms": floor_ms, "frac": floor_ms / kern_ms, "source": "profiles/r04/isa_row64_step.json"}
 
 
 def run_workload(name, args, world, rank, dev, steps, warmup):
@@ -251,7 +310,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
             em_state["params"] = p
             em_state["ll"].append(l)
             em_state["exchange_ms"].append(tm.get("exchange_ms", 0.0))
-    elif name not in ("estep", "estep_demo1", "estep_demo1_jt"):
+    elif name not in ("estep", "estep_demo1", "estep_demo1_jt", "estep_config3"):
         post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
 
         def step():
@@ -295,7 +354,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
 
     units = B * T * steps * world
     value = units / elapsed
-    posterior = name not in ("estep", "em", "estep_demo1", "estep_demo1_jt")
+    posterior = name not in ("estep", "em", "estep_demo1", "estep_demo1_jt", "estep_config3")
     bpu, bnote = kernel_bytes(kname, N, len(ov), posterior)
     metric = METRIC
     extra = {}
@@ -306,6 +365,19 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
             N, M, B, T)
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
         kname += " + tree64 + finalize"
+    elif name == "estep_config3":
+        if kname.startswith("chain_msgs_kernel"):
+            NP = 16 if N <= 16 else 32 if N <= 32 else 64
+            bpu = 3 * 4 * len(ov) + 4 * 8 * NP + 8
+            bnote = ("obs %d (read by both filters and the statistics kernel) + alpha^ and beta^ written and read "
+                     "(4 x %d) + alpha's exponent written and read 8; the counts stay on chip"
+                     % (3 * 4 * len(ov), 8 * NP))
+            kname += " + tree64 + map finalize"
+        else:
+            bpu, bnote = 4 * len(ov), "the request's input only: the engine is latency-bound (DESIGN.md 4)"
+        workload = ("config3 e_step: demo1.net structure, 5 vars x 32 states, A1 B1 observed, hidden parent D1, "
+                    "B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
+        metric = "sequence-timesteps/s batched e_step (EM expected counts), demo1 @ 32 states"
     elif name in ("estep_demo1", "estep_demo1_jt"):
         if kname == "chain_estep16_kernel":
             bpu, bnote = 4 * len(ov) + 2 * 128 + 4, ("obs %d + interface message written and read back (128 + 128) "
@@ -393,6 +465,13 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
                            "block_rounds": rounds, "clock_ghz": CLOCK_GHZ, "floor_ms": floor_ms,
                            "frac": floor_ms / kern_ms,
                            "source": "profiles/r03/r03x_mb_lat.txt (mb_lat.hip: V4 for the 16-state step, V3 for the 32-state step)"}
+    pr = pipe_roof(workload, kern_ms)
+    if pr:
+        roof["pipe"] = pr
+    if base == "chain_row64_kernel":
+        ir = row64_issue_roof(B, T, kern_ms)
+        if ir:
+            roof["issue"] = ir
     rec = {"metric": metric, "value": value, "unit": "sequence-timesteps/s", "n_gpus": world,
            "steps": steps, "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -481,7 +560,8 @@ def main():
             r = run_workload(w, args, world, rank, dev, WORKLOADS[w][6], 2 if w != "em" else 1)
             if w in cpu:
                 r["cpu_baseline"] = cpu[w]
-            sec[WORKLOADS[w][0]] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "config",
+            key = WORKLOADS[w][0] if w != "estep_config3" else "config3_estep"
+            sec[key] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "config",
                                                       "roofline", "cpu_baseline", "em", "fold") if k in r}
         rec["secondary"] = sec
     if rank == 0:

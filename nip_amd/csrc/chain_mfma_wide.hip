@@ -46,6 +46,9 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #ifndef NIPAMD_MW_ABLATE
 #define NIPAMD_MW_ABLATE 0     // timing-only builds: 1 partners only keep the barriers,
 #endif                         // 2 filters skip the mat-vec
+#ifndef NIPAMD_MW_SPARSE
+#define NIPAMD_MW_SPARSE 0     // timing-only builds: the filters rescale once per chunk (the ll is then wrong)
+#endif
 constexpr int kWSeq = 16;                  // sequences per group
 constexpr int kWGroups = 2;                // groups per block
 constexpr int kWThreads = 512;
@@ -227,12 +230,13 @@ struct WChain {
 
   // one step with the evidence rows loaded at its start: the MFMAs first, the
   // evidence product after them (its LDS loads complete under the MFMAs)
+  template <bool RS = true>
   __device__ __forceinline__ void step_rows(const WCtx& c, double* L, double* Z, const v4d (&r)[NC][NT]) {
     v4d d[NT];
     matvec(d);
     v4d e[NT];
     product(c, r, e);
-    finish(c, L, Z, d, e);
+    finish<RS>(c, L, Z, d, e);
   }
 
   __device__ __forceinline__ void step(const WCtx& c, double* L, double* Z, const v4d (&e)[NT]) {
@@ -263,6 +267,7 @@ struct WChain {
     }
   }
 
+  template <bool RS = true>
   __device__ __forceinline__ void finish(const WCtx& c, double* L, double* Z, const v4d (&d)[NT],
                                          const v4d (&e)[NT]) {
     double part = 0.0;
@@ -273,9 +278,10 @@ struct WChain {
       const v4d keep = FWD ? p : u;
       *reinterpret_cast<v2d*>(L + c.wo[q][0]) = v2d{keep.x, keep.y};
       *reinterpret_cast<v2d*>(L + c.wo[q][1]) = v2d{keep.z, keep.w};
-      part += (p.x + p.y) + (p.z + p.w);
+      if (RS) part += (p.x + p.y) + (p.z + p.w);
       X[q] = p;
     }
+    if (!RS) { sc = 0; return; }
     const double z2 = swap16_sum(swap32_sum(part));
     if (FWD && c.zw) *Z = z2;
     sc = -__builtin_amdgcn_frexp_exp(z2);
@@ -307,7 +313,13 @@ struct WChain {
         for (int q = 0; q < NC; q++) cd[q] = code(c, q, cc[k][q]);
         v4d r[NC][NT];
         rows_of(c, cd, r);
+#if NIPAMD_MW_SPARSE
+        // timing-only builds: rescale (and publish z2) on the chunk's last step only
+        if (k == CH - 1) step_rows<true>(c, slot + k * G::kStep, zs + k * kWSeq, r);
+        else step_rows<false>(c, slot + k * G::kStep, zs + k * kWSeq, r);
+#else
         step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
+#endif
       }
       barrier_lds(&dg);
       ldc(ci + 2, cc);

@@ -363,20 +363,47 @@ __device__ __forceinline__ void blocks_of(double x, double (&xb)[4]) {
   xb[3] = __hiloint2double((int)q1h[1], (int)q1l[1]);
 }
 
+// The rescale exponent from the largest element instead of the sum: any
+// power of two serves (the ring's vectors and the partners' sums carry it
+// exactly, posteriors and ll are scale-free), and an integer max over the
+// wave is 32-bit DPP work (about 16 instructions) where the f64 wave sum was
+// 43.  Zeros do not count; an all-zero vector keeps the scale (-> 0).
+__device__ __forceinline__ int max_exp_rescale(double p) {
+  int e = p != 0.0 ? __builtin_amdgcn_frexp_exp(p) : -0x40000;
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x128, 0xF, 0xF, true));   // row_ror:8
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x124, 0xF, 0xF, true));   // row_ror:4
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x122, 0xF, 0xF, true));   // row_ror:2
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x121, 0xF, 0xF, true));   // row_ror:1
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)e, (unsigned)e, false, false);
+    e = max((int)r[0], (int)r[1]);
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)e, (unsigned)e, false, false);
+    e = max((int)r[0], (int)r[1]);
+  }
+  return e > -0x40000 ? -e : 0;
+}
+
 // NC: observed columns (0..4).  The step's evidence e_t(y) = ebase(y) x one
 // table entry per column: the codes of the next 8 steps are read a chunk
 // ahead and each entry one step ahead, so no LDS load waits on the
 // recursion's path (evidence() did two dependent LDS round trips per step).
-template <bool FWD, int NC>
-__device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, int y, int nA, int nAi, int nB,
-                                           int nBi) {
-  const int T = a.T, H = a.H;
-  const int d = FWD ? 0 : 1;
-  double Ac[4][16];                       // A(16 b + j, y) (forward) / A(y, 16 b + j) (backward)
+// the filter wave's column (forward) / row (backward) of A: Ac[b][j] =
+// A(16 b + j, y) / A(y, 16 b + j), loaded before the block stages its tables
+// so that the loads' latency overlaps the staging
+__device__ __forceinline__ void r64_load_A(const WideArgs& a, bool fwd, int y, double (&Ac)[4][16]) {
 #pragma unroll
   for (int b = 0; b < 4; b++)
 #pragma unroll
-    for (int j = 0; j < 16; j++) Ac[b][j] = FWD ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
+    for (int j = 0; j < 16; j++) Ac[b][j] = fwd ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
+}
+
+template <bool FWD, int NC>
+__device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, int y, const double (&Ac)[4][16],
+                                           int nA, int nAi, int nB, int nBi) {
+  const int T = a.T, H = a.H;
+  const int d = FWD ? 0 : 1;
   double x;
   int sc = 0;
   if (FWD) {
@@ -405,35 +432,43 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
     ldc(0, cc);
 #pragma unroll
     for (int k = 0; k < NC; k++) tv[k] = row(k, cc[k][0]);
+    // one step i (j = i mod 8, the unrolled position; rs: rescale after it)
+    auto step = [&](int i, int j, bool rs) {
+      double tn[NK];                              // the next step's, loaded under this step's FMAs
+#pragma unroll
+      for (int k = 0; k < NC; k++) tn[k] = row(k, j < 7 ? cc[k][j + 1] : cn[k][0]);
+      double xb[4];
+      blocks_of(x, xb);
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      fmac16(acc, xb[0], Ac[0]);
+      fmac16(acc, xb[1], Ac[1]);
+      fmac16(acc, xb[2], Ac[2]);
+      fmac16(acc, xb[3], Ac[3]);
+      double e = eb;                              // evidence(): the same products in the same order
+#pragma unroll
+      for (int k = 0; k < NC; k++) e *= tv[k];
+      const double u = __builtin_ldexp((acc[0] + acc[1]) + (acc[2] + acc[3]), sc);
+      const double p = u * e;
+      const int slot = i & (kW4Ring - 1);
+      L.ring[(d * kW4Ring + slot) * 64 + y] = FWD ? p : u;
+      if (FWD) L.uring[slot * 64 + y] = u;
+      sc = rs ? max_exp_rescale(p) : 0;
+      x = p;
+#pragma unroll
+      for (int k = 0; k < NC; k++) tv[k] = tn[k];
+    };
     for (int c = 0; c < ni; c += 8) {
       ldc(c + 8, cn);
+      if (c + 8 <= n) {
+        // a full chunk: no bounds checks, the rescales at compile-time positions
+        // (every 4th step; the phase's last step, if it ends here, is j = 7)
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int i = c + j;
-        if (i < n) {
-          double tn[NK];                          // the next step's, loaded under this step's FMAs
+        for (int j = 0; j < 8; j++) step(c + j, j, (j & (kW4Rescale - 1)) == kW4Rescale - 1);
+      } else {
 #pragma unroll
-          for (int k = 0; k < NC; k++) tn[k] = row(k, j < 7 ? cc[k][j + 1] : cn[k][0]);
-          double xb[4];
-          blocks_of(x, xb);
-          double acc[4] = {0.0, 0.0, 0.0, 0.0};
-          fmac16(acc, xb[0], Ac[0]);
-          fmac16(acc, xb[1], Ac[1]);
-          fmac16(acc, xb[2], Ac[2]);
-          fmac16(acc, xb[3], Ac[3]);
-          double e = eb;                          // evidence(): the same products in the same order
-#pragma unroll
-          for (int k = 0; k < NC; k++) e *= tv[k];
-          const double u = __builtin_ldexp((acc[0] + acc[1]) + (acc[2] + acc[3]), sc);
-          const double p = u * e;
-          const int slot = i & (kW4Ring - 1);
-          L.ring[(d * kW4Ring + slot) * 64 + y] = FWD ? p : u;
-          if (FWD) L.uring[slot * 64 + y] = u;
-          const bool rs = (i & (kW4Rescale - 1)) == kW4Rescale - 1 || i == n - 1;
-          sc = rs ? -__builtin_amdgcn_frexp_exp(wave_sum(p)) : 0;   // frexp exponent of 0 is 0
-          x = p;
-#pragma unroll
-          for (int k = 0; k < NC; k++) tv[k] = tn[k];
+        for (int j = 0; j < 8; j++) {
+          const int i = c + j;
+          if (i < n) step(i, j, (i & (kW4Rescale - 1)) == kW4Rescale - 1 || i == n - 1);
         }
       }
 #pragma unroll
@@ -569,6 +604,8 @@ void chain_wide4_kernel(WideArgs a) {
   const long b = blockIdx.x;
   const int T = a.T, Tr = chain_codes_row(T);
   L.Tr = Tr;
+  double Ac[4][16];
+  if (R64 && wave < 2) r64_load_A(a, wave == 0, lane, Ac);
   // stage the evidence tables and this sequence's codes
 #pragma unroll
   for (int k = 0; k < 4; k++)
@@ -597,8 +634,8 @@ void chain_wide4_kernel(WideArgs a) {
   const int nAi = ((nAf > nAb ? nAf : nAb) + 7) & ~7;
   const int nBi = ((nBf > nBb ? nBf : nBb) + 7) & ~7;
   if constexpr (R64) {
-    if (wave == 0) r64_filter<true, NC>(a, L, lane, nAf, nAi, nBf, nBi);
-    else if (wave == 1) r64_filter<false, NC>(a, L, lane, nAb, nAi, nBb, nBi);
+    if (wave == 0) r64_filter<true, NC>(a, L, lane, Ac, nAf, nAi, nBf, nBi);
+    else if (wave == 1) r64_filter<false, NC>(a, L, lane, Ac, nAb, nAi, nBb, nBi);
     else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
     else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
   } else {

@@ -43,6 +43,7 @@ WORKLOADS = {
     "fb": (lambda: synth.hmm_spec(16, 16), ["M1"], "P1", 1024, "fb", 4096),
     "config3": (lambda: synth.demo1_spec(32), ["A1", "B1"], "C1", 256, "fb", 512),
     "em": (lambda: synth.hmm_spec(16, 16), ["M1"], "P1", 1024, "estep", 4096),
+    "estep_config3": (lambda: synth.demo1_spec(32), ["A1", "B1"], "C1", 256, "estep", 512),
     # config 5: the 16.7M-entry clique makes a slice cost seconds: two slices
     # per sequence (the first two of each bench sequence)
     "config5": (lambda: synth.wide_spec(64, 16), ["O1"], "X1", 2, "fb", 64),
@@ -64,7 +65,7 @@ def sample_obs(name, n):
     spec, ov, _, T, _, _ = WORKLOADS[name]
     nodes, _ = spec()
     card = {s: c for s, c, _ in nodes}
-    full_T = {"fb": 1024, "config3": 256, "em": 1024, "config5": 128}[name]
+    full_T = {"fb": 1024, "config3": 256, "em": 1024, "config5": 128, "estep_config3": 256}[name]
     cols = [synth.observations(n, full_T, card[v], seed=1 + 104729 * i) for i, v in enumerate(ov)]
     return np.ascontiguousarray(np.concatenate(cols, axis=2)[:, :T])
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a profiles/collect.sh run into committed files under profiles/.
 
-  python profiles/summarize.py <tag>     (reads gpurun_out/prof_<tag>/<workload>/)
+  python profiles/summarize.py <tag> [--fresh]   (reads gpurun_out/prof_<tag>/<workload>/;
+                                                  --fresh: drop the entries of earlier tags)
 
 For every workload collected, writes profiles/<tag>_<workload>_kernel_stats.csv
 (rocprofv3 --stats) and profiles/<tag>_<workload>_counters.json, and records in
@@ -44,12 +45,12 @@ def dominant(stats_csv):
     return rows[0]["Name"]
 
 
-def main(tag):
+def main(tag, fresh=False):
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     tp = os.path.join(HERE, "pmc_traffic.json")
     try:
         table = json.load(open(tp))
-        if "entries" not in table:
+        if "entries" not in table or fresh:
             table = {"entries": {}}
     except Exception:
         table = {"entries": {}}
@@ -62,7 +63,7 @@ def main(tag):
         kname = dominant(stats)
         rec = bench_line(os.path.join(d, "trace.log"))
         counters = {}
-        for pas in ("pmc1", "pmc2", "pmc3"):
+        for pas in ("pmc1", "pmc2", "pmc3", "pmc4"):
             f = os.path.join(d, pas, "run_counter_collection.csv")
             if not os.path.exists(f):
                 continue
@@ -83,7 +84,30 @@ def main(tag):
                  "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                  "hbm_bytes_per_launch": rd + wr, "launches_per_step": per_step,
                  "hbm_bytes_per_step": (rd + wr) * per_step,
+                 "counters_per_launch": {k: v for k, v in counters.items()
+                                         if k not in ("FETCH_SIZE", "WRITE_SIZE")},
                  "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KiB -> bytes"}
+            # every kernel of the step (e.g. the wide e_step's messages and
+            # statistics kernels), the runtime's copies excepted
+            allk = 0.0
+            f2 = os.path.join(d, "pmc2", "run_counter_collection.csv")
+            f3 = os.path.join(d, "pmc3", "run_counter_collection.csv")
+            if os.path.exists(f2) and os.path.exists(f3):
+                fr = [r for r in csv.DictReader(open(f2)) if r["Counter_Name"] == "FETCH_SIZE"]
+                wrr = [r for r in csv.DictReader(open(f3)) if r["Counter_Name"] == "WRITE_SIZE"]
+                n_disp = len({r["Dispatch_Id"] for r in fr if not r["Kernel_Name"].startswith("__amd")})
+                tot = sum(2 * float(r["Counter_Value"]) * 1024 for r in fr if not r["Kernel_Name"].startswith("__amd"))
+                tot += sum(float(r["Counter_Value"]) * 1024 for r in wrr if not r["Kernel_Name"].startswith("__amd"))
+                steps = float(rec["steps"] + rec["warmup"])
+                allk = tot / steps
+                e["all_kernels_hbm_bytes_per_step"] = allk
+                e["all_kernels_dispatches_per_step"] = n_disp / steps
+            avg_ns = [float(r["AverageNs"]) for r in csv.DictReader(open(stats)) if r["Name"] == kname][0]
+            e["kernel_avg_ns"] = avg_ns
+            g = counters.get("GRBM_GUI_ACTIVE")
+            if g:
+                # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles (MI355X_MICROARCH.md, DVFS note)
+                e["effective_clock_ghz"] = g / 8.0 / avg_ns
             table["entries"][rec["config"]["workload"]] = e
             print(w, json.dumps(e))
     with open(tp, "w") as f:
@@ -91,4 +115,5 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "run")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    main(args[0] if args else "run", fresh="--fresh" in sys.argv)
