@@ -400,7 +400,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
                        "exchange_bytes_per_rank": 8 * (P + 2),
                        "note": "kernel_ms is the whole iteration on the launch stream (e_step kernels over "
                                "8 launches of 16384 sequences, exchange, finalize, host m_step); the "
-                               "exchange packs the e_step partial (%d doubles incl. its 2-slot route tag), "
+                               "exchange packs the e_step partial (%d doubles incl. its 3-slot route tag), "
                                "the ll tree sum and the failure count" % P}
     elif name == "generate":
         bpu, bnote = 4 * model.num_vars, "the int32 draws written; the tables stay in cache"

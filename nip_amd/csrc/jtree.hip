@@ -314,7 +314,7 @@ __global__ __launch_bounds__(64) void jt_post_kernel(JtRun r) {
       }
     }
     if (r.estep && act) {
-      double* s = r.slabs + b * (long)P.slab;
+      double* s = r.slabs + un * (long)P.slab;     // one slab row per unit: (sequence, time chunk)
       for (int j = sub; j < P.slab; j += L) s[j] = ws[P.ws_slab + j];
     }
     wave_sync();

@@ -540,18 +540,26 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   const int S = P->slab;
   if (B == 0) { JT_HIP(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
   const int K = P->p.K;
+  // the posterior sweep's units: (sequence, one of nch time chunks), nch a
+  // power of two that depends on T only, one slab row per unit in (sequence,
+  // chunk) order -- a batch's tree over them contains every power-of-two
+  // shard's as a subtree, so shard partials still combine bit for bit
+  int nch = 1;
+  while (nch * 2 <= std::min(T, 16)) nch *= 2;
+  const int tch = (T + nch - 1) / nch;
   // power-of-two sequence chunks: chunk trees are subtrees of the batch tree
-  long chunk = std::min(seq_chunk(B, T, K), seq_chunk(B, 1, S, 1L << 26));
+  long chunk = std::min(seq_chunk(B, T, K), seq_chunk(B, 1, (int)std::min<long>((long)S * nch, 1L << 30), 1L << 26));
   chunk = std::min<long>(chunk, 16384);
   const long nchunks = (B + chunk - 1) / chunk;
-  const long lvl = (chunk + 63) / 64;
+  const long rows = chunk * nch;
+  const long lvl = (rows + 63) / 64;
   if (int rc = ensure_buf(&s->msg, &s->msg_bytes, (size_t)2 * chunk * T * K * sizeof(double))) return rc;
   if (!P->lds)
     if (int rc = ensure_buf(&s->wsg, &s->wsg_bytes, (size_t)2 * jt_global_units(P->p.ws) * P->p.ws * sizeof(double))) return rc;
   if (int rc = ensure_buf(&s->work, &s->work_bytes,
-                          ((size_t)chunk + 2 * lvl + nchunks + 64) * S * sizeof(double))) return rc;
+                          ((size_t)rows + 2 * lvl + nchunks + 64) * S * sizeof(double))) return rc;
   double* slab = s->work;
-  double* tA = slab + (size_t)chunk * S;
+  double* tA = slab + (size_t)rows * S;
   double* tB = tA + (size_t)lvl * S;
   double* cres = tB + (size_t)lvl * S;
   const long ocols = n_obs > 0 ? n_obs : 1;
@@ -584,11 +592,14 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     r.status = d_status ? (unsigned*)d_status + b0 : nullptr;
     r.slabs = slab;
     r.estep = 1;
-    r.chunk = T;
+    r.chunk = tch;
     if (jt_filter_launch(r, P->L, P->lds, 2, st) || jt_post_launch(r, P->L, P->lds, st))
       return set_error(NIPAMD_ERROR_DEVICE, std::string("jtree e_step launch: ") + hipGetErrorString(hipGetLastError()));
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
-    if (reduce(slab, nb, out)) return set_error(NIPAMD_ERROR_DEVICE, "jtree e_step reduction launch failed");
+    // (T not a multiple of nch: the posterior kernel's unit count is nb x
+    // ceil(T / tch), which equals nch here since tch = ceil(T / nch))
+    if (reduce(slab, nb * ((T + tch - 1) / tch), out))
+      return set_error(NIPAMD_ERROR_DEVICE, "jtree e_step reduction launch failed");
   }
   if (nchunks > 1 && reduce(cres, nchunks, d_partial))
     return set_error(NIPAMD_ERROR_DEVICE, "jtree e_step reduction launch failed");

@@ -161,6 +161,34 @@ def test_estep_general_engine_equals_chain_kernel():
     assert not s1.any().item() and not s2.any().item()
 
 
+@pytest.mark.parametrize("T", [48, 50, 3])
+def test_general_estep_partial_shard_invariant(T):
+    """The general engine's posterior sweep runs one unit per (sequence, time
+    chunk) with a slab row each; the chunk count depends on T only, so four
+    64-sequence shards combine into the 256-sequence batch bit for bit --
+    T = 50 leaves a short last chunk (ceil(50 / 4) = 13 units per sequence)."""
+    m = nip_amd.Model.from_spec(*synth.hmm_spec(16, 16, seed=4))
+    m.set_engine(nip_amd.ENGINE_JTREE)
+    obs = torch.from_numpy(synth.observations(256, T, 16, seed=T)).cuda().contiguous()
+    ov = [m.variable("M1")]
+    whole, _, _ = nip_amd.estep_partial(m, obs, ov)
+    whole = whole.clone()
+    again, _, _ = nip_amd.estep_partial(m, obs, ov)
+    assert torch.equal(whole, again)
+    parts = [nip_amd.estep_partial(m, obs[k * 64:(k + 1) * 64].contiguous(), ov)[0].clone() for k in range(4)]
+    x = torch.stack(parts)
+    comb = (x[0] + x[1]) + (x[2] + x[3])
+    assert torch.equal(comb[:-3], whole[:-3])
+    assert comb[-3:].tolist() == [0.0, 4.0, 0.0]
+    # and the counts match the chain kernel's (a different summation order)
+    m.set_engine(nip_amd.ENGINE_AUTO)
+    c1, _, _ = nip_amd.e_step(m, obs, ov)
+    m.set_engine(nip_amd.ENGINE_JTREE)
+    c2, _, _ = nip_amd.e_step(m, obs, ov)
+    c1, c2 = c1.cpu().numpy(), c2.cpu().numpy()
+    assert np.all(np.abs(c1 - c2) <= CNT_RTOL * np.maximum(1.0, np.abs(c1)))
+
+
 def test_zero_probability_data_general_engine():
     """model.net has zero CPT entries: impossible data -> ll = -DBL_MAX."""
     m = nip_amd.Model.from_net(os.path.join(GOLD, "model.net"))
