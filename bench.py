@@ -120,7 +120,12 @@ WORKLOADS = {
     # on the chain e_step kernel, and on the general engine ("estep_demo1_jt")
     "estep_demo1": ("general", lambda a: synth.demo1_spec(16), ["A1", "B1"], "C1", 16384, 1024, 5),
     "estep_demo1_jt": ("general", lambda a: synth.demo1_spec(16), ["A1", "B1"], "C1", 4096, 1024, 2),
+    # e_step of the opchain workload's request (demo1 @ 6 states, hidden parent
+    # D1 observed): the operator chain's e_step, and the general engine's
+    "estep_opchain": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 5),
+    "estep_opchain_jt": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 2),
 }
+ESTEP_WORKLOADS = ("estep", "estep_demo1", "estep_demo1_jt", "estep_config3", "estep_opchain", "estep_opchain_jt")
 # the default line: the headline, then these under "secondary" 
 SECONDARY = ["config3", "em", "config5", "estep_config3"]
 
@@ -281,7 +286,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
     nodes, pots = spec(args)
     model = nip_amd.Model.from_spec(nodes, pots)
     ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
-    if name in ("jtree", "opchain_jt", "estep_demo1_jt"):
+    if name in ("jtree", "opchain_jt", "estep_demo1_jt", "estep_opchain_jt"):
         model.set_engine(nip_amd.ENGINE_JTREE)     # the chain kernels would take it otherwise
     N, M = model.card(q), model.card(ov[0])
     obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
@@ -310,7 +315,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
             em_state["params"] = p
             em_state["ll"].append(l)
             em_state["exchange_ms"].append(tm.get("exchange_ms", 0.0))
-    elif name not in ("estep", "estep_demo1", "estep_demo1_jt", "estep_config3"):
+    elif name not in ESTEP_WORKLOADS:
         post = torch.empty((B, T, N), dtype=torch.float64, device=dev)
 
         def step():
@@ -354,7 +359,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
 
     units = B * T * steps * world
     value = units / elapsed
-    posterior = name not in ("estep", "em", "estep_demo1", "estep_demo1_jt", "estep_config3")
+    posterior = name not in ESTEP_WORKLOADS + ("em",)
     bpu, bnote = kernel_bytes(kname, N, len(ov), posterior)
     metric = METRIC
     extra = {}
@@ -388,6 +393,19 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         workload = ("e_step of demo1's structure, 5 vars x 16 states, hidden parent D1, A1 B1 observed, "
                     "B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
         metric = "sequence-timesteps/s batched e_step, demo1 structure @ 16 states"
+    elif name in ("estep_opchain", "estep_opchain_jt"):
+        if kname.startswith("op_fb_kernel"):
+            K = N                       # the joint interface is C1 alone
+            bpu = 4 * len(ov) + 2 * 128 + 8 * K * K + 4 * len(ov)
+            bnote = ("obs %d + the 16-wide interface message written and read back (128 + 128) + the step's "
+                     "xi weights written and read (%d) + obs re-read by op_xi_kernel %d"
+                     % (4 * len(ov), 8 * K * K, 4 * len(ov)))
+            kname += " + tree64 + map finalize"
+        else:
+            bpu, bnote = 4 * len(ov), "the request's input only: the engine is latency-bound (DESIGN.md 4)"
+        workload = ("e_step of demo1's structure, 6 states, A1 B1 and the hidden parent D1 observed, "
+                    "B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
+        metric = "sequence-timesteps/s batched e_step, demo1 with its hidden parent observed"
     elif name == "em":
         kname += " + tree64 + finalize"
         workload = ("config4: em_learn iterations of HMM-shaped DBN, %d hidden x %d observed, "

@@ -226,7 +226,8 @@ int nipamd_estep_host(nipamd_model* m, const int32_t* obs, int n_obs,
 /*
  * The two halves of nipamd_estep, for data-parallel EM (one process per GPU,
  * util/niptrain.c:142-195 over a sharded sequence set):
- *   nipamd_estep_partial  B sequences -> d_partial [nipamd_estep_partial_size]
+ *   nipamd_estep_partial  B sequences -> d_partial
+ *                         [nipamd_estep_partial_size_req(m, n_obs, obs_vars, T)]
  *                         (overwritten): the fixed-order binary-tree sum of the
  *                         per-sequence count slabs, before the model's tables
  *                         are applied.  Partials of power-of-two shards combine
@@ -238,12 +239,19 @@ int nipamd_estep_host(nipamd_model* m, const int32_t* obs, int n_obs,
  * kernel route (16-state chain slab, em_learn layout, wide chain slab; the
  * route depends on the engine setting and on T); the finalize fails with
  * NIP_ERROR_INVALID_ARGUMENT on partials of different routes combined,
- * instead of summing mismatched layouts.  nipamd_estep_partial requires
+ * instead of summing mismatched layouts.  The operator chain's e_step
+ * (slices outside the chain plan with a joint interface of <= 16 states,
+ * NIPAMD_ENGINE_AUTO) tags its partials (-1, -1, -1) and appends a section
+ * sized by the request -- its per-evidence-combination sums, whose count
+ * depends on the observed variables -- so its partial is
+ * nipamd_estep_partial_size_req doubles (nipamd_estep_partial_size for every
+ * other route; the _req form is always large enough).  nipamd_estep_partial requires
  * d_status (NIP_ERROR_INVALID_ARGUMENT otherwise) when the model's e_step
  * rejects series with a long leading missing run
  * (nipamd_estep_prefix_first_bad >= 0): the verdict is reported there.
  */
 int nipamd_estep_partial_size(const nipamd_model* m);
+int nipamd_estep_partial_size_req(nipamd_model* m, int n_obs, const int* obs_vars, int T);
 int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,
                          const int* obs_vars, int B, int T, double* d_partial,
                          double* d_ll, uint32_t* d_status, void* stream);

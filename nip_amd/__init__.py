@@ -49,7 +49,7 @@ EXPORTS = [
     "nipamd_model_desc_json", "nipamd_model_param_size", "nipamd_model_gpu_supported",
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error", "nipamd_last_kernel",
-    "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial",
+    "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial_size_req", "nipamd_estep_partial",
     "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_tree_sum", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
@@ -101,6 +101,7 @@ def lib():
         L.nipamd_filter_host.argtypes = L.nipamd_fb_host.argtypes
         L.nipamd_estep.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_partial_size.argtypes = [vp]
+        L.nipamd_estep_partial_size_req.argtypes = [vp, C.c_int, ip, C.c_int]
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
         L.nipamd_estep_prefix_first_bad.argtypes = [vp, C.c_int]
@@ -229,10 +230,14 @@ class Model:
         return bool(lib().nipamd_model_gpu_supported(self._h, len(obs_vars), _ints(obs_vars),
                                                      len(query), _ints(query)))
 
-    def partial_size(self) -> int:
-        """Doubles in an e_step partial (nipamd_estep_partial_size): the count
-        body plus the 3-slot route tag; -1 without an e_step plan."""
-        return lib().nipamd_estep_partial_size(self._h)
+    def partial_size(self, obs_vars=None, T: int = 0) -> int:
+        """Doubles in an e_step partial: the count body plus the 3-slot route
+        tag (nipamd_estep_partial_size), and for a request (obs_vars, T) that
+        runs the operator chain's e_step its section as well
+        (nipamd_estep_partial_size_req); -1 without an e_step plan."""
+        if obs_vars is None:
+            return lib().nipamd_estep_partial_size(self._h)
+        return lib().nipamd_estep_partial_size_req(self._h, len(obs_vars), _ints(obs_vars), int(T))
 
     def estep_prefix_first_bad(self, T: int) -> int:
         """nipamd_estep_prefix_first_bad: the first step k < T at which the
@@ -533,7 +538,7 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
     import torch
     obs = _obs3(obs, obs_vars)
     B, T, nobs = obs.shape
-    S = lib().nipamd_estep_partial_size(model._h)
+    S = lib().nipamd_estep_partial_size_req(model._h, nobs, _ints(obs_vars), T)
     if S < 0:
         raise NipError(NIPAMD_ERROR_UNSUPPORTED, "model has no GPU e_step plan")
     dev = obs.device

@@ -121,6 +121,27 @@ struct W4Lds {
   int eoff;
   lds_u8* codes;     // [ncol][Tr]
   int Tr;
+  // chain_row64_kernel: each column's codes once more per direction and
+  // phase in the filter's processing order, [ncol][2 dirs][PA | PB] bytes
+  // (phase A at 0, phase B at PA; 8-aligned, so a chunk's 8 codes are one
+  // ds_read_b64)
+  lds_u8* pcodes;
+  int PA, PAB;
+};
+
+// block-uniform iteration counts of the two phases (multiples of the
+// partners' 8-step batches) and the filters' per-direction step counts
+struct R64Iters {
+  int nAf, nAb, nBf, nBb, nAi, nBi;
+  __host__ __device__ R64Iters(int T, int H, bool filt) {
+    nAf = filt ? 0 : H; nAb = filt ? 0 : T - 1 - H;
+    nBf = filt ? T : T - H; nBb = filt ? 0 : H;
+    nAi = ((nAf > nAb ? nAf : nAb) + 7) & ~7;
+    nBi = ((nBf > nBb ? nBf : nBb) + 7) & ~7;
+  }
+  // per-phase code rows: the iterations plus two chunks of look-ahead
+  __host__ __device__ int PA() const { return nAi + 16; }
+  __host__ __device__ int PB() const { return nBi + 16; }
 };
 
 // e_t[y] = ebase[y] prod_k tab_k[code_k(t)][y]  (row M_k: the child's row sum,
@@ -209,10 +230,10 @@ __device__ __forceinline__ void w4_filter(const WideArgs& a, const W4Lds& L, int
     }
   };
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
-  phase(nA, nAi, FWD ? 0 : T - 2);
+  phase(nA, nAi, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
-  phase(nB, nBi, FWD ? H : H - 1);
+  phase(nB, nBi, 1);
   if (dg && y == 0 && w == 0) {
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 0] = __builtin_readcyclecounter() - c0;
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 1] = twait;
@@ -415,28 +436,41 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
   const double eb = L.tab[L.eoff + y];
   const int toff[4] = {L.toff0, L.toff1, L.toff2, L.toff3};
   constexpr int NK = NC > 0 ? NC : 1;
-  auto row = [&](int k, int code) { return L.tab[toff[k] + code * 64 + y]; };
   const bool dg = a.diag != nullptr;
   const unsigned long long c0 = dg ? __builtin_readcyclecounter() : 0;
   unsigned long long twait = 0;
-  auto phase = [&](int n, int ni, int t0) {
-    // codes of the chunk's 8 steps from step index c (guards cover the over-run)
-    auto ldc = [&](int c, int (&cd)[NK][8]) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+  auto phase = [&](int n, int ni, int ph) {
+    const lds_u8* pc[NK];
 #pragma unroll
-      for (int k = 0; k < NC; k++)
+    for (int k = 0; k < NK; k++) pc[k] = L.pcodes + (k * 2 + d) * L.PAB + (ph ? L.PA : 0);
+    // a chunk's 8 codes (two dwords, in VGPRs until the next chunk), and its
+    // table entries from them -- both one chunk ahead, so that every LDS
+    // load has a whole chunk and the chunk's barrier (lgkmcnt(0)) behind it
+    // before its value is used, and no wait lands on the recursion's path
+    auto ldw = [&](int c, u32x2 (&w)[NK]) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) cd[k][j] = L.codes[k * L.Tr + kW4G + (FWD ? t0 + c + j : t0 - c - j)];
+      for (int k = 0; k < NC; k++) w[k] = *(const lds_u32x2*)(pc[k] + c);
     };
-    int cc[NK][8], cn[NK][8];
-    double tv[NK];                              // the current step's table entries
-    ldc(0, cc);
+    auto ldt = [&](const u32x2 (&w)[NK], double (&tv)[NK][8]) {
 #pragma unroll
-    for (int k = 0; k < NC; k++) tv[k] = row(k, cc[k][0]);
+      for (int k = 0; k < NC; k++) {
+        const unsigned w0 = __builtin_amdgcn_readfirstlane(w[k].x), w1 = __builtin_amdgcn_readfirstlane(w[k].y);
+#pragma unroll
+        for (int j = 0; j < 8; j++) tv[k][j] = L.tab[toff[k] + (((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 0xff) * 64 + y];
+      }
+    };
+    u32x2 wn[NK];                               // codes of the next chunk
+    double tc[NK][8];                           // table entries of this chunk
+    {
+      u32x2 w0[NK];
+      ldw(0, w0);
+      ldt(w0, tc);
+    }
+    ldw(8, wn);
     // one step i (j = i mod 8, the unrolled position; rs: rescale after it)
     auto step = [&](int i, int j, bool rs) {
-      double tn[NK];                              // the next step's, loaded under this step's FMAs
-#pragma unroll
-      for (int k = 0; k < NC; k++) tn[k] = row(k, j < 7 ? cc[k][j + 1] : cn[k][0]);
       double xb[4];
       blocks_of(x, xb);
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -446,7 +480,7 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
       fmac16(acc, xb[3], Ac[3]);
       double e = eb;                              // evidence(): the same products in the same order
 #pragma unroll
-      for (int k = 0; k < NC; k++) e *= tv[k];
+      for (int k = 0; k < NC; k++) e *= tc[k][j];
       const double u = __builtin_ldexp((acc[0] + acc[1]) + (acc[2] + acc[3]), sc);
       const double p = u * e;
       const int slot = i & (kW4Ring - 1);
@@ -454,11 +488,12 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
       if (FWD) L.uring[slot * 64 + y] = u;
       sc = rs ? max_exp_rescale(p) : 0;
       x = p;
-#pragma unroll
-      for (int k = 0; k < NC; k++) tv[k] = tn[k];
     };
     for (int c = 0; c < ni; c += 8) {
-      ldc(c + 8, cn);
+      double tn[NK][8];
+      ldt(wn, tn);                              // the next chunk's entries
+      u32x2 w2[NK];
+      ldw(c + 16, w2);                          // the codes of the one after
       if (c + 8 <= n) {
         // a full chunk: no bounds checks, the rescales at compile-time positions
         // (every 4th step; the phase's last step, if it ends here, is j = 7)
@@ -472,19 +507,22 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
         }
       }
 #pragma unroll
-      for (int k = 0; k < NC; k++)
+      for (int k = 0; k < NC; k++) {
+        wn[k] = w2[k];
 #pragma unroll
-        for (int j = 0; j < 8; j++) cc[k][j] = cn[k][j];
+        for (int j = 0; j < 8; j++) tc[k][j] = tn[k][j];
+      }
       const unsigned long long tb = dg ? __builtin_readcyclecounter() : 0;
       block_barrier();                                  // the chunk to the partner
       if (dg) twait += __builtin_readcyclecounter() - tb;
     }
   };
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
-  phase(nA, nAi, FWD ? 0 : T - 2);
+  phase(nA, nAi, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
-  phase(nB, nBi, FWD ? H : H - 1);
+  phase(nB, nBi, 1);
+  block_barrier();                                      // the partners' ll hand-over
   if (dg && y == 0) {
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 0] = __builtin_readcyclecounter() - c0;
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 1] = twait;
@@ -495,25 +533,24 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
 // barrier, while the filter writes chunk c + 1 into the ring's other half.
 template <bool FWD>
 __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, int y, long b, int nA, int nAi,
-                                            int nB, int nBi) {
+                                            int nB, int nBi, int nAf, int nBf) {
   const int T = a.T, H = a.H;
   const int d = FWD ? 0 : 1;
   double* const Srow = a.S + (size_t)b * chain_scratch_row64(T) + (size_t)kW4G * 64 + y;
   double* const Prow = (a.post && y < a.N) ? a.post + (size_t)b * a.post_bstride + a.post_off + y : nullptr;
   const double s = a.s[y];
-  double m2 = 1.0, m1 = 1.0, zmin = 1.0;
-  int e2 = 0, e1 = 0;
-  // forward ll (nip.c:1461-1474): z2 = sum alpha_t, z1 = sum u_t s, both on
-  // the same (power-of-two) scale; mantissas and exponents kept apart
-  auto ll_step = [&](int slot) {
-    double z[2] = {L.ring[slot * 64 + y], L.uring[slot * 64 + y] * s};
-    wave_sum_n<2>(z);
-    zmin = __builtin_fmin(zmin, z[0]);
-    m2 *= __builtin_amdgcn_frexp_mant(z[0]); e2 += __builtin_amdgcn_frexp_exp(z[0]);
-    m1 *= __builtin_amdgcn_frexp_mant(z[1]); e1 += __builtin_amdgcn_frexp_exp(z[1]);
-    const int k2 = __builtin_amdgcn_frexp_exp(m2), k1 = __builtin_amdgcn_frexp_exp(m1);
-    m2 = __builtin_ldexp(m2, -k2); e2 += k2;
-    m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+  double m = 1.0, zmin = 1.0;
+  int e = 0;
+  // the forward ll (nip.c:1461-1474) split between the partners: the forward
+  // one sums z2 = sum alpha_t, the backward one z1 = sum u_t s, per forward
+  // step (both on the same power-of-two scale; mantissa and exponent kept
+  // apart); they meet in LDS after the last chunk
+  auto zval = [&](int slot) { return FWD ? L.ring[slot * 64 + y] : L.uring[slot * 64 + y] * s; };
+  auto ll_acc = [&](double z) {
+    if (FWD) zmin = __builtin_fmin(zmin, z);
+    m *= __builtin_amdgcn_frexp_mant(z); e += __builtin_amdgcn_frexp_exp(z);
+    const int k = __builtin_amdgcn_frexp_exp(m);
+    m = __builtin_ldexp(m, -k); e += k;
   };
   const unsigned long long c0 = a.diag ? __builtin_readcyclecounter() : 0;
   if (!FWD && !a.filter) Srow[(long)(T - 1) * 64] = y < a.N ? 1.0 : 0.0;   // beta_{T-1}, T-1 >= H
@@ -523,11 +560,9 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int j = c + k;
-      if (j < nA) {
-        const int slot = j & (kW4Ring - 1);
-        Srow[(long)(FWD ? j : T - 2 - j) * 64] = L.ring[(d * kW4Ring + slot) * 64 + y];
-        if (FWD) ll_step(slot);
-      }
+      const int slot = j & (kW4Ring - 1);
+      if (j < nA) Srow[(long)(FWD ? j : T - 2 - j) * 64] = L.ring[(d * kW4Ring + slot) * 64 + y];
+      if (j < nAf) ll_acc(wave_sum(zval(slot)));
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
@@ -548,13 +583,16 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int j = 8 * c + k;
+      const int slot = j & (kW4Ring - 1);
+      // the posterior's sum and the ll's, interleaved
+      double z[2] = {L.ring[(d * kW4Ring + slot) * 64 + y] * (a.filter ? 1.0 : r[k]), zval(slot)};
+      const double pr = z[0];
+      wave_sum_n<2>(z);
       if (j < nB) {
-        const int slot = j & (kW4Ring - 1);
-        const double pr = L.ring[(d * kW4Ring + slot) * 64 + y] * (a.filter ? 1.0 : r[k]);
-        const double q = pr * recip(wave_sum(pr));   // an all-zero row stays zero
+        const double q = pr * recip(z[0]);           // an all-zero row stays zero
         if (Prow) Prow[(long)tof(j) * a.post_tstride] = q;
-        if (FWD) ll_step(slot);
       }
+      if (j < nBf) ll_acc(z[1]);
     }
   };
   const int nch = nBi / 8;                           // nBi: a multiple of 8 (kernel)
@@ -568,8 +606,17 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
     chunk(rb, c + 1);
   }
   if (a.diag && y == 0) a.diag[blockIdx.x * 16 + (FWD ? 8 : 12)] = __builtin_readcyclecounter() - c0;
+  // z1's mantissa and exponent to the forward partner (L.xb: unused by this
+  // kernel); every wave of the block takes this last barrier
+  if (!FWD && y == 0) {
+    L.xb[0] = m;
+    L.xb[1] = (double)e;
+  }
+  block_barrier();
   if (FWD && y == 0) {
-    double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+    const double m1 = L.xb[0];
+    const int e1 = (int)L.xb[1];
+    double ll = log(m) - log(m1) + (double)(e - e1) * 0.69314718055994530942;
     const bool dead = zmin == 0.0;
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
@@ -626,18 +673,25 @@ void chain_wide4_kernel(WideArgs a) {
   }
   __syncthreads();
   const int H = a.H;
-  const bool filt = a.filter != 0;
-  // per-direction steps and the block-uniform iteration counts of each phase
-  const int nAf = filt ? 0 : H, nAb = filt ? 0 : T - 1 - H;
-  const int nBf = filt ? T : T - H, nBb = filt ? 0 : H;
-  // block-uniform iteration counts, multiples of the partners' 8-step batches
-  const int nAi = ((nAf > nAb ? nAf : nAb) + 7) & ~7;
-  const int nBi = ((nBf > nBb ? nBf : nBb) + 7) & ~7;
+  const R64Iters it(T, H, a.filter != 0);
+  const int nAf = it.nAf, nAb = it.nAb, nBf = it.nBf, nBb = it.nBb, nAi = it.nAi, nBi = it.nBi;
   if constexpr (R64) {
+    // the filters' codes in processing order (R64Iters; guards: row M_k)
+    L.PA = it.PA();
+    L.PAB = it.PA() + it.PB();
+    L.pcodes = codes + ((a.ncol * Tr + 7) & ~7);
+    for (int k = 0; k < a.ncol; k++)
+      for (int i = tid; i < 2 * L.PAB; i += kThreads) {
+        const int dd = i >= L.PAB, r = i - dd * L.PAB, ph = r >= L.PA, j = r - ph * L.PA;
+        const int n = dd ? (ph ? nBb : nAb) : (ph ? nBf : nAf);
+        const int t = dd ? (ph ? H - 1 - j : T - 2 - j) : (ph ? H + j : j);
+        L.pcodes[k * 2 * L.PAB + i] = j < n ? codes[k * Tr + kW4G + t] : (uint8_t)a.M[k];
+      }
+    __syncthreads();
     if (wave == 0) r64_filter<true, NC>(a, L, lane, Ac, nAf, nAi, nBf, nBi);
     else if (wave == 1) r64_filter<false, NC>(a, L, lane, Ac, nAb, nAi, nBb, nBi);
-    else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi);
-    else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi);
+    else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi, nAf, nBf);
+    else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi, nAf, nBf);
   } else {
     if (wave < kQ) w4_filter<true>(a, L, wave, lane, nAf, nAi, nBf, nBi);
     else if (wave < 2 * kQ) w4_filter<false>(a, L, wave - kQ, lane, nAb, nAi, nBb, nBi);
@@ -651,9 +705,11 @@ void chain_wide4_kernel(WideArgs a) {
 size_t chain_wide4_lds_bytes(const WideArgs& a) {
   int rows = 0;
   for (int k = 0; k < a.ncol; k++) rows += a.M[k] + 2;
+  const R64Iters it(a.T, a.H, a.filter != 0);
   return (size_t)(2 * kQ * 64 + 2 * 2 * kQ * 64 + 2 * kW4Ring * 64 + kW4Ring * 64 + (rows + 1) * 64) *
              sizeof(double) +
-         (size_t)(a.ncol > 0 ? a.ncol : 1) * chain_codes_row(a.T);
+         (((size_t)(a.ncol > 0 ? a.ncol : 1) * chain_codes_row(a.T) + 7) & ~(size_t)7) +
+         (size_t)a.ncol * 2 * (it.PA() + it.PB());          // chain_row64_kernel's pcodes
 }
 
 #ifndef NIPAMD_R64

@@ -1268,6 +1268,28 @@ int nipamd_estep_partial_size(const nipamd_model* mm) {
   return estep_body_size(mm) + kTagSlots;
 }
 
+static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r);
+static bool wide_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, Route& r);
+
+// The request's route is the operator chain's e_step (the chain and wide
+// routes decline it, the engine choice is automatic and the operator chain
+// takes it): its partial carries a section after the route tag.
+static bool op_estep_route(nipamd_model* mm, int n_obs, const int* obs_vars, int T) {
+  Route r;
+  if (mm->engine != NIPAMD_ENGINE_AUTO || chain_estep_ok(mm, n_obs, obs_vars, T, r) ||
+      wide_estep_ok(mm, n_obs, obs_vars, r))
+    return false;
+  std::string why;
+  return nipamd::op_estep_supported(mm, n_obs, obs_vars, T, why);
+}
+
+int nipamd_estep_partial_size_req(nipamd_model* mm, int n_obs, const int* obs_vars, int T) {
+  if (!mm || T < 1 || (n_obs > 0 && !obs_vars)) return -1;
+  const int base = nipamd_estep_partial_size(mm);
+  if (base < 0 || !op_estep_route(mm, n_obs, obs_vars, T)) return base;
+  return base + (int)nipamd::op_estep_section(mm, n_obs, obs_vars);
+}
+
 // e_step kernel of the chain route: 3 = chain_estep16_kernel (16-lane DPP
 // rows, direction-uniform waves, analytic phase-B normalisation; the
 // default), 2 = chain_kernel<true> (the round-2 DPP kernel, mixed-direction
@@ -1476,6 +1498,20 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       return estep_wide_partial(mm, rw, d_obs, n_obs, B, T, d_partial, d_ll, d_status, stream);
     if (mm->engine == NIPAMD_ENGINE_CHAIN)
       return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step covers interface chains with evidence on their children");
+    if (op_estep_route(mm, n_obs, obs_vars, T)) {
+      // the operator chain (opchain.cpp): body zeros, the tag (-1, -1, -1)
+      // that no other route's tag combines with, then its section
+      const int body = estep_body_size(mm);
+      hipStream_t st = (hipStream_t)stream;
+      HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)body * sizeof(double), st));
+      if (nipamd::estep_tag_launch(d_partial + body, -1.0, -1.0, -1.0, st))
+        return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
+      std::string err;
+      if (int rc = nipamd::op_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial + body + kTagSlots, d_ll,
+                                            d_status, stream, err))
+        return fail(rc, err);
+      return 0;
+    }
     std::string why;
     if (!nipamd::jt_supported(mm, n_obs, obs_vars, 0, nullptr, why)) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
     if (int rc = nipamd::jt_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
@@ -1909,6 +1945,13 @@ int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_c
   int route = -1, nz = 0;
   for (int k = 0; k < kTagSlots; k++)
     if (tag[k] != 0.0) { nz++; if (tag[k] >= 1.0) route = k; }
+  if (tag[0] <= -1.0 && tag[1] == tag[0] && tag[2] == tag[0]) {
+    // the operator chain's partial (its header names the request)
+    std::string err;
+    if (int rc = nipamd::op_estep_finalize(mm, d_partial + body + kTagSlots, d_counts, stream, err))
+      return fail(rc, err);
+    return 0;
+  }
   if (nz != 1 || route < 0)
     return fail(NIP_ERROR_INVALID_ARGUMENT, "e_step partial: partials of different routes (chain slab / em_learn "
                                             "layout / wide chain slab) were combined, or the buffer is not an "
@@ -1963,8 +2006,8 @@ int nipamd_estep_finalize(nipamd_model* mm, const double* d_partial, double* d_c
 
 int nipamd_estep(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                  int B, int T, double* d_counts, double* d_ll, uint32_t* d_status, void* stream) {
-  if (!mm || !d_counts) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
-  const int S = nipamd_estep_partial_size(mm);
+  if (!mm || !d_counts || T < 1) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const int S = nipamd_estep_partial_size_req(mm, n_obs, obs_vars, T);
   if (S < 0) return fail(NIPAMD_ERROR_UNSUPPORTED, "no e_step plan for this model under the selected engine");
   if (int rc = ensure_device(mm)) return rc;
   DevState* d = dev_of(mm);

@@ -18,9 +18,11 @@
 //
 // Two kernels:
 //  * chain_msgs_kernel<NP>: the two filters, every message stored.  One wave
-//    per direction holds 64 / NP sequences, lane = state; the mat-vec reads
-//    the input by LDS broadcast against the lane's column (forward) or row
-//    (backward) of A in registers.  alpha^_t = alpha_t 2^Ef_t (Ef_t stored,
+//    per direction holds 64 / NP sequences, lane = state; the mat-vec takes
+//    the input by DPP row broadcast (v_fmac_f64_dpp row_newbcast, after
+//    v_permlane16/32_swap put the sequence's 16-state blocks in each of its
+//    rows) against the lane's column (forward) or row (backward) of A in
+//    registers -- no LDS on the recursion's path.  alpha^_t = alpha_t 2^Ef_t (Ef_t stored,
 //    one int per step) and beta^_t (t = -1 .. T-1, scale free for the
 //    statistics) go to HBM; the forward wave keeps the ll (m2 / m1 per step,
 //    nip.c:1461-1474) as chain_wide.hip does.
@@ -35,10 +37,12 @@
 //    another); the waves' sums meet in LDS in a fixed order and the block
 //    writes one slab row, which tree64_kernel reduces like every e_step slab.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cfloat>
 #include <cstdint>
 
 #include "chain_kernels.h"
+#include "dpp_row.h"
 
 namespace nipamd {
 
@@ -46,7 +50,7 @@ namespace {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-constexpr int kMsgWaves = 8;                 // 4 forward + 4 backward
+constexpr int kMsgWaves = 4;                 // 2 forward + 2 backward (no LDS: blocks just group waves)
 constexpr int kMsgChunk = 8;                 // steps of evidence prefetched ahead
 constexpr int kStatSeqs = 16;                // sequences per stats block (one slab row)
 constexpr int kStatWaves = 4;
@@ -101,42 +105,110 @@ __device__ __forceinline__ double evidence(const EWideArgs& a, const int* o, int
   return e;
 }
 
+// acc[j & 3] += x(lane j of the row) * Ac[j], j = 0..15 (four chains, the
+// broadcast by DPP row_newbcast, as chain_row64_kernel does)
+__device__ __forceinline__ void fmac16(double (&acc)[4], double xb, const double (&Ac)[16]) {
+  fmac_bcast<0, true>(acc[0], xb, Ac[0]);    fmac_bcast<1, false>(acc[1], xb, Ac[1]);
+  fmac_bcast<2, false>(acc[2], xb, Ac[2]);   fmac_bcast<3, false>(acc[3], xb, Ac[3]);
+  fmac_bcast<4, false>(acc[0], xb, Ac[4]);   fmac_bcast<5, false>(acc[1], xb, Ac[5]);
+  fmac_bcast<6, false>(acc[2], xb, Ac[6]);   fmac_bcast<7, false>(acc[3], xb, Ac[7]);
+  fmac_bcast<8, false>(acc[0], xb, Ac[8]);   fmac_bcast<9, false>(acc[1], xb, Ac[9]);
+  fmac_bcast<10, false>(acc[2], xb, Ac[10]); fmac_bcast<11, false>(acc[3], xb, Ac[11]);
+  fmac_bcast<12, false>(acc[0], xb, Ac[12]); fmac_bcast<13, false>(acc[1], xb, Ac[13]);
+  fmac_bcast<14, false>(acc[2], xb, Ac[14]); fmac_bcast<15, false>(acc[3], xb, Ac[15]);
+}
+
+// the NB = NP / 16 blocks of 16 states of this lane's sequence, each in
+// every lane of the sequence's rows: xb[b](lane 16 r + j) = x(state 16 b + j).
+// One row per sequence (NB 1): x itself; two rows (NB 2): one
+// v_permlane16_swap per half ([0]: the pair's even row, [1]: its odd row);
+// four rows (NB 4): a v_permlane32_swap level on both results.
+template <int NB>
+__device__ __forceinline__ void seq_blocks(double x, double (&xb)[NB]) {
+  if constexpr (NB == 1) {
+    xb[0] = x;
+  } else {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    if constexpr (NB == 2) {
+      xb[0] = __hiloint2double((int)ph[0], (int)pl[0]);
+      xb[1] = __hiloint2double((int)ph[1], (int)pl[1]);
+    } else {
+      const auto q0l = __builtin_amdgcn_permlane32_swap(pl[0], pl[0], false, false);   // blocks 0, 2
+      const auto q0h = __builtin_amdgcn_permlane32_swap(ph[0], ph[0], false, false);
+      const auto q1l = __builtin_amdgcn_permlane32_swap(pl[1], pl[1], false, false);   // blocks 1, 3
+      const auto q1h = __builtin_amdgcn_permlane32_swap(ph[1], ph[1], false, false);
+      xb[0] = __hiloint2double((int)q0h[0], (int)q0l[0]);
+      xb[2] = __hiloint2double((int)q0h[1], (int)q0l[1]);
+      xb[1] = __hiloint2double((int)q1h[0], (int)q1l[0]);
+      xb[3] = __hiloint2double((int)q1h[1], (int)q1l[1]);
+    }
+  }
+}
+
+// u(y) = sum_x Ac[x / 16][x % 16] x(x) over this lane's sequence: NP
+// v_fmac_f64_dpp in registers, no LDS on the recursion's path
+template <int NB>
+__device__ __forceinline__ double matvec_dpp(double x, const double (&Ac)[NB][16]) {
+  double xb[NB];
+  seq_blocks<NB>(x, xb);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int b = 0; b < NB; b++) fmac16(acc, xb[b], Ac[b]);
+  return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
 template <int NP>
 __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a) {
   constexpr int SPW = 64 / NP;                        // sequences per wave
-  __shared__ __attribute__((aligned(16))) double xbuf[kMsgWaves][64];
+  constexpr int NB = NP / 16;                         // 16-lane rows per sequence
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool fwd = wave < 4;
+  constexpr int WD = kMsgWaves / 2;                  // waves per direction
+  const bool fwd = wave < WD;
   const int s = lane / NP, y = lane % NP;
-  const long b = (long)blockIdx.x * (4 * SPW) + (wave & 3) * SPW + s;
+  const long b = (long)blockIdx.x * (WD * SPW) + (wave % WD) * SPW + s;
   const bool active = b < a.B;
   const long bb = active ? b : 0;
   const int T = a.T, N = a.N;
-  double* const xb = xbuf[wave];
-  double Acol[NP];
+  // the lane's column (forward) / row (backward) of A, in 16-state blocks
+  double Ac[NB][16];
 #pragma unroll
-  for (int x = 0; x < NP; x++) Acol[x] = (x < N && y < N) ? (fwd ? a.A[x * 64 + y] : a.A[y * 64 + x]) : 0.0;
-  const int* obs = a.obs + bb * a.obs_bstride;
-  auto ev = [&](int t) {
-    if (!active || y >= N) return 0.0;
-    return evidence(a, obs + (long)t * a.obs_tstride, y);
-  };
-  // u = sum_x Acol[x] xb[x] over this sequence's NP lanes of the LDS buffer
-  auto matvec = [&](double v) {
-    xb[lane] = v;
-    __builtin_amdgcn_wave_barrier();
-    const double* q = xb + s * NP;
-    double a0 = 0.0, a1 = 0.0;
+  for (int k = 0; k < NB; k++)
 #pragma unroll
-    for (int x = 0; x < NP; x += 2) {
-      const double2 w = *reinterpret_cast<const double2*>(q + x);
-      a0 = __builtin_fma(Acol[x], w.x, a0);
-      a1 = __builtin_fma(Acol[x + 1], w.y, a1);
+    for (int j = 0; j < 16; j++) {
+      const int x = 16 * k + j;
+      Ac[k][j] = (x < N && y < N) ? (fwd ? a.A[x * 64 + y] : a.A[y * 64 + x]) : 0.0;
     }
-    __builtin_amdgcn_wave_barrier();
-    return a0 + a1;
+  const int* obs = a.obs + bb * a.obs_bstride;
+  const double eb = (active && y < N) ? a.ebase[y] : 0.0;
+  // evidence of a chunk of steps in processing order (forward t = j, backward
+  // t = T - 1 - j): the children's codes two chunks ahead, the table entries
+  // (and e) one chunk ahead, so no global load's latency meets the recursion
+  int cd[4][kMsgChunk];
+  auto ldcodes = [&](int j0) {
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      if (c < a.ncol)
+#pragma unroll
+        for (int k = 0; k < kMsgChunk; k++) {
+          const int t = fwd ? j0 + k : T - 1 - (j0 + k);
+          cd[c][k] = (t >= 0 && t < T) ? code_of(obs[(long)t * a.obs_tstride + a.col[c]], a.M[c]) : a.M[c];
+        }
+  };
+  auto evc = [&](double (&e)[kMsgChunk]) {
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) e[k] = eb;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      if (c < a.ncol)
+#pragma unroll
+        for (int k = 0; k < kMsgChunk; k++) e[k] *= a.tab[a.tab_off[c] + cd[c][k] * 64 + y];
   };
   double e[kMsgChunk], en[kMsgChunk];
+  ldcodes(0);
+  evc(e);
+  ldcodes(kMsgChunk);
   if (fwd) {
     double* Sa = a.Sa + (size_t)bb * T * NP + y;
     int* Ea = a.Ea + (size_t)bb * T;
@@ -145,16 +217,14 @@ __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a)
     int sc = 0, E = 0;
     double m2 = 1.0, m1 = 1.0, zmin = 1.0;
     int e2 = 0, e1 = 0;
-#pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) e[k] = k < T ? ev(k) : 0.0;
     for (int t0 = 0; t0 < T; t0 += kMsgChunk) {
-#pragma unroll
-      for (int k = 0; k < kMsgChunk; k++) en[k] = t0 + kMsgChunk + k < T ? ev(t0 + kMsgChunk + k) : 0.0;
+      evc(en);
+      ldcodes(t0 + 2 * kMsgChunk);
 #pragma unroll
       for (int k = 0; k < kMsgChunk; k++) {
         const int t = t0 + k;
         if (t >= T) break;
-        const double u = __builtin_ldexp(matvec(x), sc);
+        const double u = __builtin_ldexp(matvec_dpp<NB>(x, Ac), sc);
         const double p = u * e[k];
         const double z2 = group_sum<NP>(p);
         const double z1 = group_sum<NP>(u * sy);
@@ -188,14 +258,9 @@ __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a)
     double* Sb = a.Sb + (size_t)bb * (T + 1) * NP + y;
     double xbeta = (active && y < N) ? 1.0 : 0.0;
     if (active) Sb[(size_t)T * NP] = xbeta;
-#pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) e[k] = T - 1 - k >= 0 ? ev(T - 1 - k) : 0.0;
     for (int j0 = 0; j0 < T; j0 += kMsgChunk) {
-#pragma unroll
-      for (int k = 0; k < kMsgChunk; k++) {
-        const int t = T - 1 - (j0 + kMsgChunk + k);
-        en[k] = t >= 0 ? ev(t) : 0.0;
-      }
+      evc(en);
+      ldcodes(j0 + 2 * kMsgChunk);
 #pragma unroll
       for (int k = 0; k < kMsgChunk; k++) {
         const int t = T - 1 - (j0 + k);
@@ -203,7 +268,7 @@ __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a)
         const double g = e[k] * xbeta;
         const double z = group_sum<NP>(g);
         const int sc = z != 0.0 ? -__builtin_amdgcn_frexp_exp(z) : 0;
-        const double u = __builtin_ldexp(matvec(g), sc);
+        const double u = __builtin_ldexp(matvec_dpp<NB>(g, Ac), sc);
         if (active) Sb[(size_t)t * NP] = u;
         xbeta = u;
       }
@@ -219,14 +284,33 @@ __device__ __forceinline__ v4d mfma(double a, double b, v4d d) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
 }
 
-template <int NT, int HR>
+// the children's evidence tables [(M_k + 2)][64] and ebase [64], staged in
+// LDS for the statistics kernel (doubles)
+__host__ __device__ inline int stats_tab_doubles(const EWideArgs& a) {
+  int n = 0;
+  for (int c = 0; c < a.ncol; c++) n = max(n, a.tab_off[c] + (a.M[c] + 2) * 64);
+  return n + 64;
+}
+
+// TL: the tables fit the LDS (otherwise they are read from HBM / L2)
+template <int NT, int HR, bool TL>
 __global__ __launch_bounds__(kStatWaves * 64, 1) void chain_stats_kernel(EWideArgs a) {
   constexpr int NP = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* red = reinterpret_cast<double*>(smem);     // [2][NT*NT + HR*NT][4][64]: the waves' sums
+  // the evidence tables share the LDS with the reduction (used before it)
+  double* tabs = reinterpret_cast<double*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int k4 = lane >> 4, i = lane & 15;
   const int T = a.T, N = a.N;
+  if (TL) {
+    const int nt = stats_tab_doubles(a) - 64;
+    for (int j = tid; j < nt; j += kStatWaves * 64) tabs[j] = a.tab[j];
+    for (int j = tid; j < 64; j += kStatWaves * 64) tabs[nt + j] = a.ebase[j];
+    __syncthreads();
+  }
+  const double* tabl = TL ? tabs : a.tab;
+  const double* ebl = TL ? tabs + (stats_tab_doubles(a) - 64) : a.ebase;
   constexpr int NK = NT * NT, NH = HR * NT;
   v4d K[NK], Hc[NH];
 #pragma unroll
@@ -236,69 +320,90 @@ __global__ __launch_bounds__(kStatWaves * 64, 1) void chain_stats_kernel(EWideAr
   double p0 = 0.0;                                   // P0 of state `lane` (lane < NP)
   const int hr = (a.R + 15) >> 4;                    // row tiles in use (<= HR)
 
-  for (int sq = 0; sq < kStatSeqs / kStatWaves; sq++) {
-    const long b = (long)blockIdx.x * kStatSeqs + wave * (kStatSeqs / kStatWaves) + sq;
-    if (b >= a.B) break;                             // wave-uniform
+  // this wave's sequences one after another, 4 steps per iteration (lane:
+  // step t0 + k4); every global operand of iteration it + 1 is loaded while
+  // iteration it runs on the matrix cores
+  const long b0 = (long)blockIdx.x * kStatSeqs + wave * (kStatSeqs / kStatWaves);
+  const long nb = a.B - b0;
+  const int nseq = nb <= 0 ? 0 : (nb < kStatSeqs / kStatWaves ? (int)nb : kStatSeqs / kStatWaves);
+  const int nit = (T + 3) >> 2;
+  const int total = nseq * nit;
+  struct Ops {
+    double ap[NT], al[NT], be[NT];
+    int ef, oc[4], orow[4];
+  };
+  auto load = [&](int it, Ops& o) {
+    const int sq = it / nit, t0 = (it - sq * nit) * 4;
+    const long b = b0 + sq;
     const double* Sa = a.Sa + (size_t)b * T * NP;
     const double* Sb = a.Sb + (size_t)b * (T + 1) * NP;
     const int* Ea = a.Ea + (size_t)b * T;
-    const int* obs = a.obs + b * a.obs_bstride;
-    // P0: gamma_{-1} = prior o beta^_{-1} / its sum (lanes 0 .. NP-1: state = lane)
-    {
+    const int t = t0 + k4;
+    const int tc = t < T ? t : T - 1;
+#pragma unroll
+    for (int q = 0; q < NT; q++) {
+      const int st = 16 * q + i;
+      o.ap[q] = tc >= 1 ? Sa[(size_t)(tc - 1) * NP + st] : (st < N ? a.pi[st] : 0.0);
+      o.al[q] = Sa[(size_t)tc * NP + st];
+      o.be[q] = Sb[(size_t)(tc + 1) * NP + st];
+    }
+    o.ef = Ea[tc] - (tc >= 1 ? Ea[tc - 1] : 0);
+    const int* ob = a.obs + b * a.obs_bstride + (long)tc * a.obs_tstride;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      o.oc[c] = c < a.ncol ? code_of(ob[a.col[c]], a.M[c]) : 0;
+      o.orow[c] = c < a.nchild ? a.erow[c] + (a.ccol[c] >= 0 ? code_of(ob[a.ccol[c]], a.cM[c]) : a.cM[c]) : -1;
+    }
+  };
+  Ops cur, nxt;
+  if (total > 0) load(0, cur);
+  for (int it = 0; it < total; it++) {
+    if (it + 1 < total) load(it + 1, nxt);
+    const int sq = it / nit, t0 = (it - sq * nit) * 4;
+    if (t0 == 0) {
+      // P0: gamma_{-1} = prior o beta^_{-1} / its sum (lanes 0 .. NP-1: state = lane)
+      const double* Sb = a.Sb + (size_t)(b0 + sq) * (T + 1) * NP;
       const int x = lane < NP ? lane : 0;
       const double v = (lane < NP && x < N) ? a.pi[x] * Sb[x] : 0.0;
       const double z = group_sum<64>(v);
       p0 += v * recip(z);
     }
-    for (int t0 = 0; t0 < T; t0 += 4) {
-      const int t = t0 + k4;
-      const bool ok = t < T;
-      const int tc = ok ? t : T - 1;
-      // operands of this lane's step: alpha^_{t-1} (A of K), alpha^_t, beta^_t
-      double ap[NT], al[NT], be[NT], ev[NT];
+    const bool ok = t0 + k4 < T;
+    double ev[NT];
 #pragma unroll
-      for (int q = 0; q < NT; q++) {
-        const int st = 16 * q + i;
-        ap[q] = tc >= 1 ? Sa[(size_t)(tc - 1) * NP + st] : (st < N ? a.pi[st] : 0.0);
-        al[q] = Sa[(size_t)tc * NP + st];
-        be[q] = Sb[(size_t)(tc + 1) * NP + st];
-      }
-      const int ef = Ea[tc] - (tc >= 1 ? Ea[tc - 1] : 0);
-      const int* o = obs + (long)tc * a.obs_tstride;
-#pragma unroll
-      for (int q = 0; q < NT; q++) {
-        const int st = 16 * q + i;
-        ev[q] = st < N ? evidence(a, o, st) : 0.0;
-      }
-      // the one-hot rows of the children's codes at t
-      int row[4];
+    for (int q = 0; q < NT; q++) {
+      const int st = 16 * q + i;
+      double e = ebl[st];
 #pragma unroll
       for (int c = 0; c < 4; c++)
-        row[c] = c < a.nchild ? a.erow[c] + (a.ccol[c] >= 0 ? code_of(o[a.ccol[c]], a.cM[c]) : a.cM[c]) : -1;
-      double pr[NT];
-      double zz = 0.0;
-#pragma unroll
-      for (int q = 0; q < NT; q++) { pr[q] = al[q] * be[q]; zz += pr[q]; }
-      const double c = group_sum<16>(zz);
-      const double rc = ok ? recip(c) : 0.0;
-      const double f = __builtin_ldexp(rc, ef);
-      double w[NT], g[NT];
-#pragma unroll
-      for (int q = 0; q < NT; q++) { w[q] = ev[q] * be[q] * f; g[q] = pr[q] * rc; }
-#pragma unroll
-      for (int xi = 0; xi < NT; xi++)
-#pragma unroll
-        for (int yj = 0; yj < NT; yj++) K[xi * NT + yj] = mfma(ap[xi], w[yj], K[xi * NT + yj]);
-#pragma unroll
-      for (int mi = 0; mi < HR; mi++) {
-        if (mi >= hr) break;
-        const int r = 16 * mi + i;
-        const double oh = (r == row[0] || r == row[1] || r == row[2] || r == row[3]) ? 1.0 : 0.0;
-#pragma unroll
-        for (int yj = 0; yj < NT; yj++) Hc[mi * NT + yj] = mfma(oh, g[yj], Hc[mi * NT + yj]);
-      }
+        if (c < a.ncol) e *= tabl[a.tab_off[c] + cur.oc[c] * 64 + st];
+      ev[q] = st < N ? e : 0.0;
     }
+    double pr[NT];
+    double zz = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; q++) { pr[q] = cur.al[q] * cur.be[q]; zz += pr[q]; }
+    const double c = group_sum<16>(zz);
+    const double rc = ok ? recip(c) : 0.0;
+    const double f = __builtin_ldexp(rc, cur.ef);
+    double w[NT], g[NT];
+#pragma unroll
+    for (int q = 0; q < NT; q++) { w[q] = ev[q] * cur.be[q] * f; g[q] = pr[q] * rc; }
+#pragma unroll
+    for (int xi = 0; xi < NT; xi++)
+#pragma unroll
+      for (int yj = 0; yj < NT; yj++) K[xi * NT + yj] = mfma(cur.ap[xi], w[yj], K[xi * NT + yj]);
+#pragma unroll
+    for (int mi = 0; mi < HR; mi++) {
+      if (mi >= hr) break;
+      const int r = 16 * mi + i;
+      const double oh = (r == cur.orow[0] || r == cur.orow[1] || r == cur.orow[2] || r == cur.orow[3]) ? 1.0 : 0.0;
+#pragma unroll
+      for (int yj = 0; yj < NT; yj++) Hc[mi * NT + yj] = mfma(oh, g[yj], Hc[mi * NT + yj]);
+    }
+    cur = nxt;
   }
+  __syncthreads();                                   // the tables' LDS becomes the reduction's
   // the waves' sums in a fixed order: (w0 + w2) + (w1 + w3)
   constexpr int NA = NK + NH;
   auto put = [&](int slot) {
@@ -359,11 +464,17 @@ __global__ __launch_bounds__(kStatWaves * 64, 1) void chain_stats_kernel(EWideAr
 template <int NT, int HR>
 int stats_launch(const EWideArgs& a, hipStream_t stream) {
   constexpr int NA = NT * NT + HR * NT;
-  const size_t lds = (size_t)2 * NA * 256 * sizeof(double) + 4 * 64 * sizeof(double);
-  static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_stats_kernel<NT, HR>), lds, set)) return -1;
+  const size_t red = (size_t)2 * NA * 256 * sizeof(double) + 4 * 64 * sizeof(double);
+  const size_t tabs = (size_t)stats_tab_doubles(a) * sizeof(double);
+  const bool tl = std::max(red, tabs) <= 160 * 1024;
+  const size_t lds = tl ? std::max(red, tabs) : red;
+  static size_t set[2][kMaxDevices] = {};
+  const void* k = tl ? reinterpret_cast<const void*>(&chain_stats_kernel<NT, HR, true>)
+                     : reinterpret_cast<const void*>(&chain_stats_kernel<NT, HR, false>);
+  if (ensure_dyn_lds(k, lds, set[tl])) return -1;
   const int blocks = (int)((a.B + kStatSeqs - 1) / kStatSeqs);
-  hipLaunchKernelGGL((chain_stats_kernel<NT, HR>), dim3(blocks), dim3(kStatWaves * 64), lds, stream, a);
+  if (tl) hipLaunchKernelGGL((chain_stats_kernel<NT, HR, true>), dim3(blocks), dim3(kStatWaves * 64), lds, stream, a);
+  else hipLaunchKernelGGL((chain_stats_kernel<NT, HR, false>), dim3(blocks), dim3(kStatWaves * 64), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -393,7 +504,7 @@ int estep_wide_launch(const EWideArgs& a, hipStream_t stream) {
   const int NP = estep_wide_np(a.N);
   if (!estep_wide_fits(a.N, a.R) || a.nchild > 4 || a.ncol > 4) return -2;
   {
-    const int spb = 4 * (64 / NP);
+    const int spb = kMsgWaves / 2 * (64 / NP);
     const int blocks = (int)((a.B + spb - 1) / spb);
     if (NP == 16) hipLaunchKernelGGL(chain_msgs_kernel<16>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
     else if (NP == 32) hipLaunchKernelGGL(chain_msgs_kernel<32>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);

@@ -544,8 +544,10 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   // power of two that depends on T only, one slab row per unit in (sequence,
   // chunk) order -- a batch's tree over them contains every power-of-two
   // shard's as a subtree, so shard partials still combine bit for bit
-  int nch = 1;
-  while (nch * 2 <= std::min(T, 16)) nch *= 2;
+  // (and exactly nch units: ceil(T / ceil(T / nch)) == nch, true whenever
+  // (nch - 1)^2 < T, so a short T takes fewer chunks)
+  int nch = 16;
+  while (nch > 1 && (nch - 1) * ((T + nch - 1) / nch) >= T) nch /= 2;
   const int tch = (T + nch - 1) / nch;
   // power-of-two sequence chunks: chunk trees are subtrees of the batch tree
   long chunk = std::min(seq_chunk(B, T, K), seq_chunk(B, 1, (int)std::min<long>((long)S * nch, 1L << 30), 1L << 26));
@@ -596,9 +598,7 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     if (jt_filter_launch(r, P->L, P->lds, 2, st) || jt_post_launch(r, P->L, P->lds, st))
       return set_error(NIPAMD_ERROR_DEVICE, std::string("jtree e_step launch: ") + hipGetErrorString(hipGetLastError()));
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
-    // (T not a multiple of nch: the posterior kernel's unit count is nb x
-    // ceil(T / tch), which equals nch here since tch = ceil(T / nch))
-    if (reduce(slab, nb * ((T + tch - 1) / tch), out))
+    if (reduce(slab, nb * nch, out))
       return set_error(NIPAMD_ERROR_DEVICE, "jtree e_step reduction launch failed");
   }
   if (nchunks > 1 && reduce(cres, nchunks, d_partial))

@@ -182,6 +182,12 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
           long jbs, int jts, int joff, double* d_ll, uint32_t* d_status, void* stream, bool filt, int* K_out,
           std::string& err);
 bool op_fits(nipamd_model* mm, int n_obs, const int* obs_vars, int T);
+// its e_step: a partial section of op_estep_section doubles after the route tag
+bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T, std::string& why);
+long op_estep_section(nipamd_model* mm, int n_obs, const int* obs_vars);
+int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T,
+                     double* d_sec, double* d_ll, uint32_t* d_status, void* stream, std::string& err);
+int op_estep_finalize(nipamd_model* mm, const double* d_sec, double* d_counts, void* stream, std::string& err);
 void op_release(nipamd_model* mm);
 // jtree_plan.cpp: the general join-tree engine (jtree.h)
 int jt_supported(const nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,

@@ -48,7 +48,21 @@ struct OpPlan {
   double* dpi = nullptr;
   double* S = nullptr;
   size_t S_bytes = 0;
-  ~OpPlan() { (void)hipFree(dT); (void)hipFree(dw); (void)hipFree(dpi); (void)hipFree(S); }
+  // e_step: the projection of the per-combination xi sums onto the em_learn
+  // layout (CSR over count cells, built on demand per model version) and the
+  // launch buffers (W rows, P0, slab rows, tree work)
+  int map_state = 0;                 // 0 not built, 1 built, -1 unsupported
+  std::string map_why;
+  int map_n = 0;
+  int* d_mptr = nullptr;
+  int* d_midx = nullptr;
+  double* d_mcoef = nullptr;
+  double* E = nullptr;
+  size_t E_bytes = 0;
+  ~OpPlan() {
+    (void)hipFree(dT); (void)hipFree(dw); (void)hipFree(dpi); (void)hipFree(S);
+    (void)hipFree(d_mptr); (void)hipFree(d_midx); (void)hipFree(d_mcoef); (void)hipFree(E);
+  }
 };
 
 struct OpCache {
@@ -236,6 +250,296 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
   const int rc = op_fb_launch(a, (hipStream_t)stream);
   if (rc == -2) { err = "operators do not fit the kernel's LDS"; return NIPAMD_ERROR_UNSUPPORTED; }
   if (rc) { err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()); return NIPAMD_ERROR_DEVICE; }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// e_step on the operator chain.  The reference's e_step (nip.c:1708-2007)
+// sums every variable's normalised family marginal over the steps
+// (nip.c:1925-1967; the previous interface's prior families at t = 0 only).
+// On the operator chain the slice's joint posterior at step t is
+//   P_t(a) = alpha^_{t-1}(x(a)) W(a) [a consistent with c_t] beta^_t(y(a)) / Z'_t
+// (W as in build()), so every family count is linear in the per-combination
+// sums Xi_c(x, y) = sum over the steps with combination c of
+// alpha^_{t-1}(x) beta^_t(y) / Z'_t (op_fb_kernel's xi weights, summed per
+// 16-sequence group by op_xi_kernel and over the batch by the fixed-order
+// tree):  count(v, family cell) = sum over assignments a in the cell and
+// combinations c consistent with a of W(a) Xi_c(x(a), y(a)); the previous
+// interface's families come from P0 (its t = 0 marginal).  That projection
+// is a CSR map over the count cells, built per model version by the same
+// enumeration as the operators; the finalize applies it.
+//
+// Partial section (after the model's route tag, nipamd_estep_partial_size_req):
+//   [count, n_obs, ov[kOpMaxObs], K, ncomb | Xi [(ncomb + 1) K K] | P0 [K]]
+// -- the header's entries are summed with the partials and read back divided
+// by the count (exact for these small integers).
+namespace {
+
+constexpr int kOpHdr = 4 + kOpMaxObs;
+constexpr long kOpMaxMapEntries = 1L << 27;
+
+bool build_map(const Model& m, OpPlan& P) {
+  const auto& prev = m.previous_outgoing;
+  const auto& cur = m.outgoing;
+  const int nv = (int)m.vars.size(), K = P.K, no = (int)P.ov.size();
+  std::vector<long> off(nv + 1, 0);
+  for (int v = 0; v < nv; v++) {
+    long sz = m.vars[v].card;
+    for (int q : m.vars[v].parents) sz *= m.vars[q].card;
+    off[v + 1] = off[v] + sz;
+  }
+  for (int v = 0; v < nv; v++)
+    if ((m.vars[v].ifs & IF_OLD_OUTGOING) &&
+        (!m.vars[v].parents.empty() || std::find(prev.begin(), prev.end(), v) == prev.end())) {
+      P.map_why = "previous-interface variable with parents or outside the interface";
+      return false;
+    }
+  struct Ent { long row; int idx; double coef; };
+  std::vector<Ent> ents;
+  std::vector<std::vector<std::pair<int, long>>> cst(m.cliques.size());
+  for (size_t c = 0; c < m.cliques.size(); c++) {
+    long st = 1;
+    for (int v : m.cliques[c].vars) { cst[c].push_back({v, st}); st *= m.vars[v].card; }
+  }
+  std::vector<int> pri;
+  for (int v : m.independent)
+    if (m.vars[v].has_prior && !(m.vars[v].ifs & IF_OLD_OUTGOING)) pri.push_back(v);
+  std::vector<int> cnt;                               // the counted variables (every step)
+  for (int v = 0; v < nv; v++)
+    if (!(m.vars[v].ifs & IF_OLD_OUTGOING)) cnt.push_back(v);
+  long total = 1;
+  for (const Var& V : m.vars) total *= V.card;
+  std::vector<int> a(nv, 0);
+  const long KK = (long)K * K;
+  for (long it = 0; it < total; it++) {
+    double W = 1.0;                                   // the same product, in the same order, as build()
+    for (size_t c = 0; c < m.cliques.size() && W != 0.0; c++) {
+      long idx = 0;
+      for (const auto& e : cst[c]) idx += a[e.first] * e.second;
+      W *= m.cliques[c].original[(size_t)idx];
+    }
+    for (size_t i = 0; i < pri.size() && W != 0.0; i++) W *= m.vars[pri[i]].prior[a[pri[i]]];
+    if (W != 0.0) {
+      long x = 0, y = 0, sx = 1, sy = 1;
+      for (size_t i = 0; i < cur.size(); i++) {
+        x += a[prev[i]] * sx; sx *= m.vars[prev[i]].card;
+        y += a[cur[i]] * sy; sy *= m.vars[cur[i]].card;
+      }
+      for (long mask = 0; mask < (1L << no); mask++) {
+        long c = 0;
+        for (int i = 0; i < no; i++)
+          if (mask >> i & 1) c += (long)(a[P.ov[i]] + 1) * P.stride[i];
+        const int idx = (int)(c * KK + x * K + y);
+        for (int v : cnt) {
+          long cell = a[v], st = m.vars[v].card;
+          for (int q : m.vars[v].parents) { cell += (long)a[q] * st; st *= m.vars[q].card; }
+          ents.push_back({off[v] + cell, idx, W});
+        }
+        if ((long)ents.size() > kOpMaxMapEntries) { P.map_why = "e_step projection too large"; return false; }
+      }
+    }
+    for (int v = 0; v < nv; v++) {                    // odometer, variable 0 fastest
+      if (++a[v] < m.vars[v].card) break;
+      a[v] = 0;
+    }
+  }
+  // the previous interface at t = 0: P0 digits
+  const int p0 = (int)((P.ncomb + 1) * KK);
+  for (int x = 0; x < K; x++) {
+    long r = x;
+    for (int v : prev) {
+      const int card = m.vars[v].card;
+      ents.push_back({off[v] + r % card, p0 + x, 1.0});
+      r /= card;
+    }
+  }
+  // CSR by a stable counting sort on the row
+  const long nrows = off[nv];
+  std::vector<int> ptr((size_t)nrows + 1, 0);
+  for (const Ent& e : ents) ptr[(size_t)e.row + 1]++;
+  for (long r = 0; r < nrows; r++) ptr[(size_t)r + 1] += ptr[(size_t)r];
+  std::vector<int> fill(ptr.begin(), ptr.end() - 1), idx(ents.size());
+  std::vector<double> coef(ents.size());
+  for (const Ent& e : ents) {
+    const int q = fill[(size_t)e.row]++;
+    idx[(size_t)q] = e.idx;
+    coef[(size_t)q] = e.coef;
+  }
+  if (hipMalloc(&P.d_mptr, ptr.size() * sizeof(int)) != hipSuccess ||
+      hipMemcpy(P.d_mptr, ptr.data(), ptr.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMalloc(&P.d_midx, std::max<size_t>(1, idx.size()) * sizeof(int)) != hipSuccess ||
+      (!idx.empty() && hipMemcpy(P.d_midx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) ||
+      upload(&P.d_mcoef, coef)) {
+    P.map_why = "device map";
+    return false;
+  }
+  P.map_n = (int)nrows;
+  return true;
+}
+
+// sequences per launch: a power of two (chunk trees are subtrees of the
+// batch tree), the W rows within ~2 GB
+long op_estep_chunk(int K, int T) {
+  const size_t per = (size_t)T * K * K * sizeof(double) + (size_t)(T + 2) * 16 * sizeof(double);
+  long c = 16;
+  while (c < 16384 && (size_t)(c * 2) * per <= ((size_t)2 << 30)) c *= 2;
+  return c;
+}
+
+}  // namespace
+
+bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T, std::string& why) {
+  OpPlan* P = plan_for(mm, n_obs, obs_vars);
+  if (!P->ok) { why = P->why; return false; }
+  if (!op_fits(mm, n_obs, obs_vars, T)) { why = "sequence too long for the operator chain's LDS codes"; return false; }
+  if (!op_xi_fits(P->K, P->ncomb)) { why = "too many evidence combinations for the e_step's LDS sums"; return false; }
+  const long total = [&] { long t = 1; for (const Var& V : mm->m.vars) t *= V.card; return t; }();
+  if (total * (1L << P->ov.size()) * (long)mm->m.vars.size() > kOpMaxMapEntries) {
+    why = "e_step projection too large";
+    return false;
+  }
+  return true;
+}
+
+long op_estep_section(nipamd_model* mm, int n_obs, const int* obs_vars) {
+  OpPlan* P = plan_for(mm, n_obs, obs_vars);
+  if (!P->ok) return 0;
+  return kOpHdr + op_xi_row(P->K, P->ncomb);
+}
+
+int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T,
+                     double* d_sec, double* d_ll, uint32_t* d_status, void* stream, std::string& err) {
+  OpPlan* P = plan_for(mm, n_obs, obs_vars);
+  if (!P->ok) { err = P->why; return NIPAMD_ERROR_UNSUPPORTED; }
+  hipStream_t st = (hipStream_t)stream;
+  const int K = P->K, R = op_xi_row(K, P->ncomb);
+  // the header (pageable host source: staged before the call returns)
+  double hdr[kOpHdr];
+  hdr[0] = 1.0;
+  hdr[1] = n_obs;
+  for (int i = 0; i < kOpMaxObs; i++) hdr[2 + i] = i < n_obs ? obs_vars[i] : -1.0;
+  hdr[2 + kOpMaxObs] = K;
+  hdr[3 + kOpMaxObs] = P->ncomb;
+  if (hipMemcpyAsync(d_sec, hdr, sizeof(hdr), hipMemcpyHostToDevice, st) != hipSuccess) {
+    err = "header copy";
+    return NIPAMD_ERROR_DEVICE;
+  }
+  double* out = d_sec + kOpHdr;
+  if (B == 0) {
+    if (hipMemsetAsync(out, 0, (size_t)R * sizeof(double), st) != hipSuccess) { err = "memset"; return NIPAMD_ERROR_DEVICE; }
+    return 0;
+  }
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) { err = "no device"; return NIPAMD_ERROR_DEVICE; }
+  if (P->device != dev || !P->dT) {
+    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->S); (void)hipFree(P->E);
+    P->dT = P->dw = P->dpi = P->S = P->E = nullptr;
+    P->S_bytes = P->E_bytes = 0;
+    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi)) {
+      err = "device tables";
+      return NIPAMD_ERROR_DEVICE;
+    }
+    P->device = dev;
+  }
+  const long chunk = std::min<long>(op_estep_chunk(K, T), std::max(16, B));
+  const long nchunks = (B + chunk - 1) / chunk;
+  const long rows = (chunk + kOpXiSeqs - 1) / kOpXiSeqs;
+  const long lvl = (rows + 63) / 64;
+  const size_t nW = (size_t)chunk * T * K * K, nP0 = (size_t)chunk * K;
+  const size_t nE = nW + nP0 + (size_t)(rows + 2 * lvl + nchunks + 2 * ((nchunks + 63) / 64) + 1) * R;
+  if (P->S_bytes < op_scratch_bytes(chunk, T)) {
+    (void)hipFree(P->S);
+    P->S = nullptr;
+    P->S_bytes = 0;
+    if (hipMalloc(&P->S, op_scratch_bytes(chunk, T)) != hipSuccess) { err = "scratch"; return NIPAMD_ERROR_DEVICE; }
+    P->S_bytes = op_scratch_bytes(chunk, T);
+  }
+  if (P->E_bytes < nE * sizeof(double)) {
+    (void)hipFree(P->E);
+    P->E = nullptr;
+    P->E_bytes = 0;
+    if (hipMalloc(&P->E, nE * sizeof(double)) != hipSuccess) { err = "e_step buffers"; return NIPAMD_ERROR_DEVICE; }
+    P->E_bytes = nE * sizeof(double);
+  }
+  double* W = P->E;
+  double* P0 = W + nW;
+  double* slab = P0 + nP0;
+  double* work = slab + (size_t)rows * R;
+  double* cres = work + (size_t)2 * lvl * R;
+  double* cwork = cres + (size_t)nchunks * R;
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  for (long c = 0; c < nchunks; c++) {
+    const long b0 = c * chunk;
+    const long nb = (B - b0) < chunk ? (B - b0) : chunk;
+    OpArgs a{};
+    a.obs = d_obs ? d_obs + b0 * T * ocols : nullptr;
+    a.obs_bstride = (long)T * ocols;
+    a.obs_tstride = (int)ocols;
+    a.nobs = n_obs;
+    for (int i = 0; i < n_obs; i++) { a.col[i] = i; a.card[i] = P->card[i]; a.cstride[i] = P->stride[i]; }
+    a.B = nb; a.T = T; a.H = T / 2; a.K = K; a.ncomb = P->ncomb;
+    a.filter = 0;
+    a.Ttab = P->dT; a.w = P->dw; a.pi = P->dpi;
+    a.S = P->S;
+    a.post = nullptr;
+    a.ll = d_ll ? d_ll + b0 : nullptr;
+    a.status = d_status ? d_status + b0 : nullptr;
+    a.estep = 1;
+    a.W = W;
+    a.P0 = P0;
+    const int rc = op_fb_launch(a, st);
+    if (rc == -2) { err = "operators do not fit the kernel's LDS"; return NIPAMD_ERROR_UNSUPPORTED; }
+    if (rc) { err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()); return NIPAMD_ERROR_DEVICE; }
+    OpXiArgs x{};
+    x.obs = a.obs; x.obs_bstride = a.obs_bstride; x.obs_tstride = a.obs_tstride; x.nobs = n_obs;
+    for (int i = 0; i < n_obs; i++) { x.col[i] = i; x.card[i] = P->card[i]; x.cstride[i] = P->stride[i]; }
+    x.B = nb; x.T = T; x.K = K; x.ncomb = P->ncomb;
+    x.W = W; x.P0 = P0; x.slab = slab;
+    if (op_xi_launch(x, st)) { err = "xi launch failed"; return NIPAMD_ERROR_DEVICE; }
+    const long nr = (nb + kOpXiSeqs - 1) / kOpXiSeqs;
+    if (nipamd_tree_sum(slab, nr, R, work, nchunks == 1 ? out : cres + (size_t)c * R, stream)) {
+      err = "tree launch failed";
+      return NIPAMD_ERROR_DEVICE;
+    }
+  }
+  if (nchunks > 1 && nipamd_tree_sum(cres, nchunks, R, cwork, out, stream)) {
+    err = "tree launch failed";
+    return NIPAMD_ERROR_DEVICE;
+  }
+  g_last_kernel = "op_fb_kernel (e_step) + op_xi_kernel";
+  return 0;
+}
+
+int op_estep_finalize(nipamd_model* mm, const double* d_sec, double* d_counts, void* stream, std::string& err) {
+  double hdr[kOpHdr];
+  if (hipMemcpyAsync(hdr, d_sec, sizeof(hdr), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+      hipStreamSynchronize((hipStream_t)stream) != hipSuccess) {
+    err = "header read";
+    return NIPAMD_ERROR_DEVICE;
+  }
+  const double n = hdr[0];
+  auto val = [&](double v, int& out) {
+    const double q = v / n;
+    out = (int)q;
+    return q == (double)out;
+  };
+  int nobs = 0, ov[kOpMaxObs], K = 0, ncomb = 0;
+  bool ok = n >= 1.0 && n == (double)(long)n && val(hdr[1], nobs) && nobs >= 0 && nobs <= kOpMaxObs &&
+            val(hdr[2 + kOpMaxObs], K) && val(hdr[3 + kOpMaxObs], ncomb);
+  for (int i = 0; ok && i < nobs; i++) ok = val(hdr[2 + i], ov[i]);
+  if (!ok) { err = "operator-chain e_step partial: inconsistent header (partials of different requests combined?)"; return NIP_ERROR_INVALID_ARGUMENT; }
+  OpPlan* P = plan_for(mm, nobs, ov);
+  if (!P->ok || P->K != K || P->ncomb != ncomb) {
+    err = "operator-chain e_step partial does not match this model";
+    return NIP_ERROR_INVALID_ARGUMENT;
+  }
+  if (P->map_state == 0) P->map_state = build_map(mm->m, *P) ? 1 : -1;
+  if (P->map_state < 0) { err = P->map_why; return NIPAMD_ERROR_UNSUPPORTED; }
+  if (estep_map_finalize_launch(d_sec + kOpHdr, P->map_n, P->d_mptr, P->d_midx, P->d_mcoef, d_counts,
+                                (hipStream_t)stream)) {
+    err = "finalize launch failed";
+    return NIPAMD_ERROR_DEVICE;
+  }
   return 0;
 }
 

@@ -47,10 +47,39 @@ struct OpArgs {
   int post_off;
   double* ll;
   unsigned* status;
+  // e_step (estep = 1, smoothing only): instead of posteriors, every step's
+  // xi weights W_t(x, y) = alpha^_{t-1}(x) beta^_t(y) / Z'_t (Z'_t: the step's
+  // xi mass, so sum_{x,y} W_t T_{c_t} = 1) into W [B][T][K*K] (x-major), and
+  // the previous interface's t = 0 marginal into P0 [B][K]
+  int estep;
+  double* W;
+  double* P0;
 };
 
 size_t op_lds_bytes(int K, int ncomb, int T, bool tables);
 size_t op_scratch_bytes(long B, int T);
 int op_fb_launch(const OpArgs& a, hipStream_t stream);
+
+// The e_step's per-combination sums (op_xi_kernel): one slab row per 16
+// sequences, Xi[c][x][y] = sum over the group's steps with evidence
+// combination c of W_t(x, y), then P0 [K] summed over the group.
+struct OpXiArgs {
+  const int32_t* obs;      // as OpArgs
+  long obs_bstride;
+  int obs_tstride;
+  int nobs;
+  int col[kOpMaxObs];
+  int card[kOpMaxObs];
+  int cstride[kOpMaxObs];
+  long B;
+  int T, K, ncomb;
+  const double* W;         // [B][T][K*K]
+  const double* P0;        // [B][K]
+  double* slab;            // [ceil(B / 16)][op_xi_row(K, ncomb)]
+};
+constexpr int kOpXiSeqs = 16;
+__host__ __device__ inline int op_xi_row(int K, int ncomb) { return (ncomb + 1) * K * K + K; }
+bool op_xi_fits(int K, int ncomb);
+int op_xi_launch(const OpXiArgs& a, hipStream_t stream);
 
 }  // namespace nipamd

@@ -75,6 +75,19 @@ __device__ __forceinline__ double dot16(double x, const double (&c)[16]) {
 
 __device__ __forceinline__ double div_or_keep(double x, double c) { return c != 0.0 ? x / c : x; }
 
+// the value of lane J of this lane's 16-lane row (v_mov_b64_dpp row_newbcast)
+template <int J>
+__device__ __forceinline__ double bcast(double v) { return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xF, 0xF, false); }
+
+// e_step: lane y of a row writes W(x', y) = a(x') b(y) for x' < K (a(x') from
+// lane x' of the row) to dst[x' K + y]
+__device__ __forceinline__ void xi_row(double av, double bv, double* dst, int K, int y, bool w) {
+#define NIPAMD_XI(J) { const double v = bcast<J>(av) * bv; if (w && J < K) dst[J * K + y] = v; }
+  NIPAMD_XI(0) NIPAMD_XI(1) NIPAMD_XI(2) NIPAMD_XI(3) NIPAMD_XI(4) NIPAMD_XI(5) NIPAMD_XI(6) NIPAMD_XI(7)
+  NIPAMD_XI(8) NIPAMD_XI(9) NIPAMD_XI(10) NIPAMD_XI(11) NIPAMD_XI(12) NIPAMD_XI(13) NIPAMD_XI(14) NIPAMD_XI(15)
+#undef NIPAMD_XI
+}
+
 __host__ __device__ __forceinline__ int op_row(int T) { return T + 2 * kOpGuard; }
 
 }  // namespace
@@ -161,7 +174,8 @@ void op_fb_kernel(OpArgs a) {
     return (int)cd[fwd ? tc : (tc + 1 < T ? tc + 1 : T - 1)];
   };
   double Cn[16];                 // the next step's coefficients, loaded one step ahead
-  auto step = [&](int t, int tnext, bool valid, bool combine) {
+  const bool est = a.estep != 0;
+  auto step = [&](int t, int tnext, bool valid, bool combine, bool first) {
     const int tc = t < 0 ? 0 : (t > T - 1 ? T - 1 : t);
     const int c = code_at(t);
     double C[16];
@@ -187,8 +201,20 @@ void op_fb_kernel(OpArgs a) {
     } else {
       const double o = Srow[(long)tc * 16];
       const double pr = u * o;
-      const double q = div_or_keep(pr, rsum(pr));
-      (valid ? Pst : sink)[(long)tc * (valid ? pstr : 0)] = q;
+      const double z = rsum(pr);
+      if (est) {
+        // the step's xi weights: sum_y u o = 2^sc Z' (Z' the xi mass at the
+        // messages' own scale); forward rows W_t = alpha^_{t-1} (x) beta^_t,
+        // backward rows W_{t+1} = alpha^_t (x) beta^_{t+1} -- except at their
+        // first phase-B step (t = H - 1): W_H is the forward rows'
+        const double f = z != 0.0 ? __builtin_ldexp(1.0 / z, sc) : 0.0;
+        const int tw = fwd ? tc : tc + 1;
+        xi_row(fwd ? x : o, (fwd ? o : x) * f, a.W + ((size_t)b * T + tw) * KK, K, y,
+               valid && active && ys && (fwd || !first));
+      } else {
+        const double q = div_or_keep(pr, z);
+        (valid ? Pst : sink)[(long)tc * (valid ? pstr : 0)] = q;
+      }
     }
     if (valid) {
       sc = z != 0.0 ? -__builtin_amdgcn_frexp_exp(z) : 0;
@@ -198,7 +224,7 @@ void op_fb_kernel(OpArgs a) {
 
   if (a.filter) {
     coef(code_at(0), Cn);
-    for (int t = 0; t < T; t++) step(t, t + 1, fwd, false);
+    for (int t = 0; t < T; t++) step(t, t + 1, fwd, false, false);
   } else {
     // phase A: forward t = 0..H-1, backward t = T-2..H
     const int nA = H > T - 1 - H ? H : T - 1 - H;
@@ -206,7 +232,7 @@ void op_fb_kernel(OpArgs a) {
     coef(code_at(fwd ? 0 : T - 2), Cn);
     for (int j = 0; j < nA; j++) {
       const int t = fwd ? j : T - 2 - j;
-      step(t, t + dir, fwd ? j < H : t >= H, false);
+      step(t, t + dir, fwd ? j < H : t >= H, false, false);
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -215,7 +241,22 @@ void op_fb_kernel(OpArgs a) {
     coef(code_at(fwd ? H : H - 1), Cn);
     for (int j = 0; j < nB; j++) {
       const int t = fwd ? H + j : H - 1 - j;
-      step(t, t + dir, fwd ? t < T : t >= 0, true);
+      step(t, t + dir, fwd ? t < T : t >= 0, true, j == 0);
+    }
+    if (est && !fwd) {
+      // one more backward step with alpha_{-1} = prior of the previous
+      // interface (x = beta^_0): its posterior is the t = 0 marginal of the
+      // previous interface (P0), its xi weights W_0 (the forward rows took
+      // t = 0 when H = 0)
+      double C0[16];
+      coef(cd[0], C0);
+      const double u0 = __builtin_ldexp(dot16(x, C0), sc);
+      const double piy = ys ? a.pi[y] : 0.0;
+      const double pr = piy * u0;
+      const double z = rsum(pr);
+      if (active && ys) a.P0[(size_t)b * K + y] = div_or_keep(pr, z);
+      const double f = z != 0.0 ? __builtin_ldexp(1.0 / z, sc) : 0.0;
+      xi_row(piy, x * f, a.W + (size_t)b * T * KK, K, y, H > 0 && active && ys);
     }
   }
   if (fwd && active && y == 0) {
@@ -224,6 +265,75 @@ void op_fb_kernel(OpArgs a) {
     if (a.ll) a.ll[b] = ll;
     if (a.status) a.status[b] = dead ? 1u : 0u;        // NIPAMD_STATUS_ZERO_MASS
   }
+}
+
+// The e_step's per-combination sums: a block per 16 sequences, lane l < K*K
+// owns cell l of every combination's K x K block in LDS and adds the group's
+// W_t(l) in sequence and step order (one lane per cell: no races, a fixed
+// summation order); then P0 over the group; one slab row out.
+__global__ __launch_bounds__(256)
+void op_xi_kernel(OpXiArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* X = reinterpret_cast<double*>(smem);
+  const int KK = a.K * a.K, R = op_xi_row(a.K, a.ncomb);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < R; i += 256) X[i] = 0.0;
+  __syncthreads();
+  const long b0 = (long)blockIdx.x * kOpXiSeqs;
+  const int T = a.T;
+  const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
+  if (tid < KK) {
+    for (int s = 0; s < nseq; s++) {
+      const long b = b0 + s;
+      const double* Wr = a.W + (size_t)b * T * KK + tid;
+      const int32_t* ob = a.obs ? a.obs + b * a.obs_bstride : nullptr;
+      // the evidence combination of step t (op_fb_kernel's code)
+      auto comb = [&](int t) {
+        int c = 0;
+        if (ob) {
+          const int32_t* o = ob + (long)t * a.obs_tstride;
+          for (int k = 0; k < a.nobs; k++) {
+            const int v = o[a.col[k]];
+            if (v >= a.card[k]) { c = a.ncomb; break; }
+            if (v >= 0) c += (v + 1) * a.cstride[k];
+          }
+        }
+        return c;
+      };
+      constexpr int U = 8;                           // steps loaded ahead of their sums
+      for (int t0 = 0; t0 < T; t0 += U) {
+        double w[U];
+        int c[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+          const int t = t0 + k < T ? t0 + k : T - 1;
+          w[k] = Wr[(size_t)t * KK];
+          c[k] = comb(t);
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++)
+          if (t0 + k < T) X[(size_t)c[k] * KK + tid] += w[k];
+      }
+    }
+  }
+  if (tid < a.K)
+    for (int s = 0; s < nseq; s++) X[(size_t)(a.ncomb + 1) * KK + tid] += a.P0[(size_t)(b0 + s) * a.K + tid];
+  __syncthreads();
+  double* out = a.slab + (size_t)blockIdx.x * R;
+  for (int i = tid; i < R; i += 256) out[i] = X[i];
+}
+
+bool op_xi_fits(int K, int ncomb) { return (size_t)op_xi_row(K, ncomb) * sizeof(double) <= 160 * 1024; }
+
+int op_xi_launch(const OpXiArgs& a, hipStream_t stream) {
+  if (a.B <= 0) return 0;
+  if (!op_xi_fits(a.K, a.ncomb) || a.K > 16) return -2;
+  const size_t lds = ((size_t)op_xi_row(a.K, a.ncomb) * sizeof(double) + 15) & ~(size_t)15;
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_kernel), lds, lds_set)) return -1;
+  const int blocks = (int)((a.B + kOpXiSeqs - 1) / kOpXiSeqs);
+  hipLaunchKernelGGL(op_xi_kernel, dim3(blocks), dim3(256), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 size_t op_lds_bytes(int K, int ncomb, int T, bool tables) {
