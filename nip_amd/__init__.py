@@ -101,7 +101,8 @@ def lib():
         L.nipamd_filter_host.argtypes = L.nipamd_fb_host.argtypes
         L.nipamd_estep.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_partial_size.argtypes = [vp]
-        L.nipamd_estep_partial_size_req.argtypes = [vp, C.c_int, ip, C.c_int]
+        if hasattr(L, "nipamd_estep_partial_size_req"):      # (absent from A/B builds of older revisions)
+            L.nipamd_estep_partial_size_req.argtypes = [vp, C.c_int, ip, C.c_int]
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
         L.nipamd_estep_prefix_first_bad.argtypes = [vp, C.c_int]
@@ -538,7 +539,9 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
     import torch
     obs = _obs3(obs, obs_vars)
     B, T, nobs = obs.shape
-    S = lib().nipamd_estep_partial_size_req(model._h, nobs, _ints(obs_vars), T)
+    L = lib()
+    S = (L.nipamd_estep_partial_size_req(model._h, nobs, _ints(obs_vars), T)
+         if hasattr(L, "nipamd_estep_partial_size_req") else L.nipamd_estep_partial_size(model._h))
     if S < 0:
         raise NipError(NIPAMD_ERROR_UNSUPPORTED, "model has no GPU e_step plan")
     dev = obs.device

@@ -51,6 +51,10 @@ struct ChainArgs {
   // tables (rows M_k + 2 each; a.M + 2 = their sum)
   int ne;
   int ecol[4], eM[4], erow[4];
+  // chain_estep16_kernel: the transition's rows and every child's rows sum to
+  // 1 (to 1e-15): the missing mass m1_t equals the previous step's mass, so
+  // the ll telescopes to log(final mass) and neither per-step sum is needed
+  int proper;
   // chain_fb_ckpt_kernel, joint interface: write the marginals of up to four of
   // its variables instead of the joint posterior (post_tstride = their summed
   // cardinalities).  proj_digit[j][i]: variable j's value at joint state i (-1
@@ -254,6 +258,8 @@ struct EWideArgs {
   int ccol[4];           // their columns in obs, or -1 (never observed: always missing)
   int cM[4];
   int erow[4];           // first count-table row of each
+  int proper;            // rows of A and of every child sum to 1 (engine.cpp chain_proper): the
+                         // ll from the final forward mass, no per-step masses in the filters
 };
 int estep_wide_np(int N);
 int estep_wide_slab(int N, int R);

@@ -502,8 +502,24 @@ __device__ __forceinline__ double dot2_bcast(double x, const double (&c)[16]) {
   return a0 + a1;
 }
 
+// 16-lane integer max of the lanes' binary exponents (zeros excluded): the
+// rescale exponent of a proper model's forward rows, every step -- four DPP
+// integer ops where the row's f64 sum was twelve (any power of two serves:
+// the ll no longer reads the step masses, posteriors and xi are scale-free)
+__device__ __forceinline__ int row_max_exp_rescale(double p) {
+  int e = p != 0.0 ? __builtin_amdgcn_frexp_exp(p) : -0x40000;
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x128, 0xF, 0xF, true));   // row_ror:8
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x124, 0xF, 0xF, true));   // row_ror:4
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x122, 0xF, 0xF, true));   // row_ror:2
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x121, 0xF, 0xF, true));   // row_ror:1
+  return e > -0x40000 ? -e : 0;
+}
+
 // One direction's rows of a block (FWD: waves 0-3, backward: waves 4-7).
-template <bool FWD, int KC, int NE>
+// PR: a proper model (ChainArgs::proper): the ll is log of the final forward
+// mass minus its exponent, so the forward rows keep no m2 / m1 products and
+// rescale by the row's largest exponent, and the backward rows sum no m1.
+template <bool FWD, int KC, int NE, bool PR>
 __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* Et, const uint8_t* codes,
                                              double* Htab, double* m1x, int lane, int grp, long b0, int nseqb) {
   const int y = lane & 15, row = lane >> 4;
@@ -609,9 +625,9 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     // the forward rows need every step's mass (m2); the backward rows only
     // rescale, every 4th step (j is the unrolled step index: no branch) --
     // four evidence factors cannot underflow, and the exponents carry any scale
-    const bool rescale = FWD || (j & 3) == 3;
+    const bool rescale = (FWD && !PR) || (j & 3) == 3;
     const double z2 = rescale ? row_sum(p) : 1.0;
-    if (!FWD && combine) {
+    if (!FWD && combine && !PR) {
       // the m1 of the forward rows' phase-A step t + 1 (< H) from alpha^_t = other
       if (!first) m1 *= row_sum(other * As);           // t + 1 < H: every step but the first
     }
@@ -636,17 +652,18 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
       Kd = FWD ? __builtin_amdgcn_mfma_f64_16x16x4f64(x, w, Kd, 0, 0, 0)
                : __builtin_amdgcn_mfma_f64_16x16x4f64(w, x, Kd, 0, 0, 0);
     }
-    if (FWD) {
+    if (FWD && !PR) {
       m2 *= z2;
       if (combine) m1 *= row_sum(u * s_y);
     }
-    if ((FWD || combine) && (j & 3) == 3) {         // renormalise every 4 steps (0 stays 0)
+    if (!PR && (FWD || combine) && (j & 3) == 3) {  // renormalise every 4 steps (0 stays 0)
       if (FWD) { const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2; }
       const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
     }
     // the scale of the next step (a zero mass keeps every later vector 0,
     // whatever the exponent: no zero test)
-    sc = rescale ? -__builtin_amdgcn_frexp_exp(z2) : 0;
+    if (FWD && PR) sc = row_max_exp_rescale(p);
+    else sc = rescale ? -__builtin_amdgcn_frexp_exp(z2) : 0;
     x = p;
     ex = eu;
   };
@@ -690,7 +707,7 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     d[2] = st[3] - st[2];                            // phase B
   }
   double* slab = a.counts + (size_t)(active ? b : 0) * chain_estep_slab(M);
-  if (!FWD && H > 0) {
+  if (!FWD && H > 0 && !PR) {
     // the phase-A m1 part for the forward rows: step 0's from the prior, then
     // mantissa and exponent through LDS
     m1 *= row_sum(a.pi[y] * As);
@@ -731,8 +748,19 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
       for (int k = 0; k < 16; k++) slab[ko + k * 16 + y] = 0.0;
     }
   }
+  // proper model: ll = log P(obs) = log(sum alpha^_{T-1}) - Ef_{T-1} ln 2
+  // (the forward rows end phase B at t = T - 1: x = alpha^_{T-1}, ex its
+  // exponent); m1_t = the previous mass, so the reference's per-step
+  // log m2 - log m1 telescope to it
+  const double zT = (FWD && PR) ? row_sum(x) : 0.0;
   __syncthreads();                                   // the backward rows' m1 part in LDS
-  if (FWD && active && y == 0) {
+  if (FWD && PR && active && y == 0) {
+    const bool dead = zT == 0.0;
+    const double ll = dead ? -DBL_MAX : log(zT) - (double)ex * 0.69314718055994530942;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 3u : 0u;
+  }
+  if (FWD && !PR && active && y == 0) {
     double lm = log(m2) - log(m1);
     int ee = e2 - e1;
     bool dead = m2 == 0.0;                             // some step's m2 == 0 (products renormalised: no underflow)
@@ -750,7 +778,7 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
 
 }  // namespace
 
-template <int NSEQ, int KC, int NE>
+template <int NSEQ, int KC, int NE, bool PR>
 __global__ __launch_bounds__(NSEQ * 32, 1)
 void chain_estep16_kernel(ChainArgs a) {
   constexpr int kE16Seqs = NSEQ, kE16Threads = NSEQ * 32, G = NSEQ / 4;
@@ -806,8 +834,8 @@ void chain_estep16_kernel(ChainArgs a) {
   }
   __syncthreads();
   double* m1x = Htab + kE16Seqs * 2 * R * 16;                           // [NSEQ][4]
-  if (wave < G) estep16_rows<true, KC, NE>(a, Et, codes, Htab, m1x, lane, wave, b0, kE16Seqs);
-  else estep16_rows<false, KC, NE>(a, Et, codes, Htab, m1x, lane, wave - G, b0, kE16Seqs);
+  if (wave < G) estep16_rows<true, KC, NE, PR>(a, Et, codes, Htab, m1x, lane, wave, b0, kE16Seqs);
+  else estep16_rows<false, KC, NE, PR>(a, Et, codes, Htab, m1x, lane, wave - G, b0, kE16Seqs);
   __syncthreads();
   for (int i = tid; i < kE16Seqs * 2 * R * 16; i += kE16Threads) {
     const int sq = i / (2 * R * 16), r = i - sq * 2 * R * 16;
@@ -847,13 +875,18 @@ size_t chain_estep16_scratch_bytes(long B, int T) {
          (size_t)(nrow + 2) * estep16_xrow(T) * sizeof(int);
 }
 
+template <int NSEQ, int KC, int NE, bool PR>
+static int estep16_launch_pr(const ChainArgs& a, size_t lds, hipStream_t stream) {
+  static size_t lds_set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC, NE, PR>), lds, lds_set)) return -1;
+  const int blocks = (int)((a.B + NSEQ - 1) / NSEQ);
+  hipLaunchKernelGGL((chain_estep16_kernel<NSEQ, KC, NE, PR>), dim3(blocks), dim3(NSEQ * 32), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 template <int NSEQ, int KC, int NE>
 static int estep16_launch(const ChainArgs& a, size_t lds, hipStream_t stream) {
-  static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC, NE>), lds, lds_set)) return -1;
-  const int blocks = (int)((a.B + NSEQ - 1) / NSEQ);
-  hipLaunchKernelGGL((chain_estep16_kernel<NSEQ, KC, NE>), dim3(blocks), dim3(NSEQ * 32), lds, stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return a.proper ? estep16_launch_pr<NSEQ, KC, NE, true>(a, lds, stream)
+                  : estep16_launch_pr<NSEQ, KC, NE, false>(a, lds, stream);
 }
 
 int chain_estep16_launch(const ChainArgs& a, hipStream_t stream) {

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1309,6 +1310,24 @@ static int chain_estep_kernel(const nipamd_model* mm, int T) {
   return 0;
 }
 
+// The chain's transition rows and every child's rows sum to 1 within 1e-15
+// (normalised CPTs; every m_step's output): the reference's per-step
+// log m2 - log m1 then telescope to log P(obs) (m1_t is the previous step's
+// mass), which chain_estep16_kernel's proper mode computes from the final
+// forward mass -- the ll differs by the tables' rounding, <= T x 1e-15.
+static bool chain_proper(const nipamd::ChainPlan& P) {
+  if (P.N > 64) return false;
+  for (int x = 0; x < P.N; x++) {
+    double r = 0.0;
+    for (int y = 0; y < P.N; y++) r += P.A64[x * 64 + y];
+    if (!(std::fabs(r - 1.0) <= 1e-15)) return false;
+  }
+  for (const auto& E : P.emits)
+    for (int y = 0; y < P.N; y++)
+      if (!(std::fabs(E.s[y] - 1.0) <= 1e-15)) return false;
+  return true;
+}
+
 static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r) {
   std::string why;
   const auto& P = mm->m.chain;
@@ -1468,6 +1487,7 @@ static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.slab = slab; a.slab_size = S; a.R = R;
+    a.proper = chain_proper(P) ? 1 : 0;
     a.nchild = (int)P.emits.size();
     for (int k = 0, row = 0; k < a.nchild; k++) {
       a.ccol[k] = -1;
@@ -1579,6 +1599,7 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.counts = slab;
+    a.proper = ek == 3 && chain_proper(P) ? 1 : 0;
 #ifdef NIPAMD_DIAGNOSTICS
     static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
     const int nblk = (nb + 15) / 16;

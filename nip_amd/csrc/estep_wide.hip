@@ -159,7 +159,32 @@ __device__ __forceinline__ double matvec_dpp(double x, const double (&Ac)[NB][16
   return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
+// the rescale exponent of a proper model's forward filter: minus the largest
+// binary exponent over the sequence's NP lanes (zeros excluded; 0 for an
+// all-zero vector), integer DPP / permlane work instead of an f64 sum
 template <int NP>
+__device__ __forceinline__ int group_max_exp_rescale(double p) {
+  int e = p != 0.0 ? __builtin_amdgcn_frexp_exp(p) : -0x40000;
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x128, 0xF, 0xF, true));   // row_ror:8
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x124, 0xF, 0xF, true));   // row_ror:4
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x122, 0xF, 0xF, true));   // row_ror:2
+  e = max(e, __builtin_amdgcn_mov_dpp(e, 0x121, 0xF, 0xF, true));   // row_ror:1
+  if (NP >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)e, (unsigned)e, false, false);
+    e = max((int)r[0], (int)r[1]);
+  }
+  if (NP >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)e, (unsigned)e, false, false);
+    e = max((int)r[0], (int)r[1]);
+  }
+  return e > -0x40000 ? -e : 0;
+}
+
+// PR: a proper model (EWideArgs::proper): the forward filter keeps no step
+// masses -- the reference's per-step log m2 - log m1 telescope to log P(obs)
+// (m1_t is the previous step's mass when A's and the children's rows sum to
+// 1) -- and rescales by the group's largest exponent
+template <int NP, bool PR>
 __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a) {
   constexpr int SPW = 64 / NP;                        // sequences per wave
   constexpr int NB = NP / 16;                         // 16-lane rows per sequence
@@ -226,28 +251,35 @@ __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a)
         if (t >= T) break;
         const double u = __builtin_ldexp(matvec_dpp<NB>(x, Ac), sc);
         const double p = u * e[k];
-        const double z2 = group_sum<NP>(p);
-        const double z1 = group_sum<NP>(u * sy);
         E += sc;
         if (active) {
           Sa[(size_t)t * NP] = p;
           if (y == 0) Ea[t] = E;
         }
-        zmin = __builtin_fmin(zmin, z2);
-        m2 *= z2; m1 *= z1;
-        if ((k & 3) == 3) {
-          const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
-          const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+        if (PR) {
+          sc = group_max_exp_rescale<NP>(p);
+        } else {
+          const double z2 = group_sum<NP>(p);
+          const double z1 = group_sum<NP>(u * sy);
+          zmin = __builtin_fmin(zmin, z2);
+          m2 *= z2; m1 *= z1;
+          if ((k & 3) == 3) {
+            const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+            const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+          }
+          sc = z2 != 0.0 ? -__builtin_amdgcn_frexp_exp(z2) : 0;
         }
-        sc = z2 != 0.0 ? -__builtin_amdgcn_frexp_exp(z2) : 0;
         x = p;
       }
 #pragma unroll
       for (int k = 0; k < kMsgChunk; k++) e[k] = en[k];
     }
+    // proper: ll = log(sum alpha^_{T-1}) - E_{T-1} ln 2 (x = alpha^_{T-1})
+    const double zT = PR ? group_sum<NP>(x) : 0.0;
     if (active && y == 0) {
-      double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
-      const bool dead = zmin == 0.0;
+      double ll = PR ? log(zT) - (double)E * 0.69314718055994530942
+                     : log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+      const bool dead = PR ? zT == 0.0 : zmin == 0.0;
       if (dead) ll = -DBL_MAX;
       if (a.ll) a.ll[b] = ll;
       // e_step's BAD_LUCK (m1 <= 0 || m2 <= 0, nip.c:1827-1854): a zero mass
@@ -506,9 +538,16 @@ int estep_wide_launch(const EWideArgs& a, hipStream_t stream) {
   {
     const int spb = kMsgWaves / 2 * (64 / NP);
     const int blocks = (int)((a.B + spb - 1) / spb);
-    if (NP == 16) hipLaunchKernelGGL(chain_msgs_kernel<16>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
-    else if (NP == 32) hipLaunchKernelGGL(chain_msgs_kernel<32>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
-    else hipLaunchKernelGGL(chain_msgs_kernel<64>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
+    const dim3 g(blocks), th(kMsgWaves * 64);
+    if (a.proper) {
+      if (NP == 16) hipLaunchKernelGGL((chain_msgs_kernel<16, true>), g, th, 0, stream, a);
+      else if (NP == 32) hipLaunchKernelGGL((chain_msgs_kernel<32, true>), g, th, 0, stream, a);
+      else hipLaunchKernelGGL((chain_msgs_kernel<64, true>), g, th, 0, stream, a);
+    } else {
+      if (NP == 16) hipLaunchKernelGGL((chain_msgs_kernel<16, false>), g, th, 0, stream, a);
+      else if (NP == 32) hipLaunchKernelGGL((chain_msgs_kernel<32, false>), g, th, 0, stream, a);
+      else hipLaunchKernelGGL((chain_msgs_kernel<64, false>), g, th, 0, stream, a);
+    }
     if (hipGetLastError() != hipSuccess) return -1;
   }
   g_last_kernel = "chain_msgs_kernel + chain_stats_kernel";

@@ -16,4 +16,5 @@ timeout -k 10 120 env NIPAMD_LIB=$PWD/nip_amd/_lib/diag/libnip_amd_diag.so NIPAM
   --no-secondary --no-cpu-baseline --steps 1 --warmup 1 --no-check > $O/stamps.txt 2>&1 || exit 1
 bash profiles/r04/ab_tests.sh r04j/c5 config5 "" nip_amd/_lib/ab/base.so || exit 1
 bash profiles/r04/ab_tests.sh r04j/e3 estep_config3 "" nip_amd/_lib/ab/base.so || exit 1
+bash profiles/r04/ab_tests.sh r04j/e4 estep "" nip_amd/_lib/ab/base.so || exit 1
 cd /tmp && timeout -k 10 200 python3 $GRAFT_REPO_ROOT/bench.py --workload estep_opchain --no-secondary --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/estep_opchain.jsonl 2>&1
