@@ -446,7 +446,8 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   const long rows = (chunk + kOpXiSeqs - 1) / kOpXiSeqs;
   const long lvl = (rows + 63) / 64;
   const size_t nW = (size_t)chunk * T * K * K, nP0 = (size_t)chunk * K;
-  const size_t nE = nW + nP0 + (size_t)(rows + 2 * lvl + nchunks + 2 * ((nchunks + 63) / 64) + 1) * R;
+  const size_t nC = ((size_t)chunk * T * sizeof(uint16_t) + sizeof(double) - 1) / sizeof(double);
+  const size_t nE = nW + nP0 + nC + (size_t)(rows + 2 * lvl + nchunks + 2 * ((nchunks + 63) / 64) + 1) * R;
   if (P->S_bytes < op_scratch_bytes(chunk, T)) {
     (void)hipFree(P->S);
     P->S = nullptr;
@@ -463,7 +464,8 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   }
   double* W = P->E;
   double* P0 = W + nW;
-  double* slab = P0 + nP0;
+  uint16_t* Cc = reinterpret_cast<uint16_t*>(P0 + nP0);
+  double* slab = P0 + nP0 + nC;
   double* work = slab + (size_t)rows * R;
   double* cres = work + (size_t)2 * lvl * R;
   double* cwork = cres + (size_t)nchunks * R;
@@ -487,6 +489,7 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     a.estep = 1;
     a.W = W;
     a.P0 = P0;
+    a.C = Cc;
     const int rc = op_fb_launch(a, st);
     if (rc == -2) { err = "operators do not fit the kernel's LDS"; return NIPAMD_ERROR_UNSUPPORTED; }
     if (rc) { err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()); return NIPAMD_ERROR_DEVICE; }
@@ -494,7 +497,7 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     x.obs = a.obs; x.obs_bstride = a.obs_bstride; x.obs_tstride = a.obs_tstride; x.nobs = n_obs;
     for (int i = 0; i < n_obs; i++) { x.col[i] = i; x.card[i] = P->card[i]; x.cstride[i] = P->stride[i]; }
     x.B = nb; x.T = T; x.K = K; x.ncomb = P->ncomb;
-    x.W = W; x.P0 = P0; x.slab = slab;
+    x.W = W; x.P0 = P0; x.C = Cc; x.slab = slab;
     if (op_xi_launch(x, st)) { err = "xi launch failed"; return NIPAMD_ERROR_DEVICE; }
     const long nr = (nb + kOpXiSeqs - 1) / kOpXiSeqs;
     if (nipamd_tree_sum(slab, nr, R, work, nchunks == 1 ? out : cres + (size_t)c * R, stream)) {
@@ -535,8 +538,8 @@ int op_estep_finalize(nipamd_model* mm, const double* d_sec, double* d_counts, v
   }
   if (P->map_state == 0) P->map_state = build_map(mm->m, *P) ? 1 : -1;
   if (P->map_state < 0) { err = P->map_why; return NIPAMD_ERROR_UNSUPPORTED; }
-  if (estep_map_finalize_launch(d_sec + kOpHdr, P->map_n, P->d_mptr, P->d_midx, P->d_mcoef, d_counts,
-                                (hipStream_t)stream)) {
+  if (op_finalize_launch(d_sec + kOpHdr, P->map_n, P->d_mptr, P->d_midx, P->d_mcoef, d_counts,
+                         (hipStream_t)stream)) {
     err = "finalize launch failed";
     return NIPAMD_ERROR_DEVICE;
   }

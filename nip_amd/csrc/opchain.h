@@ -54,6 +54,7 @@ struct OpArgs {
   int estep;
   double* W;
   double* P0;
+  uint16_t* C;             // e_step: every step's evidence combination [B][T] (op_xi_kernel's keys)
 };
 
 size_t op_lds_bytes(int K, int ncomb, int T, bool tables);
@@ -75,11 +76,14 @@ struct OpXiArgs {
   int T, K, ncomb;
   const double* W;         // [B][T][K*K]
   const double* P0;        // [B][K]
+  const uint16_t* C;       // [B][T] evidence combinations (op_fb_kernel's codes)
   double* slab;            // [ceil(B / 16)][op_xi_row(K, ncomb)]
 };
 constexpr int kOpXiSeqs = 16;
 __host__ __device__ inline int op_xi_row(int K, int ncomb) { return (ncomb + 1) * K * K + K; }
 bool op_xi_fits(int K, int ncomb);
+int op_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef, double* counts,
+                       hipStream_t stream);
 int op_xi_launch(const OpXiArgs& a, hipStream_t stream);
 
 }  // namespace nipamd

@@ -125,6 +125,7 @@ void op_fb_kernel(OpArgs a) {
       }
     }
     codes[s * T + t] = (uint16_t)c;
+    if (a.estep && s < nseq) a.C[(size_t)(b0 + s) * T + t] = (uint16_t)c;
   }
   __syncthreads();
 
@@ -267,10 +268,10 @@ void op_fb_kernel(OpArgs a) {
   }
 }
 
-// The e_step's per-combination sums: a block per 16 sequences, lane l < K*K
-// owns cell l of every combination's K x K block in LDS and adds the group's
-// W_t(l) in sequence and step order (one lane per cell: no races, a fixed
-// summation order); then P0 over the group; one slab row out.
+// The e_step's per-combination sums: a block per 16 sequences; one lane owns
+// cell l of a combination's K x K block in LDS and adds the group's W_t(l) in
+// sequence and step order (one lane per cell and combination: no races, a
+// fixed summation order); then P0 over the group; one slab row out.
 __global__ __launch_bounds__(256)
 void op_xi_kernel(OpXiArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -282,24 +283,16 @@ void op_xi_kernel(OpXiArgs a) {
   const long b0 = (long)blockIdx.x * kOpXiSeqs;
   const int T = a.T;
   const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
-  if (tid < KK) {
+  // K*K <= 64: each of the four waves owns the combinations c = wave (mod 4)
+  // and scans every step (a quarter of the read-add-write chains per wave);
+  // larger K: lane l < K*K of the block owns cell l of every combination
+  const bool split = KK <= 64;
+  const int cell = split ? (tid & 63) : tid, part = split ? (tid >> 6) : 0, nparts = split ? 4 : 1;
+  if (cell < KK) {
     for (int s = 0; s < nseq; s++) {
       const long b = b0 + s;
-      const double* Wr = a.W + (size_t)b * T * KK + tid;
-      const int32_t* ob = a.obs ? a.obs + b * a.obs_bstride : nullptr;
-      // the evidence combination of step t (op_fb_kernel's code)
-      auto comb = [&](int t) {
-        int c = 0;
-        if (ob) {
-          const int32_t* o = ob + (long)t * a.obs_tstride;
-          for (int k = 0; k < a.nobs; k++) {
-            const int v = o[a.col[k]];
-            if (v >= a.card[k]) { c = a.ncomb; break; }
-            if (v >= 0) c += (v + 1) * a.cstride[k];
-          }
-        }
-        return c;
-      };
+      const double* Wr = a.W + (size_t)b * T * KK + cell;
+      const uint16_t* Cr = a.C + (size_t)b * T;
       constexpr int U = 8;                           // steps loaded ahead of their sums
       for (int t0 = 0; t0 < T; t0 += U) {
         double w[U];
@@ -307,12 +300,12 @@ void op_xi_kernel(OpXiArgs a) {
 #pragma unroll
         for (int k = 0; k < U; k++) {
           const int t = t0 + k < T ? t0 + k : T - 1;
-          w[k] = Wr[(size_t)t * KK];
-          c[k] = comb(t);
+          c[k] = Cr[t];
+          w[k] = (c[k] % nparts == part) ? Wr[(size_t)t * KK] : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < U; k++)
-          if (t0 + k < T) X[(size_t)c[k] * KK + tid] += w[k];
+          if (t0 + k < T && c[k] % nparts == part) X[(size_t)c[k] * KK + cell] += w[k];
       }
     }
   }
@@ -321,6 +314,29 @@ void op_xi_kernel(OpXiArgs a) {
   __syncthreads();
   double* out = a.slab + (size_t)blockIdx.x * R;
   for (int i = tid; i < R; i += 256) out[i] = X[i];
+}
+
+// The projection of the operator chain's e_step: a wave per count cell (its
+// CSR row can hold thousands of entries), lane l summing entries l, l + 64,
+// ... in order, then a fixed-order wave tree -- deterministic, and the long
+// rows no longer serialise one thread each
+__global__ __launch_bounds__(256)
+void op_finalize_kernel(const double* __restrict__ R, int n, const int* __restrict__ ptr,
+                        const int* __restrict__ idx, const double* __restrict__ coef, double* __restrict__ counts) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= n) return;
+  double acc = 0.0;
+  for (int j = ptr[row] + lane; j < ptr[row + 1]; j += 64) acc = __builtin_fma(coef[j], R[idx[j]], acc);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) counts[row] += acc;
+}
+
+int op_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef, double* counts,
+                       hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(op_finalize_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, R, n, ptr, idx, coef, counts);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 bool op_xi_fits(int K, int ncomb) { return (size_t)op_xi_row(K, ncomb) * sizeof(double) <= 160 * 1024; }

@@ -10,6 +10,10 @@
 //   V6 V0 plus the kernel's other per-step work: two LDS ring writes and the
 //      integer-max rescale every 4th step
 //   V7 V6 plus a block barrier every 8 steps (all four waves in step)
+//   V8 V6 with relative blocks: row r takes block r ^ s (s = 0: x itself, no
+//      lane swap on the path to the first 16 fmacs), the other blocks by
+//      in-place v_permlane16/32_swap (vdst = src0), no copies but one per block
+// and swapcheck: the in-place swaps' semantics (lane l gets lane l ^ 16 / l ^ 32)
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 mb_r64.hip -o mb_r64 && ./mb_r64
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -48,6 +52,22 @@ __device__ __forceinline__ void blocks_of(double x, double (&xb)[4]) {
 }
 typedef __attribute__((address_space(3))) double lds_d;
 
+__device__ __forceinline__ double self_swap16(double v) {
+  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  asm volatile("v_permlane16_swap_b32 %0, %0\n\tv_permlane16_swap_b32 %1, %1" : "+v"(lo), "+v"(hi));
+  return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ double self_swap32(double v) {
+  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  asm volatile("v_permlane32_swap_b32 %0, %0\n\tv_permlane32_swap_b32 %1, %1" : "+v"(lo), "+v"(hi));
+  return __hiloint2double((int)hi, (int)lo);
+}
+__global__ void swapcheck(double* out) {
+  const double v = (double)threadIdx.x;
+  out[threadIdx.x] = self_swap16(v);
+  out[64 + threadIdx.x] = self_swap32(v);
+}
+
 __device__ __forceinline__ int max_exp_rescale(double p) {
   int e = p != 0.0 ? __builtin_amdgcn_frexp_exp(p) : -0x40000;
   e = max(e, __builtin_amdgcn_mov_dpp(e, 0x128, 0xF, 0xF, true));
@@ -79,7 +99,12 @@ __global__ __launch_bounds__(256, 1) void k(const double* in, double* out, unsig
   const unsigned long long t0 = __builtin_readcyclecounter();
   for (int s = 0; s < n; s++) {
     double xb[4];
-    if (V == 1 || V == 2) {
+    if (V == 8) {
+      xb[0] = x;
+      xb[1] = self_swap16(x);
+      xb[2] = self_swap32(x);
+      xb[3] = self_swap32(xb[1]);
+    } else if (V == 1 || V == 2) {
 #pragma unroll
       for (int b = 0; b < 4; b++) { xb[b] = xbf[b]; asm volatile("" : "+v"(xb[b])); }
     } else {
@@ -150,5 +175,16 @@ int main() {
   run<5>("V5 V0 + an LDS read waited for in the step", din, dout, dc);
   run<6>("V6 V0 + two ring writes + max-exp rescale every 4th step", din, dout, dc);
   run<7>("V7 V6 + a block barrier every 8 steps", din, dout, dc);
+  run<8>("V8 V6 with relative blocks and in-place swaps", din, dout, dc);
+  {
+    hipLaunchKernelGGL(swapcheck, dim3(1), dim3(64), 0, 0, dout);
+    std::vector<double> h(128);
+    (void)hipMemcpy(h.data(), dout, 128 * 8, hipMemcpyDeviceToHost);
+    int ok16 = 1, ok32 = 1;
+    for (int l = 0; l < 64; l++) { ok16 &= h[l] == (double)(l ^ 16); ok32 &= h[64 + l] == (double)(l ^ 32); }
+    printf("in-place v_permlane16_swap: lane l gets l ^ 16: %s; v_permlane32_swap: l ^ 32: %s\n",
+           ok16 ? "yes" : "NO", ok32 ? "yes" : "NO");
+    if (!ok16 || !ok32) { for (int l = 0; l < 64; l++) printf("%d:%g/%g ", l, h[l], h[64 + l]); printf("\n"); }
+  }
   return 0;
 }

@@ -145,6 +145,11 @@ def test_op_em_learn_matches_general_engine():
     """em_learn on the operator chain: the learning curve and the learned
     parameters follow the general engine's within the count tolerance."""
     m1, ov, obs = demo1_hidden(48, 64, seed=11)
+    # no series starts with an unobserved step: the reference's verdict on
+    # leading missing runs (prefix.cpp) is a comparison of masses that sit at
+    # equal values, which the two engines' last-bit different parameters can
+    # tip either way after a few iterations
+    obs[:, 0, 0] = np.maximum(obs[:, 0, 0], 0)
     m2 = nip_amd.Model.from_net(os.path.join(GOLD, "demo1.net"))
     m2.set_engine(nip_amd.ENGINE_JTREE)
     o = torch.from_numpy(obs).cuda()
