@@ -413,36 +413,11 @@ __device__ __forceinline__ int max_exp_rescale(double p) {
 // the filter wave's column (forward) / row (backward) of A: Ac[b][j] =
 // A(16 b + j, y) / A(y, 16 b + j), loaded before the block stages its tables
 // so that the loads' latency overlaps the staging
-#ifndef NIPAMD_R64_REL
-#define NIPAMD_R64_REL 0         // 1: relative blocks (row r takes block r ^ s, in-place lane swaps)
-#endif
 __device__ __forceinline__ void r64_load_A(const WideArgs& a, bool fwd, int y, double (&Ac)[4][16]) {
 #pragma unroll
-  for (int s = 0; s < 4; s++) {
-    const int b = NIPAMD_R64_REL ? ((y >> 4) ^ s) : s;
+  for (int b = 0; b < 4; b++)
 #pragma unroll
-    for (int j = 0; j < 16; j++) Ac[s][j] = fwd ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
-  }
-}
-
-// relative blocks: xr[s] in row r = block r ^ s of x -- x itself for s = 0
-// (the first 16 fmacs wait on no lane swap), the others by in-place
-// v_permlane16/32_swap (vdst = src0: rows r and r ^ 1 / r ^ 2 exchange)
-__device__ __forceinline__ double self_swap16(double v) {
-  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
-  asm("v_permlane16_swap_b32 %0, %0\n\tv_permlane16_swap_b32 %1, %1" : "+v"(lo), "+v"(hi));
-  return __hiloint2double((int)hi, (int)lo);
-}
-__device__ __forceinline__ double self_swap32(double v) {
-  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
-  asm("v_permlane32_swap_b32 %0, %0\n\tv_permlane32_swap_b32 %1, %1" : "+v"(lo), "+v"(hi));
-  return __hiloint2double((int)hi, (int)lo);
-}
-__device__ __forceinline__ void blocks_rel(double x, double (&xr)[4]) {
-  xr[0] = x;
-  xr[1] = self_swap16(x);
-  xr[2] = self_swap32(x);
-  xr[3] = self_swap32(xr[1]);
+    for (int j = 0; j < 16; j++) Ac[b][j] = fwd ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
 }
 
 template <bool FWD, int NC>
@@ -497,8 +472,7 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
     // one step i (j = i mod 8, the unrolled position; rs: rescale after it)
     auto step = [&](int i, int j, bool rs) {
       double xb[4];
-      if (NIPAMD_R64_REL) blocks_rel(x, xb);
-      else blocks_of(x, xb);
+      blocks_of(x, xb);
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
       fmac16(acc, xb[0], Ac[0]);
       fmac16(acc, xb[1], Ac[1]);

@@ -289,24 +289,34 @@ void op_xi_kernel(OpXiArgs a) {
   const bool split = KK <= 64;
   const int cell = split ? (tid & 63) : tid, part = split ? (tid >> 6) : 0, nparts = split ? 4 : 1;
   if (cell < KK) {
-    for (int s = 0; s < nseq; s++) {
-      const long b = b0 + s;
-      const double* Wr = a.W + (size_t)b * T * KK + cell;
-      const uint16_t* Cr = a.C + (size_t)b * T;
-      constexpr int U = 8;                           // steps loaded ahead of their sums
-      for (int t0 = 0; t0 < T; t0 += U) {
-        double w[U];
-        int c[U];
+    // the group's steps as one stream (sequence-major), loaded a batch of U
+    // steps ahead of their sums so no global load's latency meets the chain
+    // of LDS read-add-writes
+    constexpr int U = 16;
+    const long n = (long)nseq * T;
+    const double* Wg = a.W + (size_t)b0 * T * KK + cell;
+    const uint16_t* Cg = a.C + (size_t)b0 * T;
+    double w[2][U];
+    int c[2][U];
+    auto load = [&](long i0, double (&wv)[U], int (&cv)[U]) {
 #pragma unroll
-        for (int k = 0; k < U; k++) {
-          const int t = t0 + k < T ? t0 + k : T - 1;
-          c[k] = Cr[t];
-          w[k] = (c[k] % nparts == part) ? Wr[(size_t)t * KK] : 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < U; k++)
-          if (t0 + k < T && c[k] % nparts == part) X[(size_t)c[k] * KK + cell] += w[k];
+      for (int k = 0; k < U; k++) {
+        const long i = i0 + k < n ? i0 + k : n - 1;
+        cv[k] = Cg[i];
+        wv[k] = Wg[(size_t)i * KK];
       }
+    };
+    load(0, w[0], c[0]);
+    for (long i0 = 0; i0 < n; i0 += 2 * U) {
+      load(i0 + U, w[1], c[1]);
+#pragma unroll
+      for (int k = 0; k < U; k++)
+        if (i0 + k < n && c[0][k] % nparts == part) X[(size_t)c[0][k] * KK + cell] += w[0][k];
+      if (i0 + U >= n) break;
+      load(i0 + 2 * U, w[0], c[0]);
+#pragma unroll
+      for (int k = 0; k < U; k++)
+        if (i0 + U + k < n && c[1][k] % nparts == part) X[(size_t)c[1][k] * KK + cell] += w[1][k];
     }
   }
   if (tid < a.K)

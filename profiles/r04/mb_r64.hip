@@ -13,6 +13,8 @@
 //   V8 V6 with relative blocks: row r takes block r ^ s (s = 0: x itself, no
 //      lane swap on the path to the first 16 fmacs), the other blocks by
 //      in-place v_permlane16/32_swap (vdst = src0), no copies but one per block
+//   V9 V6 plus a bare s_barrier every 8 steps (no lgkmcnt(0) drain of the ring writes)
+//   V10 V6 plus the drained barrier every 16 steps
 // and swapcheck: the in-place swaps' semantics (lane l gets lane l ^ 16 / l ^ 32)
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 mb_r64.hip -o mb_r64 && ./mb_r64
 #include <hip/hip_runtime.h>
@@ -54,12 +56,12 @@ typedef __attribute__((address_space(3))) double lds_d;
 
 __device__ __forceinline__ double self_swap16(double v) {
   unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
-  asm volatile("v_permlane16_swap_b32 %0, %0\n\tv_permlane16_swap_b32 %1, %1" : "+v"(lo), "+v"(hi));
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
   return __hiloint2double((int)hi, (int)lo);
 }
 __device__ __forceinline__ double self_swap32(double v) {
   unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
-  asm volatile("v_permlane32_swap_b32 %0, %0\n\tv_permlane32_swap_b32 %1, %1" : "+v"(lo), "+v"(hi));
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0\n\tv_permlane32_swap_b32 %1, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
   return __hiloint2double((int)hi, (int)lo);
 }
 __global__ void swapcheck(double* out) {
@@ -129,6 +131,8 @@ __global__ __launch_bounds__(256, 1) void k(const double* in, double* out, unsig
       sc = (s & 3) == 3 ? max_exp_rescale(p) : 0;
       x = p;
       if (V == 7 && (s & 7) == 7) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (V == 9 && (s & 7) == 7) asm volatile("s_barrier" ::: "memory");
+      if (V == 10 && (s & 15) == 15) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       continue;
     }
     if constexpr (NA == 8) u = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
@@ -176,6 +180,8 @@ int main() {
   run<6>("V6 V0 + two ring writes + max-exp rescale every 4th step", din, dout, dc);
   run<7>("V7 V6 + a block barrier every 8 steps", din, dout, dc);
   run<8>("V8 V6 with relative blocks and in-place swaps", din, dout, dc);
+  run<9>("V9 V6 + a bare s_barrier every 8 steps (no drain)", din, dout, dc);
+  run<10>("V10 V6 + the drained barrier every 16 steps", din, dout, dc);
   {
     hipLaunchKernelGGL(swapcheck, dim3(1), dim3(64), 0, 0, dout);
     std::vector<double> h(128);
