@@ -224,6 +224,7 @@ def load_traffic(workload: str):
 
 N_SIMD = 4 * N_CU
 VALU_ISSUE_CYC = 4.0      # one wave64 VALU instruction per 4 cycles on a 16-lane SIMD (MI355X_MICROARCH.md)
+LONE_WAVE_VALU_CYC = 6.27  # f64 VALU issue of a single wave per SIMD, measured (profiles/r04/mb_r64.hip V2)
 MFMA_F64_CYC = 64.0       # v_mfma_f64_16x16x4 occupies its SIMD's matrix pipe 64 cycles (profiles/r03/r03_mb_pipe.txt)
 
 
@@ -263,13 +264,25 @@ def row64_issue_roof(B: int, T: int, kern_ms: float):
             d = json.load(f)
     except Exception:
         return None
-    cyc = d["valu_per_step"] * VALU_ISSUE_CYC + d["salu_per_step"] + d["ds_per_step"] * 4.0
     rounds = -(-B // N_CU)
-    floor_ms = rounds * T * cyc / (CLOCK_GHZ * 1e9) * 1e3
-    return {"bound": "one filter wave's instruction issue", "cycles_per_step": cyc,
+
+    def floor(valu_cyc):
+        cyc = d["valu_per_step"] * valu_cyc + d["salu_per_step"] + d["ds_per_step"] * 4.0
+        return cyc, rounds * T * cyc / (CLOCK_GHZ * 1e9) * 1e3
+
+    # a lone wave on its SIMD issues f64 VALU at 6.27 cycles per instruction,
+    # not 4 (profiles/r04/mb_r64.hip V2: 64 independent v_fmac_f64_dpp in 401
+    # cycles, profiles/r04/gpu/r04h_mb_r64.txt) -- the filter is one sequence's
+    # chain, so that is its issue bound; the 4-cycle figure needs two waves
+    cyc, floor_ms = floor(LONE_WAVE_VALU_CYC)
+    cyc4, floor4 = floor(VALU_ISSUE_CYC)
+    return {"bound": "one filter wave's instruction issue (a lone wave's measured f64 VALU rate)",
+            "cycles_per_step": cyc, "valu_cycles": LONE_WAVE_VALU_CYC,
             "valu_per_step": d["valu_per_step"], "salu_per_step": d["salu_per_step"],
             "ds_per_step": d["ds_per_step"], "steps": T, "block_rounds": rounds, "clock_ghz": CLOCK_GHZ,
-            "floor_ms": floor_ms, "frac": floor_ms / kern_ms, "source": "profiles/r04/isa_row64_step.json"}
+            "floor_ms": floor_ms, "frac": floor_ms / kern_ms,
+            "at_4_cycles": {"cycles_per_step": cyc4, "floor_ms": floor4, "frac": floor4 / kern_ms},
+            "source": "profiles/r04/isa_row64_step.json, profiles/r04/gpu/r04h_mb_r64.txt"}
 
 
 def run_workload(name, args, world, rank, dev, steps, warmup):
