@@ -392,7 +392,10 @@ bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T,
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
   if (!P->ok) { why = P->why; return false; }
   if (!op_fits(mm, n_obs, obs_vars, T)) { why = "sequence too long for the operator chain's LDS codes"; return false; }
-  if (!op_xi_fits(P->K, P->ncomb)) { why = "too many evidence combinations for the e_step's LDS sums"; return false; }
+  if (!op_xi_fits(P->K, P->ncomb) && !op_xi_sort_fits(P->ncomb, T)) {
+    why = "too many evidence combinations for the e_step's LDS sums";
+    return false;
+  }
   const long total = [&] { long t = 1; for (const Var& V : mm->m.vars) t *= V.card; return t; }();
   if (total * (1L << P->ov.size()) * (long)mm->m.vars.size() > kOpMaxMapEntries) {
     why = "e_step projection too large";

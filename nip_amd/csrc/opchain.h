@@ -82,6 +82,7 @@ struct OpXiArgs {
 constexpr int kOpXiSeqs = 16;
 __host__ __device__ inline int op_xi_row(int K, int ncomb) { return (ncomb + 1) * K * K + K; }
 bool op_xi_fits(int K, int ncomb);
+bool op_xi_sort_fits(int ncomb, int T);
 int op_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef, double* counts,
                        hipStream_t stream);
 int op_xi_launch(const OpXiArgs& a, hipStream_t stream);

@@ -349,11 +349,130 @@ int op_finalize_launch(const double* R, int n, const int* ptr, const int* idx, c
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The same sums by a counting sort (op_xi_sort_kernel): the group's steps
+// are bucketed by combination in LDS -- stable, so every bucket lists its
+// steps in stream order -- and a lane per cell then adds a bucket's W rows in
+// a register: the same additions in the same order as op_xi_kernel (each sum
+// starts at 0 and takes its steps in stream order), without op_xi_kernel's
+// chain of LDS read-add-writes.  Four waves: each ranks a quarter of the
+// stream (ballots over the keys of 64 steps at a time), then sums a quarter
+// of the buckets.  LDS: keys [n] u16, per-wave counts -> offsets [4][NC] u32,
+// bucket starts [NC + 1] u32, the sorted step list [n] u32 (n = 16 T).
+__host__ __device__ inline size_t op_xi_sort_lds(int ncomb, int T) {
+  const size_t n = (size_t)kOpXiSeqs * T, NC = (size_t)ncomb + 1;
+  return ((n * 2 + 15) & ~(size_t)15) + (4 * NC + NC + 1) * 4 + n * 4;
+}
+
+__global__ __launch_bounds__(256)
+void op_xi_sort_kernel(OpXiArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int KK = a.K * a.K, R = op_xi_row(a.K, a.ncomb), NC = a.ncomb + 1;
+  const long b0 = (long)blockIdx.x * kOpXiSeqs;
+  const int T = a.T;
+  const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
+  const int n = nseq * T;
+  uint16_t* key = reinterpret_cast<uint16_t*>(smem);
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + (((size_t)kOpXiSeqs * T * 2 + 15) & ~(size_t)15));   // [4][NC]
+  unsigned* start = cnt + 4 * NC;                                                                            // [NC + 1]
+  unsigned* idx = start + NC + 1;                                                                            // [n]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint16_t* Cg = a.C + (size_t)b0 * T;
+  for (int i = tid; i < n; i += 256) key[i] = Cg[i];
+  for (int i = tid; i < 4 * NC; i += 256) cnt[i] = 0;
+  __syncthreads();
+  const int qn = (n + 3) / 4, q0 = min(n, wave * qn), q1 = min(n, q0 + qn);   // this wave's quarter
+  unsigned* my = cnt + wave * NC;
+  const unsigned long long lt = (1ull << lane) - 1;
+  // pass 1: the wave's count per combination
+  for (int i0 = q0; i0 < q1; i0 += 64) {
+    const int i = i0 + lane;
+    const bool v = i < q1;
+    const int k = v ? (int)key[i] : -1;
+    unsigned long long act = __ballot(v);
+    while (act) {
+      const int lk = __shfl(k, __builtin_ctzll(act));
+      const unsigned long long peers = __ballot(v && k == lk);
+      if (lane == __builtin_ctzll(act)) my[lk] += (unsigned)__builtin_popcountll(peers);
+      act &= ~peers;
+    }
+  }
+  __syncthreads();
+  // bucket sizes, and each wave's offset inside each bucket (after the waves
+  // before it: stable across the quarters)
+  for (int c = tid; c < NC; c += 256) {
+    unsigned t = 0;
+    for (int w = 0; w < 4; w++) { const unsigned x = cnt[w * NC + c]; cnt[w * NC + c] = t; t += x; }
+    start[c] = t;
+  }
+  __syncthreads();
+  if (tid == 0) {                                    // exclusive scan of the bucket sizes
+    unsigned t = 0;
+    for (int c = 0; c < NC; c++) { const unsigned x = start[c]; start[c] = t; t += x; }
+    start[NC] = t;
+  }
+  __syncthreads();
+  for (int i = tid; i < 4 * NC; i += 256) cnt[i] += start[i % NC];
+  __syncthreads();
+  // pass 2: scatter, each step to its bucket in stream order
+  for (int i0 = q0; i0 < q1; i0 += 64) {
+    const int i = i0 + lane;
+    const bool v = i < q1;
+    const int k = v ? (int)key[i] : -1;
+    unsigned long long act = __ballot(v);
+    while (act) {
+      const int leader = __builtin_ctzll(act);
+      const int lk = __shfl(k, leader);
+      const unsigned long long peers = __ballot(v && k == lk);
+      const unsigned base = my[lk];
+      if (v && k == lk) idx[base + (unsigned)__builtin_popcountll(peers & lt)] = (unsigned)i;
+      if (lane == leader) my[lk] = base + (unsigned)__builtin_popcountll(peers);
+      act &= ~peers;
+    }
+  }
+  __syncthreads();
+  // sums: wave w takes the buckets c = w (mod 4), a lane per cell
+  double* out = a.slab + (size_t)blockIdx.x * R;
+  const double* Wg = a.W + (size_t)b0 * T * KK;
+  for (int cb = 0; cb < KK; cb += 64) {
+    const int cell = cb + lane;
+    const bool on = cell < KK;
+    for (int c = wave; c < NC; c += 4) {
+      const int j0 = (int)start[c], j1 = (int)start[c + 1];
+      double acc = 0.0;
+      int j = j0;
+      for (; j + 8 <= j1; j += 8) {
+        double w[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) w[u] = on ? Wg[(size_t)idx[j + u] * KK + cell] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += w[u];
+      }
+      for (; j < j1; j++) acc += on ? Wg[(size_t)idx[j] * KK + cell] : 0.0;
+      if (on) out[(size_t)c * KK + cell] = acc;
+    }
+  }
+  if (wave == 0 && lane < a.K) {
+    double p0 = 0.0;
+    for (int sq = 0; sq < nseq; sq++) p0 += a.P0[(size_t)(b0 + sq) * a.K + lane];
+    out[(size_t)NC * KK + lane] = p0;
+  }
+}
+
 bool op_xi_fits(int K, int ncomb) { return (size_t)op_xi_row(K, ncomb) * sizeof(double) <= 160 * 1024; }
+bool op_xi_sort_fits(int ncomb, int T) { return op_xi_sort_lds(ncomb, T) <= 160 * 1024 - 16; }
 
 int op_xi_launch(const OpXiArgs& a, hipStream_t stream) {
   if (a.B <= 0) return 0;
-  if (!op_xi_fits(a.K, a.ncomb) || a.K > 16) return -2;
+  if (a.K > 16) return -2;
+  const size_t slds = (op_xi_sort_lds(a.ncomb, a.T) + 15) & ~(size_t)15;
+  if (slds <= 160 * 1024) {
+    static size_t sort_set[kMaxDevices] = {};
+    if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_sort_kernel), slds, sort_set)) return -1;
+    const int blocks = (int)((a.B + kOpXiSeqs - 1) / kOpXiSeqs);
+    hipLaunchKernelGGL(op_xi_sort_kernel, dim3(blocks), dim3(256), slds, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  if (!op_xi_fits(a.K, a.ncomb)) return -2;
   const size_t lds = ((size_t)op_xi_row(a.K, a.ncomb) * sizeof(double) + 15) & ~(size_t)15;
   static size_t lds_set[kMaxDevices] = {};
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_kernel), lds, lds_set)) return -1;
