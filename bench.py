@@ -113,6 +113,11 @@ WORKLOADS = {
     # the general join-tree engine as "opchain_jt"
     "opchain": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 20),
     "opchain_jt": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 2),
+    # the same request at 20 states (a 20-state joint interface, 9261
+    # evidence combinations): the wide operator chain (op_wide_*), and the
+    # general engine on a smaller batch ("opchain_wide_jt")
+    "opchain_wide": ("general", lambda a: synth.demo1_spec(20), ["A1", "B1", "D1"], "C1", 4096, 1024, 5),
+    "opchain_wide_jt": ("general", lambda a: synth.demo1_spec(20), ["A1", "B1", "D1"], "C1", 256, 1024, 1),
     # e_step of config 3's model (demo1 @ 32 states, A1 and B1 observed): the
     # wide chain e_step (estep_wide.hip)
     "estep_config3": ("config3", lambda a: synth.demo1_spec(32), ["A1", "B1"], "C1", 65536, 256, 5),
@@ -299,7 +304,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
     nodes, pots = spec(args)
     model = nip_amd.Model.from_spec(nodes, pots)
     ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
-    if name in ("jtree", "opchain_jt", "estep_demo1_jt", "estep_opchain_jt"):
+    if name in ("jtree", "opchain_jt", "estep_demo1_jt", "estep_opchain_jt", "opchain_wide_jt"):
         model.set_engine(nip_amd.ENGINE_JTREE)     # the chain kernels would take it otherwise
     N, M = model.card(q), model.card(ov[0])
     obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
@@ -443,6 +448,17 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         workload = ("general join-tree engine: factorial HMM, X and Y 4 states each, O1 16 states of both, "
                     "X1 posterior, B=%d seq/GPU x T=%d" % (B, T))
         metric = "sequence-timesteps/s fwd-bwd smoothing, factorial HMM (general join-tree engine)"
+    elif name in ("opchain_wide", "opchain_wide_jt"):
+        if kname.startswith("op_wide_msgs_kernel"):
+            NP = 32 if N <= 32 else 64
+            bpu, bnote = 4 * len(ov) + 4 * 8 * NP + 8 * N, (
+                "obs %d + alpha^ and beta^ written and read back (4 x %d) + the joint posterior %d (the "
+                "operators are L2 / MALL reads)" % (4 * len(ov), 8 * NP, 8 * N))
+        else:
+            bpu, bnote = 4 * len(ov) + 8 * N, "the request's I/O only: the engine is latency-bound (DESIGN.md 4)"
+        workload = ("demo1 structure, 20 states, A1 B1 and the hidden parent D1 observed, C1 posterior, "
+                    "B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
+        metric = "sequence-timesteps/s fwd-bwd smoothing, demo1 @ 20 with its hidden parent observed"
     elif name in ("opchain", "opchain_jt"):
         if kname == "op_fb_kernel":
             bpu, bnote = 4 * len(ov) + 2 * 128 + 8 * N, (

@@ -43,6 +43,7 @@
 
 #include "chain_kernels.h"
 #include "dpp_row.h"
+#include "opchain.h"
 
 namespace nipamd {
 
@@ -510,7 +511,152 @@ int stats_launch(const EWideArgs& a, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ---- the operator chain at 17..64 joint interface states (opchain.h) ----
+//
+// op_fb_kernel's recursion (opchain.hip) with the wide e_step's layout: a
+// wave per direction holds 64 / NP sequences (lane = state), the step's
+// operator column (forward: T_c(x, y) for lane y) or row (backward: T_c(y,
+// x)) is read per step from HBM / L2 -- the combinations of the next 8 steps
+// a chunk ahead -- and the mat-vec takes the input by DPP row broadcasts.
+//   forward:  alpha_t = T_{c_t}^T alpha_{t-1}  (alpha_{-1} = prior), stored
+//   backward: beta_{t-1} = T_{c_t} beta_t     (beta_{T-1} = 1), stored
+//   ll = sum over steps with evidence of log m2_t - log m1_t (nip.c:1458-1474)
+template <int NP>
+__global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs a) {
+  constexpr int SPW = 64 / NP, NB = NP / 16;
+  constexpr int WD = kMsgWaves / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool fwd = wave < WD;
+  if (!fwd && a.filter) return;
+  const int s = lane / NP, y = lane % NP;
+  const long b = (long)blockIdx.x * (WD * SPW) + (wave % WD) * SPW + s;
+  const bool active = b < a.B;
+  const long bb = active ? b : 0;
+  const int T = a.T, K = a.K, KK = K * K;
+  const bool ys = y < K;
+  const int32_t* obs = a.obs ? a.obs + bb * a.obs_bstride : nullptr;
+  auto comb = [&](int t) {
+    int c = 0;
+    if (obs && t >= 0 && t < T) {
+      const int32_t* o = obs + (long)t * a.obs_tstride;
+      for (int k = 0; k < a.nobs; k++) {
+        const int v = o[a.col[k]];
+        if (v >= a.card[k]) { c = a.ncomb; break; }
+        if (v >= 0) c += (v + 1) * a.cstride[k];
+      }
+    }
+    return c;
+  };
+  // this lane's column (forward) / row (backward) of T_c, in 16-state blocks
+  auto coef = [&](int c, double (&C)[NB][16]) {
+    const double* t = a.Ttab + (size_t)c * KK;
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int x = 16 * k + j;
+        C[k][j] = (x < K && ys) ? (fwd ? t[x * K + y] : t[y * K + x]) : 0.0;
+      }
+  };
+  int cc[kMsgChunk], cn[kMsgChunk];
+  const int dir = fwd ? 1 : -1, t0 = fwd ? 0 : T - 1;
+#pragma unroll
+  for (int k = 0; k < kMsgChunk; k++) cc[k] = comb(t0 + dir * k);
+  double x;
+  int sc = 0;
+  double m2 = 1.0, m1 = 1.0;
+  int e2 = 0, e1 = 0;
+  bool dead = false;
+  const double wy = ys ? a.w[y] : 0.0;
+  double* const Srow = (fwd ? a.Sa : a.Sb) + (size_t)bb * T * NP + y;
+  if (fwd) {
+    x = ys ? a.pi[y] : 0.0;
+  } else {
+    x = ys ? 1.0 : 0.0;                                 // beta_{T-1}
+    if (active) Srow[(size_t)(T - 1) * NP] = x;
+  }
+  // forward: steps t = 0..T-1; backward: t = T-1..1 (each making beta_{t-1})
+  const int n = fwd ? T : T - 1;
+  for (int j0 = 0; j0 < n; j0 += kMsgChunk) {
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) cn[k] = comb(t0 + dir * (j0 + kMsgChunk + k));
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) {
+      const int j = j0 + k;
+      if (j >= n) break;
+      const int t = t0 + dir * j;
+      double C[NB][16];
+      coef(cc[k], C);
+      const double m1v = fwd ? group_sum<NP>(x * wy) : 0.0;
+      const double u = __builtin_ldexp(matvec_dpp<NB>(x, C), sc);
+      const double z = group_sum<NP>(u);
+      if (fwd) {
+        if (cc[k] != 0) {                               // a step with evidence
+          m2 *= z;
+          m1 *= __builtin_ldexp(m1v, sc);
+          const int k2 = m2 != 0.0 ? __builtin_amdgcn_frexp_exp(m2) : 0;
+          const int k1 = m1 != 0.0 ? __builtin_amdgcn_frexp_exp(m1) : 0;
+          m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+          m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+        }
+        dead |= z == 0.0;
+        if (active) Srow[(size_t)t * NP] = u;           // alpha^_t
+      } else {
+        if (active) Srow[(size_t)(t - 1) * NP] = u;     // beta^_{t-1}
+      }
+      sc = z != 0.0 ? -__builtin_amdgcn_frexp_exp(z) : 0;
+      x = u;
+    }
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) cc[k] = cn[k];
+  }
+  if (fwd && active && y == 0) {
+    double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b] = ll;
+    if (a.status) a.status[b] = dead ? 1u : 0u;       // NIPAMD_STATUS_ZERO_MASS
+  }
+}
+
+// posterior_t = normalise(alpha^_t o beta^_t) (filtering: alpha^_t), an
+// all-zero row kept as is (nip_normalise_array, nippotential.c:354)
+template <int NP>
+__global__ __launch_bounds__(256) void op_wide_post_kernel(OpWideArgs a) {
+  constexpr int SPW = 64 / NP;
+  const int lane = threadIdx.x & 63, y = lane % NP;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * SPW + lane / NP;   // (b, t)
+  const long nrow = a.B * a.T;
+  const bool ok = row < nrow;
+  const long r = ok ? row : 0;
+  const double al = a.Sa[(size_t)r * NP + y];
+  const double pr = a.filter ? al : al * a.Sb[(size_t)r * NP + y];
+  const double z = group_sum<NP>(pr);
+  const double q = z != 0.0 ? pr / z : pr;
+  if (ok && y < a.K) {
+    const long b = r / a.T, t = r - b * a.T;
+    a.post[(size_t)b * a.post_bstride + (size_t)t * a.post_tstride + a.post_off + y] = q;
+  }
+}
+
 }  // namespace
+
+int op_wide_launch(const OpWideArgs& a, hipStream_t stream) {
+  if (a.B <= 0) return 0;
+  if (a.K > 64 || a.K < 1) return -2;
+  const int NP = op_wide_np(a.K);
+  const int spb = kMsgWaves / 2 * (64 / NP);
+  const int blocks = (int)((a.B + spb - 1) / spb);
+  const long prow = (a.B * a.T + 4 * (64 / NP) - 1) / (4 * (64 / NP));
+  if (NP == 32) {
+    hipLaunchKernelGGL(op_wide_msgs_kernel<32>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
+    if (a.post) hipLaunchKernelGGL(op_wide_post_kernel<32>, dim3((unsigned)prow), dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(op_wide_msgs_kernel<64>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
+    if (a.post) hipLaunchKernelGGL(op_wide_post_kernel<64>, dim3((unsigned)prow), dim3(256), 0, stream, a);
+  }
+  g_last_kernel = "op_wide_msgs_kernel + op_wide_post_kernel";
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int estep_wide_np(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 0; }
 

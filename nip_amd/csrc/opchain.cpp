@@ -82,7 +82,7 @@ bool build(const Model& m, OpPlan& P) {
   long K = 1, Kp = 1;
   for (int v : cur) K *= m.vars[v].card;
   for (int v : prev) Kp *= m.vars[v].card;
-  if (K > 16 || K != Kp) { P.why = "joint interface above 16 states"; return false; }
+  if (K > 64 || K != Kp) { P.why = "joint interface above 64 states"; return false; }
   for (int v : prev)
     if (!m.vars[v].has_prior) { P.why = "previous interface variable without a prior"; return false; }
   const int no = (int)P.ov.size();
@@ -200,6 +200,7 @@ bool op_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int n_query,
 // The kernel stages the block's evidence codes in LDS: does T fit?
 bool op_fits(nipamd_model* mm, int n_obs, const int* obs_vars, int T) {
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
+  if (P->ok && P->K > 16) return true;                  // the wide kernels read the codes from HBM
   return P->ok && op_lds_bytes(P->K, P->ncomb, T, false) <= 150 * 1024;
 }
 
@@ -221,6 +222,46 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
       return NIPAMD_ERROR_DEVICE;
     }
     P->device = dev;
+  }
+  if (P->K > 16) {
+    // 17..64 states (op_wide_launch): every message stored, launched in
+    // chunks of sequences whose two message arrays stay within ~4 GB
+    const size_t per = op_wide_scratch_bytes(P->K, 1, T);
+    long chunk = (long)std::max<size_t>(1, ((size_t)4 << 30) / per);
+    chunk = std::min<long>(chunk, B > 0 ? B : 1);
+    const size_t need = op_wide_scratch_bytes(P->K, chunk, T);
+    if (P->S_bytes < need) {
+      (void)hipFree(P->S);
+      P->S = nullptr;
+      P->S_bytes = 0;
+      if (hipMalloc(&P->S, need) != hipSuccess) { err = "scratch"; return NIPAMD_ERROR_DEVICE; }
+      P->S_bytes = need;
+    }
+    const long ocols = n_obs > 0 ? n_obs : 1;
+    for (long b0 = 0; b0 < B; b0 += chunk) {
+      const long nb = std::min<long>(chunk, B - b0);
+      OpWideArgs w{};
+      w.obs = d_obs ? d_obs + b0 * T * ocols : nullptr;
+      w.obs_bstride = (long)T * ocols;
+      w.obs_tstride = (int)ocols;
+      w.nobs = n_obs;
+      for (int i = 0; i < n_obs; i++) { w.col[i] = i; w.card[i] = P->card[i]; w.cstride[i] = P->stride[i]; }
+      w.B = nb; w.T = T; w.K = P->K; w.ncomb = P->ncomb;
+      w.filter = filt ? 1 : 0;
+      w.Ttab = P->dT; w.w = P->dw; w.pi = P->dpi;
+      w.Sa = P->S;
+      w.Sb = P->S + (size_t)nb * T * op_wide_np(P->K);
+      w.post = d_joint ? d_joint + b0 * jbs : nullptr;
+      w.post_bstride = jbs; w.post_tstride = jts; w.post_off = joff;
+      w.ll = d_ll ? d_ll + b0 : nullptr;
+      w.status = d_status ? d_status + b0 : nullptr;
+      if (op_wide_launch(w, (hipStream_t)stream)) {
+        err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError());
+        return NIPAMD_ERROR_DEVICE;
+      }
+    }
+    if (K_out) *K_out = P->K;
+    return 0;
   }
   // Smoothing keeps every sequence's rows plus a sink row past them; filter
   // mode keeps no rows, and its masked lanes (inactive sequences, states
@@ -391,6 +432,7 @@ long op_estep_chunk(int K, int T) {
 bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T, std::string& why) {
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
   if (!P->ok) { why = P->why; return false; }
+  if (P->K > 16) { why = "the operator chain's e_step covers joint interfaces of up to 16 states"; return false; }
   if (!op_fits(mm, n_obs, obs_vars, T)) { why = "sequence too long for the operator chain's LDS codes"; return false; }
   if (!op_xi_fits(P->K, P->ncomb) && !op_xi_sort_fits(P->ncomb, T)) {
     why = "too many evidence combinations for the e_step's LDS sums";

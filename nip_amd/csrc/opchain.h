@@ -82,6 +82,42 @@ struct OpXiArgs {
 constexpr int kOpXiSeqs = 16;
 __host__ __device__ inline int op_xi_row(int K, int ncomb) { return (ncomb + 1) * K * K + K; }
 bool op_xi_fits(int K, int ncomb);
+
+// 17 <= K <= 64 joint interface states (estep_wide.hip op_wide_*): the
+// operators stay in HBM / L2; one wave per direction holds 64 / NP
+// sequences (NP = 32 or 64 lanes each, lane = state), the step's column
+// (forward) or row (backward) of T_c read per step, the mat-vec by DPP row
+// broadcasts.  Every message is stored (alpha^_t in Sa, beta^_t in Sb), then
+// op_wide_post_kernel normalises alpha^ beta^ (or alpha^ alone, filtering)
+// into the caller's joint rows.
+struct OpWideArgs {
+  const int32_t* obs;
+  long obs_bstride;
+  int obs_tstride;
+  int nobs;
+  int col[kOpMaxObs];
+  int card[kOpMaxObs];
+  int cstride[kOpMaxObs];
+  long B;
+  int T, K, ncomb;
+  int filter;
+  const double* Ttab;      // [(ncomb + 1)][K][K]
+  const double* w;         // [K]
+  const double* pi;        // [K]
+  double* Sa;              // [B][T][NP]
+  double* Sb;              // [B][T][NP]
+  double* post;            // joint rows: post + b * post_bstride + t * post_tstride + post_off
+  long post_bstride;
+  int post_tstride;
+  int post_off;
+  double* ll;
+  unsigned* status;
+};
+inline int op_wide_np(int K) { return K <= 32 ? 32 : 64; }
+inline size_t op_wide_scratch_bytes(int K, long B, int T) {
+  return (size_t)2 * B * T * op_wide_np(K) * sizeof(double);
+}
+int op_wide_launch(const OpWideArgs& a, hipStream_t stream);
 bool op_xi_sort_fits(int ncomb, int T);
 int op_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef, double* counts,
                        hipStream_t stream);

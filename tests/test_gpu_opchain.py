@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 import nip_amd
+from nip_amd import synth
 from oracle.bind import PortOracle
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -145,3 +146,38 @@ def test_general_goldens_on_the_operator_chain(path):
     cols = np.concatenate([np.arange(offs[v], offs[v] + m.card(v)) for v in q])
     assert np.abs(post - z["post"][:, :, cols]).max() <= POST_TOL
     assert close_ll(ll, z["ll"])
+
+
+WIDE_CASES = [
+    # (name, spec, observed, query, B, T): joint interfaces of 17..64 states
+    # the chain plan rejects (evidence on a hidden parent): op_wide_* kernels
+    ("demo1_20_D1", lambda: synth.demo1_spec(20), ["A1", "B1", "D1"], ["C1"], 9, 23),
+    ("wide_34_Y1", lambda: synth.wide_spec(34, 4), ["Y1", "O1"], ["X1"], 5, 17),
+    ("demo1_17_D1_T1", lambda: synth.demo1_spec(17), ["A1", "D1"], ["C1"], 6, 1),
+]
+
+
+@pytest.mark.parametrize("name,spec,osyms,qsyms,B,T", WIDE_CASES, ids=[c[0] for c in WIDE_CASES])
+def test_wide_operator_chain(name, spec, osyms, qsyms, B, T):
+    """17-64 joint interface states on the operator chain (op_wide_msgs_kernel
+    + op_wide_post_kernel): smoothing and filtering against the general engine
+    (posteriors 1e-12, ll 1e-12, zero-mass flags) and the oracle."""
+    m = nip_amd.Model.from_spec(*spec())
+    ov, q = [m.variable(s) for s in osyms], [m.variable(s) for s in qsyms]
+    rng = np.random.default_rng(B * 31 + T)
+    obs = np.stack([rng.integers(-1, m.card(v), size=(B, T)) for v in ov], axis=2).astype(np.int32)
+    if B > 3:
+        obs[3, 0, 0] = m.card(ov[0])                  # out of range: a zero-mass sequence
+    for filt in (False, True):
+        a = run(m, obs, ov, q, filt)
+        assert a[3].startswith("op_wide_msgs_kernel"), a[3]
+        b = run(m, obs, ov, q, filt, nip_amd.ENGINE_JTREE)
+        assert np.abs(a[0] - b[0]).max() <= POST_TOL, np.abs(a[0] - b[0]).max()
+        assert close_ll(a[1], b[1])
+        assert np.array_equal(a[2] != 0, b[2] != 0)
+    orc = PortOracle(m.desc())
+    post, ll, _, _ = run(m, obs, ov, q)
+    for bb in (0, B - 1):
+        rp, rl = orc.fb(obs[bb], ov, q)
+        assert np.abs(post[bb] - rp).max() <= POST_TOL
+        assert close_ll([ll[bb]], [rl])
