@@ -219,10 +219,17 @@ def load_entry(workload: str):
         return None
 
 
-def load_traffic(workload: str):
-    """HBM bytes per step from the committed rocprofv3 PMC pass (profiles/)."""
+def load_traffic(workload: str, single_kernel: bool):
+    """HBM bytes per step from the committed rocprofv3 PMC pass (profiles/):
+    the dominant kernel's bytes per launch x launches per step when the step
+    is that one kernel (fb, config 3, config 5 -- a per-step sum over the
+    profiled process would also count the headline's PCIe-inclusive call and
+    the output checks), every nipamd kernel's per step otherwise (e_step:
+    filters, statistics, trees, finalize)."""
     e = load_entry(workload)
     if e:
+        if single_kernel:
+            return e.get("hbm_bytes_per_step", e.get("hbm_bytes_per_launch"))
         return e.get("all_kernels_hbm_bytes_per_step", e.get("hbm_bytes_per_step", e.get("hbm_bytes_per_launch")))
     return None
 
@@ -495,7 +502,9 @@ def run_workload(name, args, world, rank, dev, steps, warmup):
         metric = "sequence-timesteps/s fwd-bwd smoothing, wide-clique DBN (64^4 in-clique)"
     achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(workload), "kernel": kname,
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": load_traffic(workload, name in ("fb", "config3", "config5", "joint", "opchain")),
+            "kernel": kname,
             "kernel_ms": kern_ms, "bytes_per_unit": bpu, "bytes_note": bnote}
     if cfg in PRIMARY_BYTES and name in ("fb", "config3", "em", "estep", "config5"):
         pb = PRIMARY_BYTES[cfg]

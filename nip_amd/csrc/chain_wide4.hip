@@ -41,6 +41,24 @@ __device__ __forceinline__ double ror(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// x[l] + x[l ^ 16] (pl16) / x[l] + x[l ^ 32] (pl32) in every lane: the swap's
+// second operand is a copy of x made as a whole double (one v_mov_b64; the
+// two results come back in the register pairs of the two operands)
+__device__ __forceinline__ double pl16(double x) {
+  double xc = x;
+  asm("" : "+v"(xc));
+  const auto rl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+__device__ __forceinline__ double pl32(double x) {
+  double xc = x;
+  asm("" : "+v"(xc));
+  const auto rl = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
+  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
+}
+
 // fixed-order sum over the wave (identical bits in every lane)
 __device__ __forceinline__ double wave_sum(double x) {
   asm("" : "+v"(x));       // one rounded value per lane: no fma contraction into the first add
@@ -48,35 +66,13 @@ __device__ __forceinline__ double wave_sum(double x) {
   x += ror<4>(x);
   x += ror<2>(x);
   x += ror<1>(x);
-  {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    x = __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
-  }
-  {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    x = __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
-  }
+  x = pl16(x);
+  x = pl32(x);
   return x;
 }
 
 // wave_sum of n independent values, stage by stage so their dependency
 // chains interleave
-__device__ __forceinline__ double pl16(double x) {
-  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
-}
-__device__ __forceinline__ double pl32(double x) {
-  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
-}
 template <int n>
 __device__ __forceinline__ void wave_sum_n(double (&x)[n]) {
 #pragma unroll
@@ -371,13 +367,23 @@ __device__ __forceinline__ void fmac16(double (&acc)[4], double xb, const double
 // the four 16-state blocks of x (lane l holds x(l)) in every lane: xb[b] at
 // lane (row r, i) = x(16 b + i)
 __device__ __forceinline__ void blocks_of(double x, double (&xb)[4]) {
+  // the copies the in-place swaps need, made as whole doubles (one
+  // v_mov_b64 each instead of two v_mov_b32: each swap's two results sit in
+  // the register pairs of its two operands)
+  double xc = x;
+  asm("" : "+v"(xc));
   const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);   // [0]: block r & ~1, [1]: r | 1
-  const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const auto q0l = __builtin_amdgcn_permlane32_swap(pl[0], pl[0], false, false);   // blocks 0, 2
-  const auto q0h = __builtin_amdgcn_permlane32_swap(ph[0], ph[0], false, false);
-  const auto q1l = __builtin_amdgcn_permlane32_swap(pl[1], pl[1], false, false);   // blocks 1, 3
-  const auto q1h = __builtin_amdgcn_permlane32_swap(ph[1], ph[1], false, false);
+  const unsigned clo = (unsigned)__double2loint(xc), chi = (unsigned)__double2hiint(xc);
+  const auto pl = __builtin_amdgcn_permlane16_swap(lo, clo, false, false);   // [0]: block r & ~1, [1]: r | 1
+  const auto ph = __builtin_amdgcn_permlane16_swap(hi, chi, false, false);
+  double p0 = __hiloint2double((int)ph[0], (int)pl[0]), p1 = __hiloint2double((int)ph[1], (int)pl[1]);
+  double p0c = p0, p1c = p1;
+  asm("" : "+v"(p0c));
+  asm("" : "+v"(p1c));
+  const auto q0l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(p0), (unsigned)__double2loint(p0c), false, false);
+  const auto q0h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(p0), (unsigned)__double2hiint(p0c), false, false);
+  const auto q1l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(p1), (unsigned)__double2loint(p1c), false, false);
+  const auto q1h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(p1), (unsigned)__double2hiint(p1c), false, false);
   xb[0] = __hiloint2double((int)q0h[0], (int)q0l[0]);
   xb[2] = __hiloint2double((int)q0h[1], (int)q0l[1]);
   xb[1] = __hiloint2double((int)q1h[0], (int)q1l[0]);

@@ -62,16 +62,20 @@ __device__ __forceinline__ double rorK(double v) {     // row_ror:K of a double 
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x120 + K, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double swap16(double x) {   // x[l ^ 16] + x[l] in both lanes: the pair's sum
-  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+// x[l ^ 16] + x[l] in both lanes: the pair's sum (the swap's second operand
+// a copy of x made as a whole double: one v_mov_b64)
+__device__ __forceinline__ double swap16(double x) {
+  double xc = x;
+  asm("" : "+v"(xc));
+  const auto rl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
   return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
 }
 __device__ __forceinline__ double swap32(double x) {
-  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  double xc = x;
+  asm("" : "+v"(xc));
+  const auto rl = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
   return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
 }
 // sum over aligned groups of L lanes (16, 32 or 64); every level pairs equal
@@ -129,17 +133,24 @@ __device__ __forceinline__ void seq_blocks(double x, double (&xb)[NB]) {
   if constexpr (NB == 1) {
     xb[0] = x;
   } else {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    // the swaps' second operands are copies made as whole doubles (one
+    // v_mov_b64 each)
+    double xc = x;
+    asm("" : "+v"(xc));
+    const auto pl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+    const auto ph = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
     if constexpr (NB == 2) {
       xb[0] = __hiloint2double((int)ph[0], (int)pl[0]);
       xb[1] = __hiloint2double((int)ph[1], (int)pl[1]);
     } else {
-      const auto q0l = __builtin_amdgcn_permlane32_swap(pl[0], pl[0], false, false);   // blocks 0, 2
-      const auto q0h = __builtin_amdgcn_permlane32_swap(ph[0], ph[0], false, false);
-      const auto q1l = __builtin_amdgcn_permlane32_swap(pl[1], pl[1], false, false);   // blocks 1, 3
-      const auto q1h = __builtin_amdgcn_permlane32_swap(ph[1], ph[1], false, false);
+      double p0 = __hiloint2double((int)ph[0], (int)pl[0]), p1 = __hiloint2double((int)ph[1], (int)pl[1]);
+      double p0c = p0, p1c = p1;
+      asm("" : "+v"(p0c));
+      asm("" : "+v"(p1c));
+      const auto q0l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(p0), (unsigned)__double2loint(p0c), false, false);   // blocks 0, 2
+      const auto q0h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(p0), (unsigned)__double2hiint(p0c), false, false);
+      const auto q1l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(p1), (unsigned)__double2loint(p1c), false, false);   // blocks 1, 3
+      const auto q1h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(p1), (unsigned)__double2hiint(p1c), false, false);
       xb[0] = __hiloint2double((int)q0h[0], (int)q0l[0]);
       xb[2] = __hiloint2double((int)q0h[1], (int)q0l[1]);
       xb[1] = __hiloint2double((int)q1h[0], (int)q1l[0]);
