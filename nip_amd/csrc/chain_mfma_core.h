@@ -49,16 +49,18 @@ constexpr int kOBRow = 130;                        // DMA buffer doubles per cha
 __host__ __device__ inline long block_scratch(int T) { return (long)(T + 2 * kMG) * kSStep; }
 
 __device__ __forceinline__ double sum_lanes32(double x) {   // x[l] + x[l ^ 32]
-  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  double xc = x;
+  asm("" : "+v"(xc));   // the swap's second operand: a whole-double copy (one v_mov_b64)
+  const auto rl = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
   return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
 }
 
 __device__ __forceinline__ double sum_lanes16(double x) {   // x[l] + x[l ^ 16]
-  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  double xc = x;
+  asm("" : "+v"(xc));   // the swap's second operand: a whole-double copy (one v_mov_b64)
+  const auto rl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
   return __hiloint2double((int)rh[0], (int)rl[0]) + __hiloint2double((int)rh[1], (int)rl[1]);
 }
 
@@ -422,15 +424,17 @@ struct LL {
   // operation is symmetric, so all four lanes hold identical bits
   __device__ __forceinline__ void reduce(double& E2, double& E1) {
     auto pair32 = [](double x, auto f) {
-      const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-      const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-      const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+      double xc = x;
+      asm("" : "+v"(xc));   // the swap's second operand: a whole-double copy (one v_mov_b64)
+      const auto rl = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+      const auto rh = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
       return f(__hiloint2double((int)rh[0], (int)rl[0]), __hiloint2double((int)rh[1], (int)rl[1]));
     };
     auto pair16 = [](double x, auto f) {
-      const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-      const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-      const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+      double xc = x;
+      asm("" : "+v"(xc));   // the swap's second operand: a whole-double copy (one v_mov_b64)
+      const auto rl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(xc), false, false);
+      const auto rh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(xc), false, false);
       return f(__hiloint2double((int)rh[0], (int)rl[0]), __hiloint2double((int)rh[1], (int)rl[1]));
     };
     auto mul = [](double x, double y) { return x * y; };

@@ -15,6 +15,8 @@
 //      in-place v_permlane16/32_swap (vdst = src0), no copies but one per block
 //   V9 V6 plus a bare s_barrier every 8 steps (no lgkmcnt(0) drain of the ring writes)
 //   V10 V6 plus the drained barrier every 16 steps
+//   V11 V6 with 2 accumulators (one zeroing and one add fewer ... per pair)
+//   V12 V6 with 3 accumulators
 // and swapcheck: the in-place swaps' semantics (lane l gets lane l ^ 16 / l ^ 32)
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 mb_r64.hip -o mb_r64 && ./mb_r64
 #include <hip/hip_runtime.h>
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(256, 1) void k(const double* in, double* out, unsig
     } else {
       blocks_of(x, xb);
     }
-    constexpr int NA = V == 4 ? 8 : 4;
+    constexpr int NA = V == 4 ? 8 : V == 11 ? 2 : V == 12 ? 3 : 4;
     double acc[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) acc[i] = 0.0;
@@ -123,7 +125,11 @@ __global__ __launch_bounds__(256, 1) void k(const double* in, double* out, unsig
     }
     double u;
     if constexpr (V >= 6) {
-      u = __builtin_ldexp((acc[0] + acc[1]) + (acc[2] + acc[3]), sc);
+      double su;
+      if constexpr (NA == 2) su = acc[0] + acc[1];
+      else if constexpr (NA == 3) su = (acc[0] + acc[1]) + acc[2 % NA];
+      else su = (acc[0] + acc[1]) + (acc[2 % NA] + acc[3 % NA]);
+      u = __builtin_ldexp(su, sc);
       const double p = u * e;
       const int slot = s & 7;
       sm[1024 + (w * 8 + slot) * 64 + y] = p;
@@ -182,6 +188,8 @@ int main() {
   run<8>("V8 V6 with relative blocks and in-place swaps", din, dout, dc);
   run<9>("V9 V6 + a bare s_barrier every 8 steps (no drain)", din, dout, dc);
   run<10>("V10 V6 + the drained barrier every 16 steps", din, dout, dc);
+  run<11>("V11 V6 with 2 accumulators", din, dout, dc);
+  run<12>("V12 V6 with 3 accumulators", din, dout, dc);
   {
     hipLaunchKernelGGL(swapcheck, dim3(1), dim3(64), 0, 0, dout);
     std::vector<double> h(128);
