@@ -415,6 +415,9 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
 }
 
 template <int PROJ>
+#ifndef NIPAMD_CK_PRIO
+#define NIPAMD_CK_PRIO 0
+#endif
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* out = reinterpret_cast<double*>(smem);     // filter rings [2 dirs][2 slots][8][16][16]
@@ -464,6 +467,9 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
     dg.write(a, wave, lane);
     return;
   }
+  // A/B builds: static wave priority for the recompute waves (1) or the partners (2)
+  if ((NIPAMD_CK_PRIO == 1 && wave >= 6) || (NIPAMD_CK_PRIO == 2 && role >= 2 && wave < 4))
+    __builtin_amdgcn_s_setprio(1);
   if (role >= 2 && wave < 4) {
     if (fwd) ck_partner<true, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
     else ck_partner<false, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);

@@ -422,6 +422,9 @@ void chain_kernel(ChainArgs a) {
 // NSEQ sequences per block (16: 8 waves, two per SIMD; 24: 12 waves, three
 // per SIMD), waves 0 .. NSEQ/4-1 forward, the rest backward
 constexpr int kE16RowMul = 48;                 // scratch rows rounded to a multiple of every NSEQ
+#ifndef NIPAMD_ESTEP_PRIO
+#define NIPAMD_ESTEP_PRIO 0
+#endif
 #ifndef NIPAMD_WAIT_TIMES
 #define NIPAMD_WAIT_TIMES 0                    // stamps builds: per-wave phase cycle stamps into a.diag
 #endif
@@ -834,6 +837,8 @@ void chain_estep16_kernel(ChainArgs a) {
   }
   __syncthreads();
   double* m1x = Htab + kE16Seqs * 2 * R * 16;                           // [NSEQ][4]
+  // A/B builds: static wave priority for the backward (1) or the forward (2) rows
+  if ((NIPAMD_ESTEP_PRIO == 1 && wave >= G) || (NIPAMD_ESTEP_PRIO == 2 && wave < G)) __builtin_amdgcn_s_setprio(1);
   if (wave < G) estep16_rows<true, KC, NE, PR>(a, Et, codes, Htab, m1x, lane, wave, b0, kE16Seqs);
   else estep16_rows<false, KC, NE, PR>(a, Et, codes, Htab, m1x, lane, wave - G, b0, kE16Seqs);
   __syncthreads();

@@ -611,6 +611,9 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
 
 // FILT: forward_inference (filtering only): per group one filter wave and one
 // partner wave (waves 0, 1 the groups' filters, 2, 3 their partners), H = T
+#ifndef NIPAMD_WIDE_PRIO
+#define NIPAMD_WIDE_PRIO 0
+#endif
 template <int NT, bool FILT, int NC>
 __global__ __launch_bounds__(FILT ? kWThreads / 2 : kWThreads, 1)
 void chain_mfma_wide_kernel(WideMfmaArgs a) {
@@ -639,6 +642,8 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   const int nchA = (nA + G::CH - 1) / G::CH, nchB = FILT ? 0 : (nB + G::CH - 1) / G::CH;
   double* ring = out + (fwd ? 0 : 2 * G::kSlot);
   double* Sblk = FILT ? nullptr : a.S + (size_t)(b0 / kWSeq) * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;
+  // A/B builds: static wave priority for the partners (1) or the filters (2)
+  if ((NIPAMD_WIDE_PRIO == 1 && !filter) || (NIPAMD_WIDE_PRIO == 2 && filter)) __builtin_amdgcn_s_setprio(1);
   if (!filter) {
     const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
                       (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
