@@ -304,6 +304,9 @@ __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fsl
   const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
   const bool ok = kB < nk;
   double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow + hi) * 16 + a.post_off + 2 * s;
+#ifndef NIPAMD_POST_NT
+#define NIPAMD_POST_NT 0
+#endif
 #ifndef NIPAMD_CKPT_NO_STORES
 #define NIPAMD_CKPT_NO_STORES 0    // timing-only builds: posteriors not written (wrong results)
 #endif
@@ -312,7 +315,11 @@ __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fsl
     const double2 v = *reinterpret_cast<const double2*>(rslot + ck_off(kB, q, s));
     double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
     if (NIPAMD_CKPT_NO_STORES && v.x != 12345.0) continue;
+#if NIPAMD_POST_NT                 // A/B builds: streaming (nontemporal) posterior stores
+    __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+#else
     *reinterpret_cast<double2*>(p) = v;
+#endif
   }
 }
 

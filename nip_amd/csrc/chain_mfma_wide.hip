@@ -38,6 +38,9 @@
 
 namespace nipamd {
 
+#ifndef NIPAMD_POST_NT
+#define NIPAMD_POST_NT 0
+#endif
 namespace {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -519,7 +522,11 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
         if constexpr (PVEC) {
           double* p = (ok && bb < a.B) ? a.post + (size_t)bb * a.post_bstride + (long)t * NP + a.post_off + 2 * s
                                        : sink;
+#if NIPAMD_POST_NT                                   // A/B builds: streaming posterior stores
+          __builtin_nontemporal_store(v2d{px[i] * r[i], py[i] * r[i]}, reinterpret_cast<v2d*>(p));
+#else
           *reinterpret_cast<v2d*>(p) = v2d{px[i] * r[i], py[i] * r[i]};
+#endif
         } else {
           if (ok && bb < a.B) {
             double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
