@@ -181,3 +181,46 @@ def test_config4_full_shard_counts_vs_textbook():
     assert err.max() <= 1e-11, err.max()
     lg, lw = ll.cpu().numpy(), wll.cpu().numpy()
     assert np.all(np.abs(lg - lw) <= 1e-12 * np.abs(lw)), np.abs(lg - lw).max()
+
+
+def _rccl_worker(port, q):
+    """One rank over the "nccl" backend (RCCL on ROCm): the exchange's
+    all-gather of a packed config-4 partial on cuda:0."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        nodes, pots = synth.hmm_spec(16, 16, seed=31)
+        m = nip_amd.Model.from_spec(nodes, pots)
+        obs = torch.from_numpy(synth.observations(256, 64, 16, seed=5)).cuda()
+        partial, ll, st = nip_amd.estep_partial(m, obs, [m.variable("M1")])
+        packed, llt, bad = nem.exchange(partial, ll, st, None)
+        x = torch.cat([packed, torch.tensor([llt, float(bad)], dtype=torch.float64, device="cuda")])
+        out = [torch.empty_like(x)]
+        dist.all_gather(out, x)                       # RCCL, one rank
+        torch.cuda.synchronize()
+        q.put({"same": bool(torch.equal(out[0], x)), "backend": dist.get_backend(), "n": x.numel()})
+        dist.destroy_process_group()
+    except Exception as e:  # report, do not hang the parent
+        q.put({"error": repr(e)})
+
+
+def test_rccl_all_gather_one_rank():
+    """The exchange's collective through RCCL on the test box's one GPU (two
+    ranks cannot share a device under RCCL; the 2-rank path above is gloo).
+    Executes the nccl backend's init and all-gather with the packed buffer."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        res = q.get(timeout=100)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert "error" not in res, res
+    assert res["backend"] == "nccl" and res["same"] and res["n"] > 2
