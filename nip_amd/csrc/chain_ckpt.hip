@@ -32,6 +32,7 @@
 // The same recursion as nip.c:1320-1581 (forward_backward_inference), see
 // chain_kernels.hip for the derivation.
 #include "chain_mfma_core.h"
+#include "store_pol.h"
 
 namespace nipamd {
 
@@ -304,9 +305,6 @@ __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fsl
   const int nk = nB - ci * kMChunk < kMChunk ? nB - ci * kMChunk : kMChunk;
   const bool ok = kB < nk;
   double* const base = a.post + (size_t)b0 * a.post_bstride + (long)(tlow + hi) * 16 + a.post_off + 2 * s;
-#ifndef NIPAMD_POST_NT
-#define NIPAMD_POST_NT 0
-#endif
 #ifndef NIPAMD_CKPT_NO_STORES
 #define NIPAMD_CKPT_NO_STORES 0    // timing-only builds: posteriors not written (wrong results)
 #endif
@@ -315,11 +313,7 @@ __device__ __forceinline__ void norm_store(const ChainArgs& a, const double* fsl
     const double2 v = *reinterpret_cast<const double2*>(rslot + ck_off(kB, q, s));
     double* p = (ok && b0 + q < a.B) ? base + q * a.post_bstride : sink;
     if (NIPAMD_CKPT_NO_STORES && v.x != 12345.0) continue;
-#if NIPAMD_POST_NT                 // A/B builds: streaming (nontemporal) posterior stores
-    __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
-#else
-    *reinterpret_cast<double2*>(p) = v;
-#endif
+    store_pol<NIPAMD_POST_NT>(reinterpret_cast<v2d*>(p), v2d{v.x, v.y});
   }
 }
 
@@ -380,8 +374,8 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const int e = -__builtin_amdgcn_frexp_exp(z[q]);
-        *reinterpret_cast<double2*>(Sblk + (long)t * kSStep + (q * 8 + hi) * 16 + 2 * s) =
-            make_double2(__builtin_ldexp(v[q].x, e), __builtin_ldexp(v[q].y, e));
+        store_pol<NIPAMD_SCR_NT>(reinterpret_cast<v2d*>(Sblk + (long)t * kSStep + (q * 8 + hi) * 16 + 2 * s),
+                                 v2d{__builtin_ldexp(v[q].x, e), __builtin_ldexp(v[q].y, e)});
       }
     }
   };

@@ -40,6 +40,7 @@
 #include "chain_kernels.h"
 #include "diag.h"
 #include "dpp_row.h"
+#include "store_pol.h"
 
 namespace nipamd {
 
@@ -635,8 +636,8 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
       if (!first) m1 *= row_sum(other * As);           // t + 1 < H: every step but the first
     }
     if (!combine) {
-      cx.Sstore[(long)t * cx.Sstride] = keep;
-      if (xw) Xrow[t] = eu;                          // one lane per row (exec-masked store)
+      store_pol<NIPAMD_SCR_NT>(cx.Sstore + (long)t * cx.Sstride, keep);
+      if (xw) store_pol<NIPAMD_SCR_NT>(Xrow + t, eu);                          // one lane per row (exec-masked store)
     } else {
       const double pr = keep * other;                // alpha^_t beta^_t = Z gamma_t 2^(eu + xo)
       if (first) {

@@ -35,12 +35,10 @@
 #include <cstdint>
 
 #include "chain_kernels.h"
+#include "store_pol.h"
 
 namespace nipamd {
 
-#ifndef NIPAMD_POST_NT
-#define NIPAMD_POST_NT 0
-#endif
 namespace {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -522,16 +520,12 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
         if constexpr (PVEC) {
           double* p = (ok && bb < a.B) ? a.post + (size_t)bb * a.post_bstride + (long)t * NP + a.post_off + 2 * s
                                        : sink;
-#if NIPAMD_POST_NT                                   // A/B builds: streaming posterior stores
-          __builtin_nontemporal_store(v2d{px[i] * r[i], py[i] * r[i]}, reinterpret_cast<v2d*>(p));
-#else
-          *reinterpret_cast<v2d*>(p) = v2d{px[i] * r[i], py[i] * r[i]};
-#endif
+          store_pol<NIPAMD_POST_NT>(reinterpret_cast<v2d*>(p), v2d{px[i] * r[i], py[i] * r[i]});
         } else {
           if (ok && bb < a.B) {
             double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
-            if (st0) p[0] = px[i] * r[i];
-            if (st1) p[1] = py[i] * r[i];
+            if (st0) store_pol<NIPAMD_POST_NT>(p, px[i] * r[i]);
+            if (st1) store_pol<NIPAMD_POST_NT>(p + 1, py[i] * r[i]);
           }
         }
       }
@@ -560,7 +554,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
       for (int u0 = 0; u0 < kWSeq * LPC; u0 += 64) {
         const int u = u0 + lane, jj = u / LPC, p = u % LPC;
         const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(jj, p));
-        *reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u) = v;
+        store_pol<NIPAMD_SCR_NT>(reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u), v);
       }
     }
   };

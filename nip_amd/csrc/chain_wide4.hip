@@ -23,6 +23,7 @@
 #include <cstdint>
 
 #include "chain_kernels.h"
+#include "store_pol.h"
 
 namespace nipamd {
 
@@ -296,7 +297,7 @@ __device__ __forceinline__ void w4_partner(const WideArgs& a, const W4Lds& L, in
         const int slot = j & (kW4Ring - 1);
         const double pr = L.ring[(d * kW4Ring + slot) * 64 + y] * (a.filter ? 1.0 : r[k]);
         const double q = pr * recip(wave_sum(pr));   // an all-zero row stays zero
-        if (Prow) Prow[(long)tof(j) * a.post_tstride] = q;
+        if (Prow) store_pol<NIPAMD_POST_NT>(Prow + (long)tof(j) * a.post_tstride, q);
         if (FWD) ll_step(slot);
       }
     }
@@ -567,7 +568,7 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
     for (int k = 0; k < 8; k++) {
       const int j = c + k;
       const int slot = j & (kW4Ring - 1);
-      if (j < nA) Srow[(long)(FWD ? j : T - 2 - j) * 64] = L.ring[(d * kW4Ring + slot) * 64 + y];
+      if (j < nA) store_pol<NIPAMD_SCR_NT>(Srow + (long)(FWD ? j : T - 2 - j) * 64, (double)L.ring[(d * kW4Ring + slot) * 64 + y]);
       if (j < nAf) ll_acc(wave_sum(zval(slot)));
     }
   }
@@ -596,7 +597,7 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
       wave_sum_n<2>(z);
       if (j < nB) {
         const double q = pr * recip(z[0]);           // an all-zero row stays zero
-        if (Prow) Prow[(long)tof(j) * a.post_tstride] = q;
+        if (Prow) store_pol<NIPAMD_POST_NT>(Prow + (long)tof(j) * a.post_tstride, q);
       }
       if (j < nBf) ll_acc(z[1]);
     }
