@@ -123,7 +123,12 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
     const int ts = H + 8 * ci + 4 * h + 3;
     return ts < T - 1 ? ts : T - 1;
   };
-  auto ld = [&](int ci, int h) { return load4(Sw + (long)start(ci < nchB ? ci : nchB - 1, h) * kSStep); };
+  auto ld = [&](int ci, int h) {
+    const double* p = Sw + (long)start(ci < nchB ? ci : nchB - 1, h) * kSStep;
+    const v2d u = load_pol<NIPAMD_SCR_NTLD>(reinterpret_cast<const v2d*>(p));
+    const v2d w = load_pol<NIPAMD_SCR_NTLD>(reinterpret_cast<const v2d*>(p + 8));
+    return v4d{u.x, u.y, w.x, w.y};
+  };
   // a chunk's evidence rows
   constexpr int kE = kMChunk;
   // codes two chunks ahead, evidence rows one chunk ahead: no load waits on

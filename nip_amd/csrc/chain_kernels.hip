@@ -461,7 +461,10 @@ __device__ __forceinline__ void load_chunk16(const E16Ctx<NE>& c, Prefetch16<KC,
     const int t = t0 + dir * j;
 #pragma unroll
     for (int k = 0; k < NE; k++) p.c[j][k] = c.erow16[k] + c.codes[k][t] * 16;
-    if (with_s) { p.s[j] = c.Sload[(long)t * 16]; p.x[j] = c.Xload[t]; }
+    if (with_s) {
+      p.s[j] = load_pol<NIPAMD_SCR_NTLD>(c.Sload + (long)t * 16);
+      p.x[j] = load_pol<NIPAMD_SCR_NTLD>(c.Xload + t);
+    }
   }
 #pragma unroll
   for (int j = 0; j < KC; j++) {

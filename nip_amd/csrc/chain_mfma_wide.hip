@@ -576,7 +576,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     if (NIPAMD_MW_ABLATE == 1) return;
     const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
 #pragma unroll
-    for (int c = 0; c < kWSeq; c++) o[c] = *reinterpret_cast<const v2d*>(q + c * NP);
+    for (int c = 0; c < kWSeq; c++) o[c] = load_pol<NIPAMD_SCR_NTLD>(reinterpret_cast<const v2d*>(q + c * NP));
   };
   const int nBf = T - H;                         // the forward side's phase-B steps (from t = H)
   auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {

@@ -286,7 +286,7 @@ __device__ __forceinline__ void w4_partner(const WideArgs& a, const W4Lds& L, in
   const long sstr = a.filter ? 0 : 64;
   auto load8 = [&](double (&r)[8], int c) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) r[k] = Sld[(long)tof(8 * c + k) * sstr];   // guards cover the over-run
+    for (int k = 0; k < 8; k++) r[k] = load_pol<NIPAMD_SCR_NTLD>(Sld + (long)tof(8 * c + k) * sstr);   // guards cover the over-run
   };
   auto chunk = [&](const double (&r)[8], int c) {
 #pragma unroll
@@ -583,7 +583,7 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
   const long sstr = a.filter ? 0 : 64;
   auto load8 = [&](double (&r)[8], int c) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) r[k] = Sld[(long)tof(8 * c + k) * sstr];   // guards cover the over-run
+    for (int k = 0; k < 8; k++) r[k] = load_pol<NIPAMD_SCR_NTLD>(Sld + (long)tof(8 * c + k) * sstr);   // guards cover the over-run
   };
   auto chunk = [&](const double (&r)[8], int c) {
     block_barrier();                                 // the filter's chunk c is in the ring

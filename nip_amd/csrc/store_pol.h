@@ -15,6 +15,9 @@
 #ifndef NIPAMD_SCR_NT
 #define NIPAMD_SCR_NT 0
 #endif
+#ifndef NIPAMD_SCR_NTLD
+#define NIPAMD_SCR_NTLD 0       // A/B builds: scratch rows read back (their last use) nontemporal
+#endif
 
 namespace nipamd {
 
@@ -22,6 +25,12 @@ template <bool NT, typename V>
 __device__ __forceinline__ void store_pol(V* p, const V& v) {
   if constexpr (NT) __builtin_nontemporal_store(v, p);
   else *p = v;
+}
+
+template <bool NT, typename V>
+__device__ __forceinline__ V load_pol(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
 }
 
 }  // namespace nipamd
