@@ -554,7 +554,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
       for (int u0 = 0; u0 < kWSeq * LPC; u0 += 64) {
         const int u = u0 + lane, jj = u / LPC, p = u % LPC;
         const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(jj, p));
-        store_pol<NIPAMD_SCR_NT>(reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u), v);
+        store_pol<NIPAMD_WIDE_SCR_NT>(reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u), v);
       }
     }
   };

@@ -568,7 +568,7 @@ __device__ __forceinline__ void r64_partner(const WideArgs& a, const W4Lds& L, i
     for (int k = 0; k < 8; k++) {
       const int j = c + k;
       const int slot = j & (kW4Ring - 1);
-      if (j < nA) store_pol<NIPAMD_SCR_NT>(Srow + (long)(FWD ? j : T - 2 - j) * 64, (double)L.ring[(d * kW4Ring + slot) * 64 + y]);
+      if (j < nA) store_pol<NIPAMD_WIDE_SCR_NT>(Srow + (long)(FWD ? j : T - 2 - j) * 64, (double)L.ring[(d * kW4Ring + slot) * 64 + y]);
       if (j < nAf) ll_acc(wave_sum(zval(slot)));
     }
   }
