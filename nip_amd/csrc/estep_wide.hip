@@ -44,6 +44,7 @@
 #include "chain_kernels.h"
 #include "dpp_row.h"
 #include "opchain.h"
+#include "store_pol.h"
 
 namespace nipamd {
 
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(kMsgWaves * 64) void chain_msgs_kernel(EWideArgs a)
         const double p = u * e[k];
         E += sc;
         if (active) {
-          Sa[(size_t)t * NP] = p;
+          store_pol<NIPAMD_MSG_NT>(Sa + (size_t)t * NP, p);
           if (y == 0) Ea[t] = E;
         }
         if (PR) {
@@ -611,9 +612,9 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
           m1 = __builtin_ldexp(m1, -k1); e1 += k1;
         }
         dead |= z == 0.0;
-        if (active) Srow[(size_t)t * NP] = u;           // alpha^_t
+        if (active) store_pol<NIPAMD_MSG_NT>(Srow + (size_t)t * NP, u);   // alpha^_t
       } else {
-        if (active) Srow[(size_t)(t - 1) * NP] = u;     // beta^_{t-1}
+        if (active) store_pol<NIPAMD_MSG_NT>(Srow + (size_t)(t - 1) * NP, u);   // beta^_{t-1}
       }
       sc = z != 0.0 ? -__builtin_amdgcn_frexp_exp(z) : 0;
       x = u;
