@@ -23,7 +23,7 @@
 #define NIPAMD_WIDE_SCR_NT 1    // chain_mfma_wide_kernel, chain_row64_kernel
 #endif
 #ifndef NIPAMD_MSG_NT
-#define NIPAMD_MSG_NT 0         // A/B builds: the e_step message kernels' rows (estep_wide.hip)
+#define NIPAMD_MSG_NT 1         // the wide e_step message kernels' rows (estep_wide.hip): 0.3-0.5%
 #endif
 #ifndef NIPAMD_SCR_NTLD
 #define NIPAMD_SCR_NTLD 0       // A/B builds: scratch rows read back (their last use) nontemporal
