@@ -422,7 +422,7 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
 
 template <int PROJ>
 #ifndef NIPAMD_CK_PRIO
-#define NIPAMD_CK_PRIO 2   // the partners at s_setprio 1: 0.279-0.281 vs 0.282-0.292 ms (profiles/r04/gpu/r04zd_fb*_ab.txt)
+#define NIPAMD_CK_PRIO 2   // the partners at s_setprio 1: -1% mean over 12 interleaved A/B rounds on 3 boxes (within noise; r04y, r04zd, r04f)
 #endif
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
