@@ -423,6 +423,9 @@ void chain_kernel(ChainArgs a) {
 // NSEQ sequences per block (16: 8 waves, two per SIMD; 24: 12 waves, three
 // per SIMD), waves 0 .. NSEQ/4-1 forward, the rest backward
 constexpr int kE16RowMul = 48;                 // scratch rows rounded to a multiple of every NSEQ
+#ifndef NIPAMD_E16_PIPE
+#define NIPAMD_E16_PIPE 1                      // phase B's count cells read one step ahead (0: A/B builds)
+#endif
 #ifndef NIPAMD_ESTEP_PRIO
 #define NIPAMD_ESTEP_PRIO 0
 #endif
@@ -475,6 +478,9 @@ __device__ __forceinline__ void load_chunk16(const E16Ctx<NE>& c, Prefetch16<KC,
   }
 }
 
+// step(t, e, s, x, count rows of t, j, count rows of the next step): the
+// next step's rows are in the other buffer at a chunk's last step (loaded a
+// chunk ahead; past the phase's end they are guard codes, valid rows)
 template <int KC, int NE, typename Step>
 __device__ __forceinline__ void run_phase16(const E16Ctx<NE>& c, int n, int t0, int dir, bool with_s, Step&& step) {
   Prefetch16<KC, NE> pa, pb;
@@ -484,12 +490,13 @@ __device__ __forceinline__ void run_phase16(const E16Ctx<NE>& c, int n, int t0, 
     load_chunk16(c, pb, t0 + dir * (base + KC), dir, with_s);
 #pragma unroll
     for (int j = 0; j < KC; j++)
-      if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], pa.x[j], pa.c[j], j);
+      if (base + j < n) step(t0 + dir * (base + j), pa.e[j], pa.s[j], pa.x[j], pa.c[j], j, j + 1 < KC ? pa.c[j + 1] : pb.c[0]);
     if (base + KC >= n) break;
     load_chunk16(c, pa, t0 + dir * (base + 2 * KC), dir, with_s);
 #pragma unroll
     for (int j = 0; j < KC; j++)
-      if (base + KC + j < n) step(t0 + dir * (base + KC + j), pb.e[j], pb.s[j], pb.x[j], pb.c[j], j);
+      if (base + KC + j < n)
+        step(t0 + dir * (base + KC + j), pb.e[j], pb.s[j], pb.x[j], pb.c[j], j, j + 1 < KC ? pb.c[j + 1] : pa.c[0]);
   }
 }
 
@@ -611,18 +618,28 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   double rc0 = 0.0;           // phase B: 1 / c at the phase's first step
   int E0 = 0;                 //          and that step's exponent sum
 
+  // phase B: the step's count cells (one per child).  E16_PIPE: read one
+  // step ahead, right after this step's write (the wave's LDS operations
+  // complete in order, so a next step with the same cell reads the new
+  // value), and consumed a whole step later; otherwise read at the step's
+  // start, pinned there (the compiler then waits for it at once)
+  double hn[NE];
+#pragma unroll
+  for (int k = 0; k < NE; k++) hn[k] = 0.0;
   // one step; combine: phase B (posterior, M1 count, xi), first: its first step
-  auto step = [&](int t, double e, double other, int xo, const int (&code)[NE], bool combine, bool first, int j) {
-    // phase B: this step's count cells (one per child), read before the
-    // step's arithmetic so the LDS latency overlaps it (the previous step's
-    // write to the same cell precedes it in the wave's LDS order)
+  auto step = [&](int t, double e, double other, int xo, const int (&code)[NE], bool combine, bool first, int j,
+                  const int (&cnext)[NE]) {
     double hv[NE];
 #pragma unroll
     for (int k = 0; k < NE; k++) {
       hv[k] = 0.0;
       if (combine) {
-        hv[k] = Hrow[code[k]];
-        asm volatile("" : "+v"(hv[k]));              // keep the read here
+        if (NIPAMD_E16_PIPE) {
+          hv[k] = hn[k];
+        } else {
+          hv[k] = Hrow[code[k]];
+          asm volatile("" : "+v"(hv[k]));            // keep the read here
+        }
       }
     }
     const double u = __builtin_ldexp(dot2_bcast(x, C), sc);
@@ -651,6 +668,10 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
       const double q = __builtin_ldexp(pr * rc0, E0 - (eu + xo));
 #pragma unroll
       for (int k = 0; k < NE; k++) Hrow[code[k]] = hv[k] + q;
+      if (NIPAMD_E16_PIPE) {
+#pragma unroll
+        for (int k = 0; k < NE; k++) hn[k] = Hrow[cnext[k]];
+      }
       // xi_t (forward, x = alpha^_{t-1}) / xi_{t+1} (backward, x = g_{t+1}, t + 1 < H):
       // x(.) A e_t beta_t / Z resp. alpha_t A g_{t+1} / Z, the A factor applied after the reduction
       const double f = __builtin_ldexp(rc0, E0 - (ex + xo));
@@ -680,8 +701,8 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
   if (NIPAMD_WAIT_TIMES) st[0] = __builtin_readcyclecounter();
   // phase A: forward t = 0..H-1; backward t = T-2..H
   run_phase16<KC, NE>(cx, FWD ? H : T - 1 - H, FWD ? 0 : T - 2, dir, false,
-                      [&](int t, double e, double o, int xo, const int (&c)[NE], int j) {
-                        step(t, e, o, xo, c, false, false, j);
+                      [&](int t, double e, double o, int xo, const int (&c)[NE], int j, const int (&cn)[NE]) {
+                        step(t, e, o, xo, c, false, false, j, cn);
                       });
   const int efa = ex;                                // forward: Ef_{H-1}, the phase-A m1 exponents' sum
   if (NIPAMD_WAIT_TIMES) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); st[1] = __builtin_readcyclecounter(); }
@@ -699,10 +720,16 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
       double e0 = cx.Et[c0[0]];
 #pragma unroll
       for (int k = 1; k < NE; k++) e0 *= cx.Et[c0[k]];
-      step(t0, e0, cx.Sload[(long)t0 * 16], cx.Xload[t0], c0, true, true, 3);
+      int c1[NE];                                    // the next step's rows (t0 + dir: a guard code at most)
+#pragma unroll
+      for (int k = 0; k < NE; k++) {
+        c1[k] = cx.erow16[k] + cx.codes[k][t0 + dir] * 16;
+        if (NIPAMD_E16_PIPE) hn[k] = Hrow[c0[k]];
+      }
+      step(t0, e0, cx.Sload[(long)t0 * 16], cx.Xload[t0], c0, true, true, 3, c1);
       run_phase16<KC, NE>(cx, n - 1, t0 + dir, dir, true,
-                          [&](int t, double e, double o, int xo, const int (&c)[NE], int j) {
-                            step(t, e, o, xo, c, true, false, j);
+                          [&](int t, double e, double o, int xo, const int (&c)[NE], int j, const int (&cn)[NE]) {
+                            step(t, e, o, xo, c, true, false, j, cn);
                           });
     }
   }
