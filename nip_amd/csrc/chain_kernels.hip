@@ -426,6 +426,9 @@ constexpr int kE16RowMul = 48;                 // scratch rows rounded to a mult
 #ifndef NIPAMD_E16_PIPE
 #define NIPAMD_E16_PIPE 1                      // phase B's count cells read one step ahead (0: A/B builds)
 #endif
+#ifndef NIPAMD_E16_FWD_SPARSE
+#define NIPAMD_E16_FWD_SPARSE 1                // proper mode: forward rows rescale every 4th step (0: A/B builds)
+#endif
 #ifndef NIPAMD_ESTEP_PRIO
 #define NIPAMD_ESTEP_PRIO 0
 #endif
@@ -690,7 +693,9 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     }
     // the scale of the next step (a zero mass keeps every later vector 0,
     // whatever the exponent: no zero test)
-    if (FWD && PR) sc = row_max_exp_rescale(p);
+    // (proper mode: the forward rows rescale every 4th step as the backward
+    // rows do -- NIPAMD_E16_FWD_SPARSE; the final ll reads the exponent)
+    if (FWD && PR) sc = (!NIPAMD_E16_FWD_SPARSE || (j & 3) == 3) ? row_max_exp_rescale(p) : 0;
     else sc = rescale ? -__builtin_amdgcn_frexp_exp(z2) : 0;
     x = p;
     ex = eu;

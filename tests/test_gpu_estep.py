@@ -155,6 +155,35 @@ def test_estep_missing_multiblock_vs_oracle(B, T, proper):
         assert abs(fll[b].item() - r_ll) <= LL_RTOL * max(1.0, abs(r_ll))
 
 
+def _near_identity(n, eps):
+    d = np.full((n, n), eps)
+    np.fill_diagonal(d, 1.0)
+    return (d / d.sum(axis=1, keepdims=True)).ravel()
+
+
+@pytest.mark.parametrize("T", [40, 203])
+def test_estep_peaked_proper_model_sparse_rescaling(T):
+    """A proper model (rows sum to 1: the kernel's proper mode) with a
+    near-identity transition (1e-50 off the diagonal) and emission (1e-60):
+    random data puts each step's evidence mass near 1e-50, so both filters'
+    rescaling every 4th step runs at ~1e-200 between rescales.  Counts, ll
+    and flags against the oracle (per-step normalisation, nip.c:1461-1474)."""
+    N = 16
+    nodes = [("P0", N, "P1"), ("P1", N, None), ("M1", N, None)]
+    pots = [("M1", ["P1"], _near_identity(N, 1e-60)),
+            ("P1", ["P0"], _near_identity(N, 1e-50)),
+            ("P0", [], np.full(N, 1.0 / N))]
+    m = nip_amd.Model.from_spec(nodes, pots)
+    obs = synth.observations(37, T, N, seed=T)
+    ov = [m.variable("M1")]
+    cnt, ll, st = gpu_estep(m, obs, ov)
+    assert nip_amd.last_kernel().startswith("chain_estep16_kernel")
+    rc, rl, rb = PortOracle(m.desc()).estep(obs, ov, np.ones(m.param_size()))
+    assert np.array_equal(st != 0, rb != 0) and not rb.any()
+    assert close(ll, rl, LL_RTOL)
+    assert close(cnt, rc, CNT_RTOL), np.abs(cnt - rc).max()
+
+
 def test_estep_bad_luck_flags():
     """Invalid codes / impossible data: the reference's e_step BAD_LUCK."""
     nodes, pots = synth.hmm_spec(16, 16, seed=5)
