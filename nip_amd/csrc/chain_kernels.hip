@@ -536,9 +536,11 @@ __device__ __forceinline__ int row_max_exp_rescale(double p) {
 // PR: a proper model (ChainArgs::proper): the ll is log of the final forward
 // mass minus its exponent, so the forward rows keep no m2 / m1 products and
 // rescale by the row's largest exponent, and the backward rows sum no m1.
-template <bool FWD, int KC, int NE, bool PR>
+template <bool FWD, int KC, int NE, int PRM>
 __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* Et, const uint8_t* codes,
                                              double* Htab, double* m1x, int lane, int grp, long b0, int nseqb) {
+  constexpr bool PR = PRM != 0;                     // proper mode
+  constexpr bool SP = PRM == 2;                     // and the forward rows may rescale every 4th step
   const int y = lane & 15, row = lane >> 4;
   const int seq = grp * 4 + row;                    // within the block
   const long b = b0 + seq;
@@ -693,9 +695,11 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     }
     // the scale of the next step (a zero mass keeps every later vector 0,
     // whatever the exponent: no zero test)
-    // (proper mode: the forward rows rescale every 4th step as the backward
-    // rows do -- NIPAMD_E16_FWD_SPARSE; the final ll reads the exponent)
-    if (FWD && PR) sc = (!NIPAMD_E16_FWD_SPARSE || (j & 3) == 3) ? row_max_exp_rescale(p) : 0;
+    // (SP: the forward rows rescale every 4th step as the backward rows do,
+    // when the host's bound says a product of the two directions' vectors
+    // cannot underflow -- engine.cpp estep16_sparse_ok; the final ll reads
+    // the exponent)
+    if (FWD && PR) sc = (!(SP && NIPAMD_E16_FWD_SPARSE) || (j & 3) == 3) ? row_max_exp_rescale(p) : 0;
     else sc = rescale ? -__builtin_amdgcn_frexp_exp(z2) : 0;
     x = p;
     ex = eu;
@@ -817,7 +821,7 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
 
 }  // namespace
 
-template <int NSEQ, int KC, int NE, bool PR>
+template <int NSEQ, int KC, int NE, int PR>
 __global__ __launch_bounds__(NSEQ * 32, 1)
 void chain_estep16_kernel(ChainArgs a) {
   constexpr int kE16Seqs = NSEQ, kE16Threads = NSEQ * 32, G = NSEQ / 4;
@@ -916,7 +920,7 @@ size_t chain_estep16_scratch_bytes(long B, int T) {
          (size_t)(nrow + 2) * estep16_xrow(T) * sizeof(int);
 }
 
-template <int NSEQ, int KC, int NE, bool PR>
+template <int NSEQ, int KC, int NE, int PR>
 static int estep16_launch_pr(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC, NE, PR>), lds, lds_set)) return -1;
@@ -926,8 +930,9 @@ static int estep16_launch_pr(const ChainArgs& a, size_t lds, hipStream_t stream)
 }
 template <int NSEQ, int KC, int NE>
 static int estep16_launch(const ChainArgs& a, size_t lds, hipStream_t stream) {
-  return a.proper ? estep16_launch_pr<NSEQ, KC, NE, true>(a, lds, stream)
-                  : estep16_launch_pr<NSEQ, KC, NE, false>(a, lds, stream);
+  return a.proper == 2 ? estep16_launch_pr<NSEQ, KC, NE, 2>(a, lds, stream)
+       : a.proper      ? estep16_launch_pr<NSEQ, KC, NE, 1>(a, lds, stream)
+                        : estep16_launch_pr<NSEQ, KC, NE, 0>(a, lds, stream);
 }
 
 int chain_estep16_launch(const ChainArgs& a, hipStream_t stream) {

@@ -1328,6 +1328,27 @@ static bool chain_proper(const nipamd::ChainPlan& P) {
   return true;
 }
 
+// chain_estep16_kernel's proper mode may let the forward rows rescale every
+// 4th step (as the backward rows do) when no step can shrink a vector's
+// largest entry by more than 1e-30: then either direction's vector keeps its
+// largest entry above 1e-120 between rescales and phase B's products
+// alpha^ beta^ stay far above the subnormals.  Bound: for every previous
+// state x and every code o (the missing row included), the largest entry of
+// row x of A times the evidence column of o.  One child only (the HMM shape);
+// otherwise every step rescales (tests/test_gpu_estep.py peaked models).
+static bool estep16_sparse_ok(const nipamd::ChainPlan& P, int ne) {
+  if (ne != 1 || P.emits.empty() || P.N > 64) return false;
+  const auto& E = P.emits[0];
+  for (int o = 0; o <= E.M; o++)
+    for (int x = 0; x < P.N; x++) {
+      double best = 0.0;
+      for (int y = 0; y < P.N; y++)
+        best = std::max(best, P.A64[x * 64 + y] * (o < E.M ? E.E[(size_t)o * 64 + y] : E.s[y]));
+      if (!(best >= 1e-30)) return false;
+    }
+  return true;
+}
+
 static bool chain_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars, int T, Route& r) {
   std::string why;
   const auto& P = mm->m.chain;
@@ -1599,7 +1620,7 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.counts = slab;
-    a.proper = ek == 3 && chain_proper(P) ? 1 : 0;
+    a.proper = ek == 3 && chain_proper(P) ? (estep16_sparse_ok(P, a.ne) ? 2 : 1) : 0;
 #ifdef NIPAMD_DIAGNOSTICS
     static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
     const int nblk = (nb + 15) / 16;
