@@ -426,6 +426,9 @@ constexpr int kE16RowMul = 48;                 // scratch rows rounded to a mult
 #ifndef NIPAMD_E16_PIPE
 #define NIPAMD_E16_PIPE 1                      // phase B's count cells read one step ahead (0: A/B builds)
 #endif
+#ifndef NIPAMD_E16_BWD_MAXEXP
+#define NIPAMD_E16_BWD_MAXEXP 1                // backward rows rescale by the largest exponent (0: A/B builds)
+#endif
 #ifndef NIPAMD_E16_FWD_SPARSE
 #define NIPAMD_E16_FWD_SPARSE 1                // proper mode: forward rows rescale every 4th step (0: A/B builds)
 #endif
@@ -655,7 +658,10 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     // rescale, every 4th step (j is the unrolled step index: no branch) --
     // four evidence factors cannot underflow, and the exponents carry any scale
     const bool rescale = (FWD && !PR) || (j & 3) == 3;
-    const double z2 = rescale ? row_sum(p) : 1.0;
+    // (the backward rows' rescale needs no sum: the row's largest binary
+    // exponent, four integer DPP maxes, serves as well -- NIPAMD_E16_BWD_MAXEXP)
+    constexpr bool bmx = !FWD && NIPAMD_E16_BWD_MAXEXP;
+    const double z2 = (rescale && !bmx) ? row_sum(p) : 1.0;
     if (!FWD && combine && !PR) {
       // the m1 of the forward rows' phase-A step t + 1 (< H) from alpha^_t = other
       if (!first) m1 *= row_sum(other * As);           // t + 1 < H: every step but the first
@@ -700,6 +706,7 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     // cannot underflow -- engine.cpp estep16_sparse_ok; the final ll reads
     // the exponent)
     if (FWD && PR) sc = (!(SP && NIPAMD_E16_FWD_SPARSE) || (j & 3) == 3) ? row_max_exp_rescale(p) : 0;
+    else if (bmx) sc = rescale ? row_max_exp_rescale(p) : 0;
     else sc = rescale ? -__builtin_amdgcn_frexp_exp(z2) : 0;
     x = p;
     ex = eu;
