@@ -357,23 +357,32 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         torch.cuda.synchronize()
 
     # W warmup steps; the secondary lines (whose W is the bench's own choice)
-    # continue, at most 64 steps, until min_warm_s of warmup work has run:
-    # the f64-heavy kernels run their first launches at a lower clock while
-    # the part settles (config 3: 3.2-3.7 ms before 2.8-2.9 ms,
-    # profiles/r04g_timed_region.txt); every rank runs the same count
+    # then add steps, at most 64, until about min_warm_s of warmup work has
+    # run: the f64-heavy kernels run their first launches at a lower clock
+    # while the part settles (config 3: 3.2-3.7 ms before 2.8-2.9 ms,
+    # profiles/r04g_timed_region.txt).  The extra count is agreed on before
+    # any extra step runs (a MAX over ranks), so steps that contain a
+    # collective (em's exchange) stay matched across ranks
     tw = time.perf_counter()
-    nw = 0
-    while nw < warmup or (nw < 64 and time.perf_counter() - tw < min_warm_s):
+    for _ in range(warmup):
         step()
+    nw = warmup
+    if min_warm_s > 0.0:
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
         nw += 1
-        if nw >= warmup:
-            torch.cuda.synchronize()
-    if world > 1:                                   # the same warmup count on every rank
-        n_t = torch.tensor([nw], device=dev)
-        dist.all_reduce(n_t, op=dist.ReduceOp.MAX)
-        for _ in range(int(n_t.item()) - nw):
+        one = max(time.perf_counter() - t1, 1e-6)
+        left = min_warm_s - (time.perf_counter() - tw)
+        extra = min(63, max(0, int(np.ceil(left / one))))
+        if world > 1:
+            n_t = torch.tensor([extra], device=dev)
+            dist.all_reduce(n_t, op=dist.ReduceOp.MAX)
+            extra = int(n_t.item())
+        for _ in range(extra):
             step()
-        nw = int(n_t.item())
+        nw += extra
     barrier()
     kname = nip_amd.last_kernel()       # the kernel the engine chose for this request
     # one event pair around the K steps on the launch stream (torch's current
