@@ -554,7 +554,8 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     err = "tree launch failed";
     return NIPAMD_ERROR_DEVICE;
   }
-  g_last_kernel = "op_fb_kernel (e_step) + op_xi_kernel";
+  g_last_kernel = op_xi_sort_fits(P->ncomb, T) ? "op_fb_kernel (e_step) + op_xi_sort_kernel"
+                                               : "op_fb_kernel (e_step) + op_xi_kernel";
   return 0;
 }
 
