@@ -70,6 +70,7 @@ LATENCY_STEP = {
     "chain_mfma_wide_kernel<2>": (1136.1, 32, 1),      # 2 x 8 chained MFMAs, interleaved (V3); two groups of 16
 }
 CLOCK_GHZ = 2.39                 # in-kernel clock under the chain loop (s_memtime / s_memrealtime, r03_mb_lat.txt)
+MAX_CLOCK_GHZ = 2.4              # MI355X max engine clock (MI355X_MICROARCH.md chip table)
 
 # SURVEY 8(d)'s primary per-unit figures (HBM bytes per sequence-timestep)
 PRIMARY_BYTES = {"config2": 392, "config3": 784, "config4": 264, "config5": 1544}
@@ -254,15 +255,18 @@ def pipe_roof(workload: str, kern_ms: float):
     if valu is None:
         return None
     mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
-    clock = e.get("effective_clock_ghz") or CLOCK_GHZ
+    # the part's max engine clock (MI355X_MICROARCH.md: 2400 MHz), not the
+    # clock of the counter pass (profiled passes run slower): the
+    # smallest floor the instruction counts allow, so frac is a lower bound
+    clock = MAX_CLOCK_GHZ
     per = e.get("launches_per_step", 1)
     cyc = (valu * VALU_ISSUE_CYC + (mfma or 0.0)) / N_SIMD
     floor_ms = per * cyc / (clock * 1e9) * 1e3
     return {"bound": "SIMD issue (VALU + matrix core)", "valu_insts_per_launch": valu,
             "mfma_busy_cycles_per_launch": mfma, "launches_per_step": per,
             "clock_ghz": clock, "floor_ms": floor_ms, "frac": floor_ms / kern_ms,
-            "source": "profiles/pmc_traffic.json tag %s (rocprofv3 --pmc SQ_INSTS_VALU, SQ_VALU_MFMA_BUSY_CYCLES, "
-                      "GRBM_GUI_ACTIVE)" % e.get("tag")}
+            "source": "profiles/pmc_traffic.json tag %s (rocprofv3 --pmc SQ_INSTS_VALU, SQ_VALU_MFMA_BUSY_CYCLES) "
+                      "at the max engine clock" % e.get("tag")}
 
 
 def row64_issue_roof(B: int, T: int, kern_ms: float):
@@ -397,11 +401,14 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / steps
-    if name == "em":
-        ll.zero_()
-        st.zero_()
-    if not args.no_check and (not bool(torch.isfinite(ll).all()) or int(st.abs().sum()) != 0):
-        raise SystemExit("bench: non-finite log-likelihood / zero-mass status on synthetic data (%s)" % name)
+    if not args.no_check:
+        if name == "em":
+            # em.iteration raised on any BAD_LUCK series already; its ll (the
+            # exchange's tree sum over the shard) must be finite every iteration
+            if not np.all(np.isfinite(em_state["ll"])):
+                raise SystemExit("bench: non-finite em_learn log-likelihood on synthetic data")
+        elif name != "generate" and (not bool(torch.isfinite(ll).all()) or int(st.abs().sum()) != 0):
+            raise SystemExit("bench: non-finite log-likelihood / zero-mass status on synthetic data (%s)" % name)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -589,6 +596,64 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
     return rec
 
 
+# The printed line must fit the driver's ~8 KB stdout tail with every config
+# in it (config 3 fell off a 14 KB line): each record keeps its
+# figures -- ms_per_step, value, roofline frac / achieved / traffic, the other
+# roofs' frac and floor -- and the long notes, byte breakdowns and sources go
+# to the detail file (--detail, default gpurun_out/bench_detail.json).
+ROOF_KEEP = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms", "bytes_per_unit")
+
+
+def compact_roof(roof):
+    r = {k: roof[k] for k in ROOF_KEEP if k in roof}
+    for k in ("primary", "latency", "pipe", "issue"):
+        if k in roof:
+            r[k] = {"frac": roof[k]["frac"]}
+            if "floor_ms" in roof[k]:
+                r[k]["floor_ms"] = roof[k]["floor_ms"]
+            if k == "issue" and "at_4_cycles" in roof[k]:
+                r[k]["frac_at_4cyc"] = roof[k]["at_4_cycles"]["frac"]
+    return r
+
+
+def compact_cpu(cb):
+    if not cb or "value" not in cb:
+        return cb
+    r = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+    if "port" in cb:
+        r["port_value"] = cb["port"]["value"]
+    return r
+
+
+def compact(rec, secondary=False):
+    if secondary:
+        r = {k: rec[k] for k in ("value", "ms_per_step", "steps", "warmup") if k in rec}
+        r["workload"] = rec["config"]["workload"]
+    else:
+        r = {k: v for k, v in rec.items() if k not in ("roofline", "cpu_baseline", "secondary", "em", "fold")}
+    r["roofline"] = compact_roof(rec["roofline"])
+    if "cpu_baseline" in rec:
+        r["cpu_baseline"] = compact_cpu(rec["cpu_baseline"])
+    if "em" in rec:
+        r["em"] = {k: rec["em"][k] for k in ("exchange_ms_median", "exchange_bytes_per_rank")}
+    if "fold" in rec:
+        r["fold"] = {"kernel_ms": rec["fold"]["kernel_ms"], "frac": rec["fold"]["roofline"]["frac"]}
+    if "pcie_inclusive" in rec:
+        r["pcie_inclusive"] = {k: rec["pcie_inclusive"][k] for k in ("value", "ms")}
+    return r
+
+
+def rounded(x):
+    """Floats to 6 significant digits (the line's size; the detail file keeps all)."""
+    if isinstance(x, float):
+        return float("%.6g" % x)
+    if isinstance(x, dict):
+        return {k: rounded(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [rounded(v) for v in x]
+    return x
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -606,9 +671,14 @@ def main():
                          "clique smoothing; jtree: a factorial HMM on the general join-tree engine; "
                          "joint: the same slice as a joint-interface chain; generate: generate_data")
     ap.add_argument("--no-secondary", action="store_true", help="the headline workload only")
+    ap.add_argument("--min-warm", type=float, default=0.0,
+                    help="headline: add warmup steps until this many seconds of warmup ran (the secondary "
+                         "lines use 0.5; kernel traces of a secondary workload run it as the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="the full records (notes, byte breakdowns, roof sources) as JSON ('' = none)")
     args = ap.parse_args()
     world = launch_or_check(args, sys.argv[1:])
     rank = int(os.environ.get("RANK", "0"))
@@ -630,23 +700,33 @@ def main():
     torch.cuda.set_device(dev)
 
     steps = args.steps or WORKLOADS[args.workload][6]
-    rec = run_workload(args.workload, args, world, rank, dev, steps, args.warmup)
+    rec = run_workload(args.workload, args, world, rank, dev, steps, args.warmup, min_warm_s=args.min_warm)
     if args.workload in cpu:
         rec["cpu_baseline"] = cpu[args.workload]
     if world == 1 and rank == 0 and not args.no_cpu_baseline and args.workload == "generate":
         rec["cpu_baseline"] = cpu_baseline_generate(*WORKLOADS["generate"][1](args), T=rec["config"]["T"])
+    line = compact(rec)
+    detail = {"headline": rec}
     if secondary:
-        sec = {}
+        sec, full = {}, {}
         for w in secondary:
             r = run_workload(w, args, world, rank, dev, WORKLOADS[w][6], 2 if w != "em" else 1, min_warm_s=0.5)
             if w in cpu:
                 r["cpu_baseline"] = cpu[w]
             key = WORKLOADS[w][0] if w != "estep_config3" else "config3_estep"
-            sec[key] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config",
-                                                      "roofline", "cpu_baseline", "em", "fold") if k in r}
-        rec["secondary"] = sec
+            full[key] = r
+            sec[key] = compact(r, secondary=True)
+        line["secondary"] = sec
+        detail["secondary"] = full
     if rank == 0:
-        print(json.dumps(rec))
+        if args.detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+                with open(args.detail, "w") as f:
+                    json.dump(detail, f, indent=1)
+            except OSError as e:
+                print("bench: detail file not written: %s" % e, file=sys.stderr)
+        print(json.dumps(rounded(line)))
     if world > 1:
         dist.destroy_process_group()
 

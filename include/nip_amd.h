@@ -245,7 +245,8 @@ int nipamd_estep_host(nipamd_model* m, const int32_t* obs, int n_obs,
  * sized by the request -- its per-evidence-combination sums, whose count
  * depends on the observed variables -- so its partial is
  * nipamd_estep_partial_size_req doubles (nipamd_estep_partial_size for every
- * other route; the _req form is always large enough).  nipamd_estep_partial requires
+ * other route; the _req form is always large enough) and is written only by
+ * nipamd_estep_partial_ex given that capacity.  nipamd_estep_partial requires
  * d_status (NIP_ERROR_INVALID_ARGUMENT otherwise) when the model's e_step
  * rejects series with a long leading missing run
  * (nipamd_estep_prefix_first_bad >= 0): the verdict is reported there.
@@ -255,6 +256,16 @@ int nipamd_estep_partial_size_req(nipamd_model* m, int n_obs, const int* obs_var
 int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,
                          const int* obs_vars, int B, int T, double* d_partial,
                          double* d_ll, uint32_t* d_status, void* stream);
+/* The same with the partial's capacity in doubles.  nipamd_estep_partial
+ * promises only nipamd_estep_partial_size doubles, so it never takes the
+ * operator chain's e_step (whose partial is larger): such requests run on the
+ * general engine there.  With capacity >= nipamd_estep_partial_size_req the
+ * operator chain takes them; capacity < nipamd_estep_partial_size fails with
+ * NIP_ERROR_INVALID_ARGUMENT. */
+int nipamd_estep_partial_ex(nipamd_model* m, const int32_t* d_obs, int n_obs,
+                            const int* obs_vars, int B, int T, double* d_partial,
+                            long capacity, double* d_ll, uint32_t* d_status,
+                            void* stream);
 int nipamd_estep_finalize(nipamd_model* m, const double* d_partial,
                           double* d_counts, void* stream);
 
@@ -277,8 +288,11 @@ int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double*
  * rounding turned > 0, or a mass was <= 0 -- or -1 if no such step exists.
  * nipamd_estep / _partial set NIPAMD_STATUS_BAD_LUCK on every such series in
  * d_status.  Computed on the host once per model version (the join tree's
- * state over missing steps does not depend on the data); -2 when the model's
- * tables exceed 2^20 entries, whose leading missing runs are not simulated.
+ * state over missing steps does not depend on the data); -2 when the run was
+ * not simulated -- the model's tables exceed 2^26 entries, or the simulation's
+ * work bound (2^29 table entries x steps for a chain whose forward message has
+ * not repeated within 32 steps) ran out -- and its leading missing runs are
+ * accepted.
  */
 int nipamd_estep_prefix_first_bad(nipamd_model* m, int T);
 

@@ -50,6 +50,7 @@ EXPORTS = [
     "nipamd_fb", "nipamd_fb_host", "nipamd_estep", "nipamd_m_step",
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error", "nipamd_last_kernel",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial_size_req", "nipamd_estep_partial",
+    "nipamd_estep_partial_ex",
     "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_tree_sum", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
@@ -104,6 +105,8 @@ def lib():
         if hasattr(L, "nipamd_estep_partial_size_req"):      # (absent from A/B builds of older revisions)
             L.nipamd_estep_partial_size_req.argtypes = [vp, C.c_int, ip, C.c_int]
         L.nipamd_estep_partial.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp, vp]
+        if hasattr(L, "nipamd_estep_partial_ex"):            # (absent from A/B builds of older revisions)
+            L.nipamd_estep_partial_ex.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, C.c_long, vp, vp, vp]
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
         L.nipamd_estep_prefix_first_bad.argtypes = [vp, C.c_int]
         L.nipamd_tree_sum.argtypes = [vp, C.c_long, C.c_int, vp, vp, vp]
@@ -548,7 +551,14 @@ def estep_partial(model: Model, obs, obs_vars, partial=None, ll=None, status=Non
     partial = _out_buf(partial, (S,), torch.float64, dev, "partial")
     ll = _out_buf(ll, (B,), torch.float64, dev, "ll")
     status = _out_buf(status, (B,), torch.int32, dev, "status")
-    _check(lib().nipamd_estep_partial(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars),
+    if hasattr(L, "nipamd_estep_partial_ex"):
+        # with the request's capacity: the operator chain may take the request
+        _check(L.nipamd_estep_partial_ex(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars), B, T,
+                                         C.c_void_p(partial.data_ptr()), int(partial.numel()),
+                                         C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()),
+                                         _stream_ptr(stream)))
+    else:
+        _check(L.nipamd_estep_partial(model._h, C.c_void_p(obs.data_ptr()), nobs, _ints(obs_vars),
                                       B, T, C.c_void_p(partial.data_ptr()), C.c_void_p(ll.data_ptr()),
                                       C.c_void_p(status.data_ptr()), _stream_ptr(stream)))
     return partial, ll, status

@@ -1275,19 +1275,25 @@ static bool wide_estep_ok(const nipamd_model* mm, int n_obs, const int* obs_vars
 // The request's route is the operator chain's e_step (the chain and wide
 // routes decline it, the engine choice is automatic and the operator chain
 // takes it): its partial carries a section after the route tag.
-static bool op_estep_route(nipamd_model* mm, int n_obs, const int* obs_vars, int T) {
+// capacity: the caller's partial in doubles (-1: unbounded, the size query).
+// The operator chain's partial is larger than nipamd_estep_partial_size, so a
+// partial of that size (nipamd_estep_partial, which takes no capacity) runs
+// such requests on the general engine, whose partial fits.
+static bool op_estep_route(nipamd_model* mm, int n_obs, const int* obs_vars, int T, long capacity) {
   Route r;
   if (mm->engine != NIPAMD_ENGINE_AUTO || chain_estep_ok(mm, n_obs, obs_vars, T, r) ||
       wide_estep_ok(mm, n_obs, obs_vars, r))
     return false;
   std::string why;
-  return nipamd::op_estep_supported(mm, n_obs, obs_vars, T, why);
+  if (!nipamd::op_estep_supported(mm, n_obs, obs_vars, T, why)) return false;
+  return capacity < 0 ||
+         capacity >= (long)nipamd_estep_partial_size(mm) + (long)nipamd::op_estep_section(mm, n_obs, obs_vars);
 }
 
 int nipamd_estep_partial_size_req(nipamd_model* mm, int n_obs, const int* obs_vars, int T) {
   if (!mm || T < 1 || (n_obs > 0 && !obs_vars)) return -1;
   const int base = nipamd_estep_partial_size(mm);
-  if (base < 0 || !op_estep_route(mm, n_obs, obs_vars, T)) return base;
+  if (base < 0 || !op_estep_route(mm, n_obs, obs_vars, T, -1)) return base;
   return base + (int)nipamd::op_estep_section(mm, n_obs, obs_vars);
 }
 
@@ -1397,13 +1403,35 @@ static int prefix_first_bad(nipamd_model* mm, int T) {
 }
 
 static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
-                                int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
-                                void* stream);
+                                int B, int T, double* d_partial, long capacity, double* d_ll,
+                                uint32_t* d_status, void* stream);
 static int ensure_etab_all(nipamd_model* mm);
+static int estep_partial_cap(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                             int B, int T, double* d_partial, long capacity, double* d_ll,
+                             uint32_t* d_status, void* stream);
 
 int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
                          int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
                          void* stream) {
+  if (!mm) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const int base = nipamd_estep_partial_size(mm);
+  return estep_partial_cap(mm, d_obs, n_obs, obs_vars, B, T, d_partial, base > 0 ? base : 0, d_ll, d_status,
+                           stream);
+}
+
+int nipamd_estep_partial_ex(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                            int B, int T, double* d_partial, long capacity, double* d_ll,
+                            uint32_t* d_status, void* stream) {
+  if (!mm) return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  const int base = nipamd_estep_partial_size(mm);
+  if (base >= 0 && capacity < base)
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "partial capacity below nipamd_estep_partial_size");
+  return estep_partial_cap(mm, d_obs, n_obs, obs_vars, B, T, d_partial, capacity, d_ll, d_status, stream);
+}
+
+static int estep_partial_cap(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
+                             int B, int T, double* d_partial, long capacity, double* d_ll,
+                             uint32_t* d_status, void* stream) {
   if (!mm || B < 0 || T < 1 || !d_partial || (n_obs > 0 && (!d_obs || !obs_vars)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   // The reference rejects series whose leading missing run reaches the
@@ -1412,7 +1440,8 @@ int nipamd_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, cons
   if (!d_status && B > 0 && prefix_first_bad(mm, T) >= 0)
     return fail(NIP_ERROR_INVALID_ARGUMENT,
                 "d_status is required: this model's e_step rejects series with a long leading missing run");
-  if (int rc = estep_partial_routes(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
+  if (int rc = estep_partial_routes(mm, d_obs, n_obs, obs_vars, B, T, d_partial, capacity, d_ll, d_status,
+                                    stream))
     return rc;
   if (!d_status || B == 0) return 0;
   // the kernels are queued: this host work overlaps them
@@ -1440,7 +1469,9 @@ int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double*
 int nipamd_estep_prefix_first_bad(nipamd_model* mm, int T) {
   if (!mm || T < 1) { fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments"); return -2; }
   if (nipamd::estep_prefix_entries(mm->m) > kPrefixMaxEntries) return -2;
-  return prefix_first_bad(mm, T);
+  const int k = prefix_first_bad(mm, T);
+  // -2: the simulation's work bound ran out (not simulated), not "no step"
+  return k < 0 && mm->pf_first_bad == -2 ? -2 : k;
 }
 
 // A route writes the first `written` doubles of the body; the rest (another
@@ -1469,10 +1500,17 @@ static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d
   if (int rc = ensure_tables(mm)) return rc;
   ReqTables* rt = nullptr;
   if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
-  // sequences per launch: the messages of a chunk stay within ~4 GB of HBM
+  // sequences per launch: the messages of a chunk stay within ~4 GB of HBM,
+  // and the chunk is a power of two (>= 16), so every chunk's tree is a
+  // subtree of the batch's tree and power-of-two shards combine into exactly
+  // the whole batch's partial (nip_amd.h).  NIPAMD_ESTEP_WIDE_BYTES lowers the
+  // byte budget in diagnostics builds (the multi-chunk shard-invariance test).
   const size_t per_seq = nipamd::estep_wide_scratch_bytes(P.N, 1, T);
-  long chunk = (long)std::min<size_t>(kEstepChunk, std::max<size_t>(16, ((size_t)4 << 30) / per_seq));
-  chunk = std::max(16L, chunk / 16 * 16);
+  size_t budget = (size_t)4 << 30;
+  if (const char* wb = nipamd::diag_env("NIPAMD_ESTEP_WIDE_BYTES")) budget = (size_t)std::atoll(wb);
+  const size_t cap = std::min<size_t>(kEstepChunk, std::max<size_t>(16, budget / per_seq));
+  long chunk = 16;
+  while ((size_t)chunk * 2 <= cap) chunk *= 2;
   if (B < chunk) chunk = B;
   const long nchunks = (B + chunk - 1) / chunk;
   const long rows = (chunk + 15) / 16;
@@ -1530,8 +1568,8 @@ static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d
 }
 
 static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars,
-                                int B, int T, double* d_partial, double* d_ll, uint32_t* d_status,
-                                void* stream) {
+                                int B, int T, double* d_partial, long capacity, double* d_ll,
+                                uint32_t* d_status, void* stream) {
   Route r;
   if (!chain_estep_ok(mm, n_obs, obs_vars, T, r)) {
     Route rw;
@@ -1539,7 +1577,7 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       return estep_wide_partial(mm, rw, d_obs, n_obs, B, T, d_partial, d_ll, d_status, stream);
     if (mm->engine == NIPAMD_ENGINE_CHAIN)
       return fail(NIPAMD_ERROR_UNSUPPORTED, "chain e_step covers interface chains with evidence on their children");
-    if (op_estep_route(mm, n_obs, obs_vars, T)) {
+    if (op_estep_route(mm, n_obs, obs_vars, T, capacity)) {
       // the operator chain (opchain.cpp): body zeros, the tag (-1, -1, -1)
       // that no other route's tag combines with, then its section
       const int body = estep_body_size(mm);
@@ -2061,7 +2099,7 @@ int nipamd_estep(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* o
     d->R_size = S;
   }
   double* part = d->R;
-  int rc = nipamd_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, part, d_ll, d_status, stream);
+  int rc = nipamd_estep_partial_ex(mm, d_obs, n_obs, obs_vars, B, T, part, S, d_ll, d_status, stream);
   if (rc) return rc;
   return nipamd_estep_finalize(mm, part, d_counts, stream);
 }

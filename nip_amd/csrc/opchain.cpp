@@ -311,12 +311,17 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
 // enumeration as the operators; the finalize applies it.
 //
 // Partial section (after the model's route tag, nipamd_estep_partial_size_req):
-//   [count, n_obs, ov[kOpMaxObs], K, ncomb | Xi [(ncomb + 1) K K] | P0 [K]]
-// -- the header's entries are summed with the partials and read back divided
-// by the count (exact for these small integers).
+//   [count, f[kOpFields], f^2[kOpFields] | Xi [(ncomb + 1) K K] | P0 [K]]
+// with the request's fields f = (n_obs, ov[kOpMaxObs], K, ncomb) -- the
+// header's entries are summed with the partials and read back divided by the
+// count (exact for these small integers); the squares make the check exact:
+// sum(f^2) / n == (sum(f) / n)^2 only when every partial had the same f, so
+// partials of different requests whose fields merely average to integers
+// ([1] and [3] giving [2], permuted lists) are refused.
 namespace {
 
-constexpr int kOpHdr = 4 + kOpMaxObs;
+constexpr int kOpFields = 3 + kOpMaxObs;
+constexpr int kOpHdr = 1 + 2 * kOpFields;
 constexpr long kOpMaxMapEntries = 1L << 27;
 
 bool build_map(const Model& m, OpPlan& P) {
@@ -465,6 +470,7 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   for (int i = 0; i < kOpMaxObs; i++) hdr[2 + i] = i < n_obs ? obs_vars[i] : -1.0;
   hdr[2 + kOpMaxObs] = K;
   hdr[3 + kOpMaxObs] = P->ncomb;
+  for (int i = 0; i < kOpFields; i++) hdr[1 + kOpFields + i] = hdr[1 + i] * hdr[1 + i];
   if (hipMemcpyAsync(d_sec, hdr, sizeof(hdr), hipMemcpyHostToDevice, st) != hipSuccess) {
     err = "header copy";
     return NIPAMD_ERROR_DEVICE;
@@ -567,15 +573,20 @@ int op_estep_finalize(nipamd_model* mm, const double* d_sec, double* d_counts, v
     return NIPAMD_ERROR_DEVICE;
   }
   const double n = hdr[0];
-  auto val = [&](double v, int& out) {
-    const double q = v / n;
+  // field i of every combined partial was the same integer
+  auto val = [&](int i, int& out) {
+    const double q = hdr[1 + i] / n;
     out = (int)q;
-    return q == (double)out;
+    return q == (double)out && hdr[1 + kOpFields + i] / n == q * q;
   };
   int nobs = 0, ov[kOpMaxObs], K = 0, ncomb = 0;
-  bool ok = n >= 1.0 && n == (double)(long)n && val(hdr[1], nobs) && nobs >= 0 && nobs <= kOpMaxObs &&
-            val(hdr[2 + kOpMaxObs], K) && val(hdr[3 + kOpMaxObs], ncomb);
-  for (int i = 0; ok && i < nobs; i++) ok = val(hdr[2 + i], ov[i]);
+  bool ok = n >= 1.0 && n == (double)(long)n && val(0, nobs) && nobs >= 0 && nobs <= kOpMaxObs &&
+            val(1 + kOpMaxObs, K) && val(2 + kOpMaxObs, ncomb);
+  for (int i = 0; ok && i < kOpMaxObs; i++) {
+    int v = 0;
+    ok = val(1 + i, v);
+    if (i < nobs) ov[i] = v;
+  }
   if (!ok) { err = "operator-chain e_step partial: inconsistent header (partials of different requests combined?)"; return NIP_ERROR_INVALID_ARGUMENT; }
   OpPlan* P = plan_for(mm, nobs, ov);
   if (!P->ok || P->K != K || P->ncomb != ncomb) {

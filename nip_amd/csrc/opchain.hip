@@ -156,7 +156,7 @@ void op_fb_kernel(OpArgs a) {
   int sc = 0;
   double m2 = 1.0, m1 = 1.0;
   int e2 = 0, e1 = 0;
-  bool dead = false;
+  bool dead = false, bad = false;
   if (fwd) {
     x = ys ? a.pi[y] : 0.0;
   } else {
@@ -193,6 +193,10 @@ void op_fb_kernel(OpArgs a) {
       const int k1 = m1 != 0.0 ? __builtin_amdgcn_frexp_exp(m1) : 0;
       m2 = __builtin_ldexp(m2, -k2); e2 += k2;
       m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+      // e_step's BAD_LUCK (nip.c:1827-1854): a mass <= 0, or the running ll
+      // > 0, i.e. m2 2^e2 > m1 2^e1 (both mantissas in [0.5, 1)), as the
+      // general engine's e_step checks it after every step with evidence
+      if (est && (m2 <= 0.0 || m1 <= 0.0 || e2 > e1 || (e2 == e1 && m2 > m1))) bad = true;
     }
     if (fwd && valid) dead |= z == 0.0;
     if (a.filter) {
@@ -264,7 +268,9 @@ void op_fb_kernel(OpArgs a) {
     double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
-    if (a.status) a.status[b] = dead ? 1u : 0u;        // NIPAMD_STATUS_ZERO_MASS
+    // NIPAMD_STATUS_ZERO_MASS (1); in e_step mode also NIPAMD_STATUS_BAD_LUCK
+    // (2), which a zero mass implies, as the general engine's e_step sets them
+    if (a.status) a.status[b] = (dead ? 1u : 0u) | (est && (dead || bad) ? 2u : 0u);
   }
 }
 

@@ -122,17 +122,14 @@ def run(which, name, procs, budget, desc=None):
     units = sum(r[1] for r in res)
     wall = max(r[2] for r in res)
     seqs = units // T
-    what = "e_step with pseudo-counts 1.0" if kind == "estep" else "forward_backward_inference with ll"
-    code = ("the reference's own code (oracle/_ref/libnipref.so: nippotential.c, nipjointree.c, ... "
-            "compiled unmodified from the reference sources; nip.c's time loop restated in "
-            "oracle/ref/nipref_harness.c), gcc -O2" if which == "reference"
-            else "the C restatement oracle/nip_oracle.c, gcc -O2")
+    what = "e_step" if kind == "estep" else "fwd-bwd + ll"
+    # oracle/_ref: the reference's nippotential.c, nipjointree.c, ... compiled
+    # unmodified, nip.c's time loop restated in oracle/ref/nipref_harness.c
+    code = "oracle/_ref (reference sources, gcc -O2)" if which == "reference" else "oracle/nip_oracle.c (gcc -O2)"
     return {"value": units / wall, "unit": "sequence-timesteps/s", "cores": procs,
             "kind": which if which == "reference" else "port",
-            "sample": "%d sequences x T=%d of the bench workload (first %d slices)%s, %s, %s, "
-                      "%d processes (one per core), %.1f s" % (
-                          seqs, T, T, "" if name != "config5" else " -- the 16.7M-entry in-clique",
-                          what, code, procs, wall)}
+            "sample": "%d seq x T=%d of the bench inputs%s, %s, %s, %d procs, %.1f s" % (
+                seqs, T, "" if name != "config5" else " (first slices)", what, code, procs, wall)}
 
 
 def main():

@@ -44,7 +44,7 @@ def test_host_side_errors():
 def test_request_sized_estep_partials():
     """nipamd_estep_partial_size_req (host only): the model-level size for
     requests the chain routes take, plus the operator chain's section --
-    header (12) + (ncomb + 1) K^2 + K -- for one they decline (demo1 with its
+    header (23: count, 11 request fields, their squares) + (ncomb + 1) K^2 + K -- for one they decline (demo1 with its
     hidden parent D1 observed: K = 2 joint states of C, 3 x 3 x 3 evidence
     combinations); the general engine's requests keep the model size."""
     m = nip_amd.Model.from_net(os.path.join(ROOT, "tests", "golden", "demo1.net"))
@@ -56,6 +56,6 @@ def test_request_sized_estep_partials():
     ncomb = 1
     for v in abd:
         ncomb *= m.card(v) + 1
-    assert m.partial_size(abd, 40) == base + 12 + (ncomb + 1) * K * K + K
+    assert m.partial_size(abd, 40) == base + 23 + (ncomb + 1) * K * K + K
     m.set_engine(nip_amd.ENGINE_JTREE)
     assert m.partial_size(abd, 40) == m.partial_size()

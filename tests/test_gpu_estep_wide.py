@@ -119,6 +119,21 @@ def test_wide_partial_is_shard_invariant_and_reproducible():
     assert comb[-3:].tolist() == [0.0, 0.0, 4.0] and whole[-3:].tolist() == [0.0, 0.0, 1.0]
 
 
+def test_wide_partial_shard_invariant_over_launch_chunks():
+    """The launch chunk of the wide e_step is a power of two even when the
+    per-launch byte budget would allow 48 sequences: shard
+    partials still combine into the batch's bit for bit.  Runs in a worker on
+    the diagnostics build, whose NIPAMD_ESTEP_WIDE_BYTES lowers the budget."""
+    import subprocess
+    import sys
+    from nip_amd import build as nb
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "_estep_wide_chunk_worker.py")],
+                       env=dict(os.environ, NIPAMD_LIB=nb.DIAG_LIB), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "all passed" in r.stdout
+
+
 def test_config5_model_estep_matches_reference_golden():
     """Config 5's model (64^4 in-clique folded on the GPU, hidden parents Y1
     and Z1): the reference's own e_step on gappy series (wide64_prefix.npz) --

@@ -70,7 +70,7 @@ def test_op_estep_equals_general_engine(T):
     b = estep(m, obs, ov, nip_amd.ENGINE_JTREE)
     assert close_cnt(a[0], b[0]), np.abs(a[0] - b[0]).max()
     assert close_ll(a[1], b[1])
-    assert np.array_equal(a[2] != 0, b[2] != 0)
+    assert np.array_equal(a[2], b[2])           # the status words, bit for bit
 
 
 def test_op_estep_vs_oracle():
@@ -105,7 +105,8 @@ def test_op_estep_zero_mass_sequences():
     obs[17, 0, 2] = m.card(ov[2]) + 3
     a = estep(m, obs, ov)
     b = estep(m, obs, ov, nip_amd.ENGINE_JTREE)
-    assert np.array_equal(a[2] != 0, b[2] != 0) and (a[2] != 0).sum() == 2
+    assert np.array_equal(a[2], b[2]) and (a[2] != 0).sum() == 2
+    assert set(a[2][a[2] != 0].tolist()) == {3}   # ZERO_MASS | BAD_LUCK, as the general engine's e_step
     assert close_cnt(a[0], b[0])
     assert close_ll(a[1], b[1])
 
@@ -126,7 +127,8 @@ def test_op_partial_shard_invariant_and_refused_with_others():
     body = m.partial_size() - 3
     assert whole[body:body + 3].tolist() == [-1.0, -1.0, -1.0]
     assert comb[body:body + 3].tolist() == [-4.0, -4.0, -4.0]
-    assert torch.equal(comb[body + 3 + 12:], whole[body + 3 + 12:])      # the xi sums and P0
+    hdr = 1 + 2 * (3 + 8)                     # opchain.cpp kOpHdr: count, 11 request fields and their squares
+    assert torch.equal(comb[body + 3 + hdr:], whole[body + 3 + hdr:])    # the xi sums and P0
     c1 = nip_amd.estep_finalize(m, whole, None).cpu().numpy()
     c4 = nip_amd.estep_finalize(m, comb, None).cpu().numpy()
     assert np.array_equal(c1, c4)
@@ -139,6 +141,40 @@ def test_op_partial_shard_invariant_and_refused_with_others():
     mixed[:g.numel()] += g
     with pytest.raises(nip_amd.NipError):
         nip_amd.estep_finalize(m, mixed, None)
+
+
+def test_plain_partial_api_never_overruns_the_model_level_size():
+    """nipamd_estep_partial takes no capacity and promises only
+    nipamd_estep_partial_size doubles, so it runs an operator-chain request on
+    the general engine (route tag (0, 1, 0)) and writes nothing past that size;
+    nipamd_estep_partial_ex with the request's size takes the operator chain,
+    and one below the model-level size is refused."""
+    import ctypes as C
+    m, ov, obs = demo1_hidden(24, 64, seed=12)
+    o = torch.from_numpy(obs).cuda().contiguous()
+    L = nip_amd.lib()
+    base = L.nipamd_estep_partial_size(m._h)
+    req = m.partial_size(ov, 24)
+    assert req > base
+    buf = torch.full((req + 64,), 7.0, dtype=torch.float64, device="cuda")
+    ll = torch.empty(64, dtype=torch.float64, device="cuda")
+    st = torch.empty(64, dtype=torch.int32, device="cuda")
+    ivars = (C.c_int * len(ov))(*ov)
+    rc = L.nipamd_estep_partial(m._h, C.c_void_p(o.data_ptr()), len(ov), ivars, 64, 24, C.c_void_p(buf.data_ptr()),
+                                C.c_void_p(ll.data_ptr()), C.c_void_p(st.data_ptr()), None)
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert nip_amd.last_kernel().startswith("jt_"), nip_amd.last_kernel()
+    assert buf[base - 3:base].tolist() == [0.0, 1.0, 0.0]
+    assert bool((buf[base:] == 7.0).all())                     # nothing written past the promised size
+    g = nip_amd.estep_finalize(m, buf[:base], None).cpu().numpy()
+    a = estep(m, obs, ov)
+    assert a[3].startswith("op_fb_kernel")
+    assert close_cnt(g, a[0]), np.abs(g - a[0]).max()
+    rc = L.nipamd_estep_partial_ex(m._h, C.c_void_p(o.data_ptr()), len(ov), ivars, 64, 24,
+                                   C.c_void_p(buf.data_ptr()), base - 1, C.c_void_p(ll.data_ptr()),
+                                   C.c_void_p(st.data_ptr()), None)
+    assert rc == nip_amd.NIP_ERROR_INVALID_ARGUMENT
 
 
 def test_op_em_learn_matches_general_engine():
