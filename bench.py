@@ -428,7 +428,14 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
         kname += " + tree64 + finalize"
     elif name == "estep_config3":
-        if kname.startswith("chain_msgs_kernel"):
+        if kname.startswith("chain_estep_mw_kernel"):
+            NP = 32
+            bpu = 2 * 4 * len(ov) + 2 * 8 * NP + 8
+            bnote = ("obs %d (read by both filters) + half of each direction's messages written to the scratch and "
+                     "read back (%d + %d) + their exponents 8; the three sums stay on chip"
+                     % (2 * 4 * len(ov), 8 * NP, 8 * NP))
+            kname += " + tree64 + map finalize"
+        elif kname.startswith("chain_msgs_kernel"):
             NP = 16 if N <= 16 else 32 if N <= 32 else 64
             bpu = 3 * 4 * len(ov) + 4 * 8 * NP + 8
             bnote = ("obs %d (read by both filters and the statistics kernel) + alpha^ and beta^ written and read "

@@ -267,6 +267,47 @@ bool estep_wide_fits(int N, int R);
 size_t estep_wide_scratch_bytes(int N, long B, int T);
 int estep_wide_launch(const EWideArgs& a, hipStream_t stream);
 
+// fused matrix-core e_step for interface chains of 17..32 states (estep_mw.hip,
+// round 5): chain_mfma_wide_kernel's block (two groups of 16 sequences, a
+// matrix-core filter and a partner wave per direction and group), whose
+// partners form the e_step's three sums in phase B on the matrix cores
+// instead of writing posteriors -- the messages never leave the chip beyond
+// the phase-A scratch round trip.  Writes the wide slab (estep_wide_slab,
+// NP = 32) one row per 16 sequences.
+struct EMwArgs {
+  const int* obs;        // int32 observations [B][T][n_obs]
+  long obs_bstride;
+  int obs_tstride;
+  int ncol;              // observed children (evidence columns, 0: the row sums only)
+  int col[4], M[4];
+  int tab_off[4];        // doubles: column k's table [(M_k + 2)][32] within tab (column 0 x ebase)
+  int tab_rows;
+  const double* tab;
+  long B;
+  int T, H, N;
+  const double* A;       // [64][64]
+  const double* pi;      // [64]
+  const double* w;       // [64] = A s_all (ll weights)
+  double* S;             // estep_mw_scratch_bytes
+  double* ll;
+  unsigned* status;
+  double* slab;          // [ceil(B / 16)][slab_size]: K [32][32], H [R][32], P0 [32]
+  int slab_size, R;
+  // per evidence column: first virtual row of its in-range codes (the
+  // matrix-core count rows, sum_k M_k <= 64) and its child's first slab row
+  int voff[4], crow[4];
+  // the plan's children no column observes: their missing rows take every
+  // step's posterior (the code is always "missing"); their other rows are 0
+  int n_unobs;
+  int urow[4], uM[4];
+  unsigned long long* diag;   // stamps builds: per group [4 waves][4] cycles, else null
+};
+size_t estep_mw_lds_bytes(int tab_rows);
+int estep_mw_max_cols();
+size_t estep_mw_scratch_bytes(long B, int T);
+// -2: the request does not fit the kernel (N > 32, more than 64 count rows, LDS)
+int estep_mw_launch(const EMwArgs& a, hipStream_t stream);
+
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);
 // matrix-core variant (chain_mfma.hip): 16 sequences per 4-wave block

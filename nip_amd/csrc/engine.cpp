@@ -1487,9 +1487,107 @@ static int zero_tail(nipamd_model* mm, double* d_partial, int written, hipStream
 // a chunk of sequences, the statistics kernel writes one slab row per 16
 // sequences, and the fixed-order tree sums the rows (per chunk, then over
 // the chunks) into the partial.
+// The fused matrix-core e_step (estep_mw.hip) for 17..32 states: the wide
+// slab layout (K [32][32], H [R][32], P0 [32]), one row per 16 sequences.
+// taken = false (nothing done) when the request does not fit the kernel: the
+// caller takes the two-kernel route.
+static int estep_mw_partial(nipamd_model* mm, const Route& r, const int32_t* d_obs, int n_obs, int B, int T,
+                            double* d_partial, double* d_ll, uint32_t* d_status, void* stream, bool& taken) {
+  const auto& P = mm->m.chain;
+  taken = false;
+  if (nipamd::estep_wide_np(P.N) != 32 || r.ncol > nipamd::estep_mw_max_cols() || P.emits.size() > 4) return 0;
+  if (nipamd::diag_env("NIPAMD_ESTEP_WIDE_TWO_KERNELS")) return 0;   // A/B: the round-4 route
+  int rows = 0;
+  bool seen[4] = {false, false, false, false};
+  for (int i = 0; i < r.ncol; i++) {
+    const int k = r.emit[i];
+    if (k < 0 || k >= (int)P.emits.size() || seen[k]) return 0;
+    seen[k] = true;
+    rows += P.emits[k].M;
+  }
+  if (rows > 64) return 0;
+  if (int rc = ensure_tables(mm)) return rc;
+  ReqTables* rt = nullptr;
+  if (int rc = ensure_req_tables(mm, r, &rt)) return rc;
+  if (nipamd::estep_mw_lds_bytes(rt->mtab_rows) > 160 * 1024) return 0;
+  taken = true;
+  const int R = estep_rows(P);
+  const int S = nipamd::estep_wide_slab(P.N, R);
+  hipStream_t st = (hipStream_t)stream;
+  if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 0.0, 1.0, st))
+    return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
+  if (int rc = zero_tail(mm, d_partial, S, st)) return rc;
+  if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
+  // sequences per launch: a power of two (the chunk trees are subtrees of the
+  // batch's tree), scratch within ~8 GB: config 3's 65,536 x 256 in one launch
+  const size_t per_seq = nipamd::estep_mw_scratch_bytes(32, T) / 32 + 1;
+  const size_t cap = std::min<size_t>(65536, std::max<size_t>(32, ((size_t)8 << 30) / per_seq));
+  long chunk = 32;
+  while ((size_t)chunk * 2 <= cap) chunk *= 2;
+  if (B < chunk) chunk = B;
+  const long nchunks = (B + chunk - 1) / chunk;
+  const long srows = (chunk + 15) / 16;
+  const long lvl = (srows + 63) / 64;
+  const size_t work = ((size_t)srows + 2 * lvl + nchunks + 64) * S * sizeof(double);
+  if (int rc = ensure_scratch(mm, nipamd::estep_mw_scratch_bytes(chunk, T))) return rc;
+  if (int rc = ensure_work(mm, work)) return rc;
+  DevState* d = dev_of(mm);
+  double* slab = d->W;
+  double* tA = slab + (size_t)srows * S;
+  double* tB = tA + (size_t)lvl * S;
+  double* cres = tB + (size_t)lvl * S;
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  nipamd::EMwArgs a{};
+  a.obs_bstride = (long)T * ocols;
+  a.obs_tstride = (int)ocols;
+  a.ncol = r.ncol;
+  for (int i = 0, v = 0; i < 4; i++) {
+    a.col[i] = i < r.ncol ? r.col[i] : 0;
+    a.M[i] = i < r.ncol ? P.emit(r.emit[i]).M : 0;
+    a.tab_off[i] = rt->mtab_off[i];
+    a.voff[i] = v;
+    v += a.M[i];
+  }
+  for (int k = 0, row = 0; k < (int)P.emits.size(); k++) {
+    for (int i = 0; i < r.ncol; i++)
+      if (r.emit[i] == k) a.crow[i] = row;
+    if (!seen[k]) {
+      a.urow[a.n_unobs] = row;
+      a.uM[a.n_unobs++] = P.emits[k].M;
+    }
+    row += P.emits[k].M + 2;
+  }
+  a.tab_rows = rt->mtab_rows; a.tab = rt->mtab;
+  a.T = T; a.H = T / 2; a.N = P.N;
+  a.A = d->A64; a.pi = d->pi64; a.w = rt->wv; a.S = d->S;
+  a.slab = slab; a.slab_size = S; a.R = R;
+  for (long c = 0; c < nchunks; c++) {
+    const long b0 = c * chunk;
+    const long nb = (B - b0) < chunk ? (B - b0) : chunk;
+    a.obs = d_obs ? d_obs + b0 * T * ocols : nullptr;
+    a.B = nb;
+    a.ll = d_ll ? d_ll + b0 : nullptr;
+    a.status = d_status ? d_status + b0 : nullptr;
+    const int lrc = nipamd::estep_mw_launch(a, st);
+    if (lrc == -2) return fail(NIPAMD_ERROR_UNSUPPORTED, "matrix-core e_step: the request does not fit the kernel");
+    if (lrc) return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
+    if (reduce_rows(slab, (nb + 15) / 16, S, tA, tB, out, st))
+      return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
+  }
+  if (nchunks > 1 && reduce_rows(cres, nchunks, S, tA, tB, d_partial, st))
+    return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
+  return 0;
+}
+
 static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d_obs, int n_obs, int B, int T,
                               double* d_partial, double* d_ll, uint32_t* d_status, void* stream) {
   const auto& P = mm->m.chain;
+  {
+    bool taken = false;
+    const int rc = estep_mw_partial(mm, r, d_obs, n_obs, B, T, d_partial, d_ll, d_status, stream, taken);
+    if (rc || taken) return rc;
+  }
   const int R = estep_rows(P);
   const int S = nipamd::estep_wide_slab(P.N, R);
   hipStream_t st = (hipStream_t)stream;

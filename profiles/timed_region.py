@@ -21,6 +21,10 @@ import os
 import sys
 
 
+# bench labels (nipamd_last_kernel) whose kernel symbol differs
+ALIAS = {"chain_row64_kernel": "chain_wide4_kernel"}
+
+
 def trace_rows(d):
     f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))
     if not f:
@@ -58,6 +62,7 @@ def main():
         line = bench_line(d)
         rows = trace_rows(d)
         dom = line["roofline"]["kernel"].split(" + ")[0].split("<")[0].split(" (")[0]
+        dom = ALIAS.get(dom, dom)
         steps, warm = int(line["steps"]), int(line["warmup"])
         # the dominant kernel's launches: per step = (total - the 2 launches of
         # the fb line's PCIe-inclusive calls, when present) / (warmup + steps)

@@ -27,6 +27,13 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CNT_RTOL = 1e-11
 LL_RTOL = 1e-12
 WIDE = "chain_msgs_kernel + chain_stats_kernel"
+FUSED = "chain_estep_mw_kernel"         # estep_mw.hip: 17..32 states, up to two observed children
+
+
+def expected_kernel(m, ov, N):
+    """The route the engine takes: the fused matrix-core e_step for 17..32
+    states with at most two observed children, the two-kernel one otherwise."""
+    return FUSED if 16 < N <= 32 and len(ov) <= 2 else WIDE
 
 
 def close(a, b, rtol):
@@ -41,20 +48,20 @@ def gpu_estep(model, obs, obs_vars):
 
 
 CASES = [
-    # name, spec, observed children
-    ("demo1_32_AB", lambda: synth.demo1_spec(32), ["A1", "B1"]),
-    ("demo1_20_A", lambda: synth.demo1_spec(20, seed=2), ["A1"]),
-    ("demo1_32_none", lambda: synth.demo1_spec(32, seed=4), []),
-    ("hmm_32", lambda: synth.hmm_spec(32, 20, seed=6), ["M1"]),
-    ("hmm_64", lambda: synth.hmm_spec(64, 16, seed=7), ["M1"]),
-    ("wide_24", lambda: synth.wide_spec(24, 5), ["O1"]),
-    ("wide_18", lambda: synth.wide_spec(18, 6, seed=8), ["O1"]),
+    # name, spec, observed children, interface variable
+    ("demo1_32_AB", lambda: synth.demo1_spec(32), ["A1", "B1"], "C1"),
+    ("demo1_20_A", lambda: synth.demo1_spec(20, seed=2), ["A1"], "C1"),
+    ("demo1_32_none", lambda: synth.demo1_spec(32, seed=4), [], "C1"),
+    ("hmm_32", lambda: synth.hmm_spec(32, 20, seed=6), ["M1"], "P1"),
+    ("hmm_64", lambda: synth.hmm_spec(64, 16, seed=7), ["M1"], "P1"),
+    ("wide_24", lambda: synth.wide_spec(24, 5), ["O1"], "X1"),
+    ("wide_18", lambda: synth.wide_spec(18, 6, seed=8), ["O1"], "X1"),
 ]
 
 
-@pytest.mark.parametrize("name,spec,osyms", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("name,spec,osyms,iface", CASES, ids=[c[0] for c in CASES])
 @pytest.mark.parametrize("B,T", [(37, 41), (16, 1), (3, 2), (70, 33)])
-def test_wide_estep_vs_oracle_and_general_engine(name, spec, osyms, B, T):
+def test_wide_estep_vs_oracle_and_general_engine(name, spec, osyms, iface, B, T):
     m = nip_amd.Model.from_spec(*spec())
     ov = [m.variable(s) for s in osyms]
     rng = np.random.default_rng(B * 31 + T + len(name))
@@ -65,7 +72,7 @@ def test_wide_estep_vs_oracle_and_general_engine(name, spec, osyms, B, T):
     else:
         obs = np.zeros((B, T, 0), np.int32)
     cnt, ll, st = gpu_estep(m, obs, ov)
-    assert nip_amd.last_kernel() == WIDE, nip_amd.last_kernel()
+    assert nip_amd.last_kernel() == expected_kernel(m, ov, m.card(m.variable(iface))), nip_amd.last_kernel()
     orc = PortOracle(m.desc())
     rc, rl, rb = orc.estep(obs, ov, np.ones(m.param_size()))
     assert np.array_equal(st != 0, rb != 0)
@@ -107,7 +114,7 @@ def test_wide_partial_is_shard_invariant_and_reproducible():
                                           axis=2)).cuda().contiguous()
     whole, _, _ = nip_amd.estep_partial(m, obs, ov)
     whole = whole.clone()
-    assert nip_amd.last_kernel() == WIDE
+    assert nip_amd.last_kernel() == FUSED
     again, _, _ = nip_amd.estep_partial(m, obs, ov)
     assert torch.equal(whole, again)
     parts = []
@@ -170,7 +177,7 @@ def test_em_learn_demo1_32_on_chain_kernels_matches_general_engine():
         rc = em_learn(m, torch.from_numpy(obs_np).cuda(), ov, 1e-6, curve,
                       init=synth.uniform01(5, m.param_size()) + 0.05, max_iterations=5)
         if engine == nip_amd.ENGINE_AUTO:
-            assert nip_amd.last_kernel() == WIDE
+            assert nip_amd.last_kernel() == FUSED
         curves.append((rc, curve))
     assert curves[0][0] == curves[1][0]
     assert len(curves[0][1]) == len(curves[1][1])
@@ -189,3 +196,51 @@ def test_em_learn_config5_model_on_chain_kernels_vs_oracle():
     rc = em_learn(m, torch.from_numpy(obs_np).cuda(), ov, 1e-9, curve, init=init, max_iterations=2)
     assert nip_amd.last_kernel() == WIDE
     assert len(curve) == 2 and np.all(np.isfinite(curve))
+
+
+def test_config3_estep_full_size_sums_vs_textbook():
+    """Config 3's e_step at its full size (demo1 @ 32 states, A1 and B1
+    observed, 65,536 x 256, the bench's inputs) on the fused matrix-core
+    kernel: the partial's three sums -- K (the in-clique's xi sums without the
+    transition), both children's count tables H and P0, each summed over all
+    sequences by the kernel's fixed-order trees -- element by element against
+    a textbook e_step in torch fp64 on the same GPU (tests/textbook_util.py
+    chain_sums_torch: per-step normalised family marginals, nip.c:1925-1967),
+    every sequence's ll, and the counts against the general formula of the
+    finalize (the projection is checked against the oracle by the cases
+    above).  Counts rel 1e-11, ll rel 1e-11 (32-state configs)."""
+    from textbook_util import chain_tables, clique_vars, chain_sums_torch
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(32))
+    ov = [m.variable("A1"), m.variable("B1")]
+    B, T = 65536, 256
+    obs_np = np.concatenate([synth.observations(B, T, 32, seed=1 + 104729 * i) for i in range(2)], axis=2)
+    obs = torch.from_numpy(obs_np).cuda()
+    partial, ll, st = nip_amd.estep_partial(m, obs, ov)
+    torch.cuda.synchronize()
+    assert nip_amd.last_kernel() == FUSED
+    assert not bool(st.any())
+    # the slab's children in the chain plan's order: by their {C1, child} clique
+    c1 = m.variable("C1")
+    nc = nip_amd.lib().nipamd_model_num_cliques(m._h)
+    order = sorted(ov, key=lambda v: next(c for c in range(nc) if set(clique_vars(m, c)) == {c1, v}))
+    A, pi, Es = chain_tables(m, m.variable("C0"), c1, order)
+    tA, tpi = torch.from_numpy(A).cuda(), torch.from_numpy(pi).cuda()
+    tEs = [torch.from_numpy(E).cuda() for E in Es]
+    N = 32
+    K = torch.zeros((N, N), dtype=torch.float64, device="cuda")
+    Hs = [torch.zeros((E.shape[1] + 2, N), dtype=torch.float64, device="cuda") for E in Es]
+    P0 = torch.zeros(N, dtype=torch.float64, device="cuda")
+    lls = []
+    for b0 in range(0, B, 8192):
+        cols = [obs[b0:b0 + 8192, :, ov.index(v)].long() for v in order]
+        k, h, p, l = chain_sums_torch(tA, tpi, tEs, cols)
+        K += k
+        for i in range(len(Hs)):
+            Hs[i] += h[i]
+        P0 += p
+        lls.append(l)
+    ref = torch.cat([K.reshape(-1)] + [h.reshape(-1) for h in Hs] + [P0]).cpu().numpy()
+    got = partial[:ref.size].cpu().numpy()
+    assert close(got, ref, CNT_RTOL), np.abs(got - ref).max()
+    lr = torch.cat(lls).cpu().numpy()
+    assert close(ll.cpu().numpy(), lr, 1e-11), np.abs(ll.cpu().numpy() - lr).max()

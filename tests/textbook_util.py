@@ -189,3 +189,56 @@ def hmm_estep_torch(A, pi, E, obs):
             g0 = pi[None, :] * (w @ A.T)
             c0 += (g0 / g0.sum(dim=1, keepdim=True)).sum(dim=0)
     return torch.cat([c0, c1.reshape(-1), c2.reshape(-1)]), ll
+
+
+def chain_sums_torch(A, pi, Es, cols):
+    """The wide chain e_step's three sums (estep_wide.hip / estep_mw.hip, DESIGN.md
+    4) over B sequences of an interface chain with children Es (cols: one [B, T]
+    long tensor per child, -1 missing; every child observed):
+      K [N, N]   = sum_t alpha_{t-1}(x) e_t(y) beta_t(y) / Z   (alpha_{-1} = prior)
+      H_k [M_k + 2, N] = sum_t [row of child k's code at t] gamma_t(y)
+                   (rows: the states, then missing, then out of range)
+      P0 [N]     = gamma_{-1} = prior o beta_{-1} / Z,
+    and the per-sequence ll -- each step normalised on its own, as the
+    reference's family marginals are (nip.c:1925-1967); sums in torch's order."""
+    import torch
+    B, T = cols[0].shape
+    N = A.shape[0]
+    dev, dt = A.device, A.dtype
+    s_list = [E.sum(dim=1) for E in Es]
+    s_all = torch.ones(N, dtype=dt, device=dev)
+    for s in s_list:
+        s_all = s_all * s
+    ah = torch.empty((B, T, N), dtype=dt, device=dev)
+    ll = torch.zeros(B, dtype=dt, device=dev)
+    prev = pi[None, :].expand(B, N)
+    for t in range(T):
+        u = prev @ A
+        al = u * _ev_torch(Es, s_list, cols, t)
+        c = al.sum(dim=1)
+        ll += torch.log(c) - torch.log((u * s_all).sum(dim=1))
+        prev = al / c[:, None]
+        ah[:, t] = prev
+    K = torch.zeros((N, N), dtype=dt, device=dev)
+    Hs = [torch.zeros((E.shape[1] + 2, N), dtype=dt, device=dev) for E in Es]
+    P0 = torch.zeros(N, dtype=dt, device=dev)
+    b = torch.ones((B, N), dtype=dt, device=dev)
+    for t in range(T - 1, -1, -1):
+        if t < T - 1:
+            b = (_ev_torch(Es, s_list, cols, t + 1) * b) @ A.T
+            b = b / b.sum(dim=1, keepdim=True)
+        w = _ev_torch(Es, s_list, cols, t) * b
+        pv = ah[:, t - 1] if t > 0 else pi[None, :].expand(B, N)
+        n = ((pv @ A) * w).sum(dim=1)
+        K += (pv / n[:, None]).T @ w
+        g = ah[:, t] * b
+        g = g / g.sum(dim=1, keepdim=True)
+        for H, E, c in zip(Hs, Es, cols):
+            M = E.shape[1]
+            r = c[:, t]
+            r = torch.where(r < 0, torch.full_like(r, M), torch.where(r >= M, torch.full_like(r, M + 1), r))
+            H.index_add_(0, r, g)
+        if t == 0:
+            g0 = pi[None, :] * (w @ A.T)
+            P0 += (g0 / g0.sum(dim=1, keepdim=True)).sum(dim=0)
+    return K, Hs, P0, ll
