@@ -327,6 +327,8 @@ int chain_estep_launch(const ChainArgs& a, hipStream_t stream);
 // its scratch holds the messages plus one exponent per (sequence, step)
 int chain_estep16_launch(const ChainArgs& a, hipStream_t stream);
 size_t chain_estep16_lds_bytes(int M, int T, int ne);
+// sequences per slab row of chain_estep16_kernel (one row per block: 16, or 8 / 24)
+int chain_estep16_seqs_per_row(int M, int T, int ne);
 size_t chain_estep16_scratch_bytes(long B, int T);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);

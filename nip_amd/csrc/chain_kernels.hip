@@ -541,7 +541,8 @@ __device__ __forceinline__ int row_max_exp_rescale(double p) {
 // rescale by the row's largest exponent, and the backward rows sum no m1.
 template <bool FWD, int KC, int NE, int PRM>
 __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* Et, const uint8_t* codes,
-                                             double* Htab, double* m1x, int lane, int grp, long b0, int nseqb) {
+                                             double* Htab, double* m1x, double* kdl, double* p0l, int lane, int grp,
+                                             long b0, int nseqb) {
   constexpr bool PR = PRM != 0;                     // proper mode
   constexpr bool SP = PRM == 2;                     // and the forward rows may rescale every 4th step
   const int y = lane & 15, row = lane >> 4;
@@ -756,7 +757,6 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     d[1] = st[2] - st[1];                            // phase barrier wait
     d[2] = st[3] - st[2];                            // phase B
   }
-  double* slab = a.counts + (size_t)(active ? b : 0) * chain_estep_slab(M);
   if (!FWD && H > 0 && !PR) {
     // the phase-A m1 part for the forward rows: step 0's from the prior, then
     // mantissa and exponent through LDS
@@ -778,26 +778,12 @@ __device__ __forceinline__ void estep16_rows(const ChainArgs& a, const double* E
     const double rc = c != 0.0 ? __builtin_ldexp(div_by(1.0, c), sc) : 0.0;
     const double w = H > 0 ? pi_y * rc : 0.0;
     Kd = __builtin_amdgcn_mfma_f64_16x16x4f64(w, x, Kd, 0, 0, 0);
-    if (active) slab[chain_slab_p0(M) + y] = q;
+    p0l[seq * 16 + y] = active ? q : 0.0;
   }
-  // the wave's xi sum goes to its first sequence's slab row, zeros to the
-  // other three (the batch tree sums rows; shards are whole 16-sequence blocks)
-  {
-    const int ko = FWD ? kSlabKf : kSlabKb;
-    const long lead = b0 + grp * 4;                  // the group's first sequence
-    if (lead < a.B) {
-      double* const g = a.counts + (size_t)lead * chain_estep_slab(M) + ko;
+  // the wave's xi sum (over its four sequences) to LDS: the block sums its
+  // waves' and writes one slab row (chain_estep16_kernel)
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = (lane >> 4) + 4 * r;           // D row: the previous state x
-        g[i * 16 + y] = Kd[r];                       // lane (row', y): element (x, y)
-      }
-    }
-    if (active && row != 0) {
-#pragma unroll
-      for (int k = 0; k < 16; k++) slab[ko + k * 16 + y] = 0.0;
-    }
-  }
+  for (int r = 0; r < 4; r++) kdl[(size_t)((FWD ? 0 : nseqb / 4) + grp) * 256 + r * 64 + lane] = Kd[r];
   // proper model: ll = log P(obs) = log(sum alpha^_{T-1}) - Ef_{T-1} ln 2
   // (the forward rows end phase B at t = T - 1: x = alpha^_{T-1}, ex its
   // exponent); m1_t = the previous mass, so the reference's per-step
@@ -884,14 +870,36 @@ void chain_estep16_kernel(ChainArgs a) {
   }
   __syncthreads();
   double* m1x = Htab + kE16Seqs * 2 * R * 16;                           // [NSEQ][4]
+  double* kdl = m1x + kE16Seqs * 4;                                     // [NSEQ / 4 * 2 waves][4][64]
+  double* p0l = kdl + (kE16Seqs / 4) * 2 * 256;                         // [NSEQ][16]
   // A/B builds: static wave priority for the backward (1) or the forward (2) rows
   if ((NIPAMD_ESTEP_PRIO == 1 && wave >= G) || (NIPAMD_ESTEP_PRIO == 2 && wave < G)) __builtin_amdgcn_s_setprio(1);
-  if (wave < G) estep16_rows<true, KC, NE, PR>(a, Et, codes, Htab, m1x, lane, wave, b0, kE16Seqs);
-  else estep16_rows<false, KC, NE, PR>(a, Et, codes, Htab, m1x, lane, wave - G, b0, kE16Seqs);
+  if (wave < G) estep16_rows<true, KC, NE, PR>(a, Et, codes, Htab, m1x, kdl, p0l, lane, wave, b0, kE16Seqs);
+  else estep16_rows<false, KC, NE, PR>(a, Et, codes, Htab, m1x, kdl, p0l, lane, wave - G, b0, kE16Seqs);
   __syncthreads();
-  for (int i = tid; i < kE16Seqs * 2 * R * 16; i += kE16Threads) {
-    const int sq = i / (2 * R * 16), r = i - sq * 2 * R * 16;
-    if (b0 + sq < a.B) a.counts[(size_t)(b0 + sq) * chain_estep_slab(a.M) + kSlabH + r] = Htab[i];
+  // the block's slab row (chain_estep_slab layout): the block's sums in a
+  // fixed order -- Kf / Kb over the direction's waves (D[i][y]: lane
+  // (i % 4) * 16 + y, register i / 4), every sequence's count tables and P0
+  // in sequence order.  One row per NSEQ sequences instead of one per
+  // sequence: 1/NSEQ of the slab bytes written and read back by the tree.
+  double* slab = a.counts + (size_t)blockIdx.x * chain_estep_slab(a.M);
+  for (int e = tid; e < 512; e += kE16Threads) {
+    const int dir = e >> 8, i = (e >> 4) & 15, y = e & 15;
+    const int off = (i >> 2) * 64 + (i & 3) * 16 + y;
+    double v = 0.0;
+#pragma unroll
+    for (int g = 0; g < G; g++) v += kdl[(size_t)(dir * G + g) * 256 + off];
+    slab[e] = v;                                                        // kSlabKf = 0, kSlabKb = 256
+  }
+  for (int e = tid; e < 2 * R * 16; e += kE16Threads) {
+    double v = 0.0;
+    for (int sq = 0; sq < kE16Seqs; sq++) v += Htab[(size_t)sq * 2 * R * 16 + e];
+    slab[kSlabH + e] = v;
+  }
+  for (int y = tid; y < 16; y += kE16Threads) {
+    double v = 0.0;
+    for (int sq = 0; sq < kE16Seqs; sq++) v += p0l[sq * 16 + y];
+    slab[chain_slab_p0(a.M) + y] = v;
   }
   if (NIPAMD_WAIT_TIMES && a.diag && lane == 0) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -910,7 +918,10 @@ static int estep16_seqs() {
 
 static size_t estep16_lds(int nseq, int M, int T, int ne) {
   const size_t n = (size_t)(M + 2) * 16 * sizeof(double) + (size_t)ne * nseq * chain_codes_row(T);
-  return ((n + 15) & ~(size_t)15) + (size_t)nseq * 2 * (M + 2) * 16 * sizeof(double) + (size_t)nseq * 4 * sizeof(double);
+  return ((n + 15) & ~(size_t)15) + (size_t)nseq * 2 * (M + 2) * 16 * sizeof(double) +
+         (size_t)nseq * 4 * sizeof(double) +                           // m1x
+         (size_t)(nseq / 4) * 2 * 256 * sizeof(double) +               // the waves' xi sums
+         (size_t)nseq * 16 * sizeof(double);                           // P0 per sequence
 }
 
 // sequences per block: 16, or 8 when the children's count tables of 16 do not fit
@@ -920,6 +931,7 @@ static int estep16_nseq(int M, int T, int ne) {
 }
 
 size_t chain_estep16_lds_bytes(int M, int T, int ne) { return estep16_lds(estep16_nseq(M, T, ne), M, T, ne); }
+int chain_estep16_seqs_per_row(int M, int T, int ne) { return estep16_nseq(M, T, ne); }
 
 size_t chain_estep16_scratch_bytes(long B, int T) {
   const long nrow = (B + kE16RowMul - 1) / kE16RowMul * kE16RowMul;

@@ -57,6 +57,7 @@ struct ReqTables {
   int mtab_rows = 0;
   int mtab_off[4] = {0, 0, 0, 0};
   double* wv = nullptr;           // [64] A s_all
+  double* arena = nullptr;        // the pool buffer all of the above live in (one upload)
 };
 
 struct DevState {
@@ -67,6 +68,7 @@ struct DevState {
   double* A64 = nullptr;          // [64][64]
   double* pi64 = nullptr;         // [64]
   double* sall64 = nullptr;       // [64]
+  double* arena = nullptr;        // the pool buffer A .. sall64 and childE live in (one upload)
   std::deque<ReqTables> reqs;      // deque: pointers returned by ensure_req_tables stay valid
   double* S = nullptr;
   size_t S_bytes = 0;
@@ -128,15 +130,10 @@ void free_tables(DevState* d) {
   // queued kernels may still read the tables: they return to the pool only
   // once the device is idle (hipFree synchronised the same way)
   if (!d->live.empty()) (void)hipDeviceSynchronize();
-  dfree(d, d->A); dfree(d, d->pi); dfree(d, d->A64); dfree(d, d->pi64);
-  dfree(d, d->sall64);
-  d->A = d->pi = d->A64 = d->pi64 = d->sall64 = nullptr;
-  for (auto& r : d->reqs) {
-    dfree(d, r.Etab16); dfree(d, r.ts16); dfree(d, r.tabw); dfree(d, r.ebase);
-    dfree(d, r.mtab); dfree(d, r.wv);
-  }
+  dfree(d, d->arena);
+  d->A = d->pi = d->A64 = d->pi64 = d->sall64 = d->arena = nullptr;
+  for (auto& r : d->reqs) dfree(d, r.arena);
   d->reqs.clear();
-  for (double* p : d->childE) dfree(d, p);
   for (double* p : d->G) dfree(d, p);
   d->childE.clear();
   d->G.clear();
@@ -155,11 +152,35 @@ void dev_release(DevState* d) {
   *d = DevState();
 }
 
+// Several tables in one pool buffer with one host-to-device copy: every
+// em_learn iteration re-uploads the model's tables after its m_step, and a
+// synchronous copy per table kept the device idle for ~0.2 ms per iteration
+// (profiles/r05/em_phases.py).  Each table starts on a 64-byte boundary.
+struct Staged {
+  std::vector<double> host;
+  std::vector<std::pair<double**, size_t>> dst;
+  template <typename V>
+  void add(double** p, const V& v) {
+    dst.push_back({p, host.size()});
+    host.insert(host.end(), v.begin(), v.end());
+    host.resize((host.size() + 8) & ~(size_t)7, 0.0);     // >= 1 double, 64-byte aligned
+  }
+  int commit(DevState* d, double** arena);
+};
+
 template <typename V>
 int upload(DevState* d, double** dst, const V& v) {
   *dst = static_cast<double*>(dalloc(d, (v.size() ? v.size() : 1) * sizeof(double)));
   if (!*dst) return fail(NIPAMD_ERROR_DEVICE, "device allocation failed");
   if (v.size()) HIP_OK(hipMemcpy(*dst, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int Staged::commit(DevState* d, double** arena) {
+  *arena = static_cast<double*>(dalloc(d, host.size() * sizeof(double)));
+  if (!*arena) return fail(NIPAMD_ERROR_DEVICE, "device allocation failed");
+  HIP_OK(hipMemcpy(*arena, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice));
+  for (auto& e : dst) *e.first = *arena + e.second;
   return 0;
 }
 
@@ -204,20 +225,21 @@ int ensure_tables(nipamd_model* mm) {
   if (int rc = nipamd::ensure_fold(mm)) return rc;
   const auto& P = mm->m.chain;
   free_tables(d);
+  Staged sg;
   if (P.N <= 16) {
-    if (int rc = upload(d, &d->A, P.A)) return rc;
-    if (int rc = upload(d, &d->pi, P.pi)) return rc;
+    sg.add(&d->A, P.A);
+    sg.add(&d->pi, P.pi);
   }
-  if (int rc = upload(d, &d->A64, P.A64)) return rc;
-  if (int rc = upload(d, &d->pi64, P.pi64)) return rc;
-  if (int rc = upload(d, &d->sall64, P.s_all64)) return rc;
-  for (const auto& E : P.emits) {
-    std::vector<double> t(E.E);
-    t.insert(t.end(), E.s.begin(), E.s.end());
-    double* p = nullptr;
-    if (int rc = upload(d, &p, t)) return rc;
-    d->childE.push_back(p);
+  sg.add(&d->A64, P.A64);
+  sg.add(&d->pi64, P.pi64);
+  sg.add(&d->sall64, P.s_all64);
+  d->childE.assign(P.emits.size(), nullptr);
+  for (size_t k = 0; k < P.emits.size(); k++) {
+    std::vector<double> t(P.emits[k].E);
+    t.insert(t.end(), P.emits[k].s.begin(), P.emits[k].s.end());
+    sg.add(&d->childE[k], t);
   }
+  if (int rc = sg.commit(d, &d->arena)) return rc;
   d->G.assign(P.hidden.size(), nullptr);
   d->version = mm->version;
   return 0;
@@ -259,6 +281,7 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
   for (auto& t : d->reqs) if (t.key == key) { *out = &t; return 0; }
   ReqTables t;
   t.key = key;
+  Staged sg;                                 // every table of the request, one upload
   const int N = P.N;
   if (N <= 16) {
     // narrow: the primary child's table times the other children's row sums
@@ -281,8 +304,8 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
       ts[x] = acc;
     }
     t.M0 = M;
-    if (int rc = upload(d, &t.Etab16, E)) return rc;
-    if (int rc = upload(d, &t.ts16, ts)) return rc;
+    sg.add(&t.Etab16, E);
+    sg.add(&t.ts16, ts);
   }
   // wide: one unscaled table per observed child, the unobserved ones in ebase
   std::vector<double> W;
@@ -306,8 +329,8 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
     }
     eb[y] = v;
   }
-  if (int rc = upload(d, &t.tabw, W)) return rc;
-  if (int rc = upload(d, &t.ebase, eb)) return rc;
+  sg.add(&t.tabw, W);
+  sg.add(&t.ebase, eb);
   if (N <= 32) {
     const int NP = N <= 16 ? 16 : 32;
     std::vector<double> MT;
@@ -335,9 +358,10 @@ int ensure_req_tables(nipamd_model* mm, const Route& r, ReqTables** out) {
       for (int y = 0; y < N; y++) acc += P.A64[(size_t)x * 64 + y] * P.s_all64[y];
       wv[x] = acc;
     }
-    if (int rc = upload(d, &t.mtab, MT)) return rc;
-    if (int rc = upload(d, &t.wv, wv)) return rc;
+    sg.add(&t.mtab, MT);
+    sg.add(&t.wv, wv);
   }
+  if (int rc = sg.commit(d, &t.arena)) return rc;
   d->reqs.push_back(std::move(t));
   *out = &d->reqs.back();
   return 0;
@@ -1704,7 +1728,9 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   const int S = nipamd::chain_estep_slab(Mo);
   const int ek = chain_estep_kernel(mm, T);
   const bool mfma = ek == 1;
-  const int per_row = mfma ? 16 : 1;            // sequences per slab row
+  // sequences per slab row: the matrix-core kernel's and chain_estep16_kernel's
+  // blocks (one row each), the round-2 DPP kernel's sequences
+  const int per_row = mfma ? 16 : ek == 3 ? nipamd::chain_estep16_seqs_per_row(Mo, T, general ? (int)P.emits.size() : 1) : 1;
   hipStream_t st = (hipStream_t)stream;
   if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, 0.0, st))
     return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
