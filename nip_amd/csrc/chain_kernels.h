@@ -335,7 +335,9 @@ int estep_finalize_launch(const double* R, const ChainFinalize& f, double* count
 // the e_step partial's route tag: tag[0] = a, tag[1] = b, tag[2] = c
 int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stream);
 // BAD_LUCK for sequences missing every observation at steps 0..first_bad (prefix.cpp)
-int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, uint32_t* status,
+// trivial: bit c set when column c observes a one-state variable (no evidence)
+int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, unsigned trivial,
+                             uint32_t* status,
                              hipStream_t stream);
 // counts[p] += sum_j coef[j] * R[idx[j]] over j in [ptr[p], ptr[p + 1]) (a
 // linear map of the reduced slab, e.g. a joint interface's counts projected

@@ -1074,23 +1074,30 @@ int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stre
 // whose observations at steps 0..first_bad are all missing (< 0) gets
 // BAD_LUCK.  One thread per sequence; almost every sequence leaves at its
 // first step, so the launch reads a few bytes per sequence.
+// A series whose steps 0..first_bad carry no evidence: every column missing,
+// or (bit c of `trivial`) an observation of a one-state variable, whose
+// indicator multiplies every table by 1.0 -- the reference's propagation
+// over such a step is bit for bit the missing step's (nip_update_evidence,
+// nippotential.c:499-522, divides by the likelihood 1 as well)
 __global__ void estep_prefix_flag_kernel(const int32_t* obs, long bstride, int n_obs, int B, int first_bad,
-                                         uint32_t* status) {
+                                         unsigned trivial, uint32_t* status) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int32_t* o = obs + (long)b * bstride;
   for (int t = 0; t <= first_bad; t++)
-    for (int c = 0; c < n_obs; c++)
-      if (o[(long)t * n_obs + c] >= 0) return;
+    for (int c = 0; c < n_obs; c++) {
+      const int32_t v = o[(long)t * n_obs + c];
+      if (v >= 0 && !(v == 0 && ((trivial >> c) & 1u))) return;
+    }
   status[b] |= 2u;                                   // NIPAMD_STATUS_BAD_LUCK
 }
 
-int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, uint32_t* status,
-                             hipStream_t stream) {
+int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, unsigned trivial,
+                             uint32_t* status, hipStream_t stream) {
   if (B <= 0) return 0;
   if (first_bad < 0 || first_bad >= T || (n_obs > 0 && !obs)) return -1;
   hipLaunchKernelGGL(estep_prefix_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, obs,
-                     (long)T * n_obs, n_obs, B, first_bad, status);
+                     (long)T * n_obs, n_obs, B, first_bad, trivial, status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1471,7 +1471,11 @@ static int estep_partial_cap(nipamd_model* mm, const int32_t* d_obs, int n_obs, 
   // the kernels are queued: this host work overlaps them
   const int k = prefix_first_bad(mm, T);
   if (k < 0) return 0;
-  if (nipamd::estep_prefix_flag_launch(d_obs, n_obs, B, T, k, d_status, (hipStream_t)stream))
+  unsigned trivial = 0;                          // columns observing a one-state variable
+  for (int c = 0; c < n_obs && c < 32; c++)
+    if (obs_vars[c] >= 0 && obs_vars[c] < (int)mm->m.vars.size() && mm->m.vars[obs_vars[c]].card == 1)
+      trivial |= 1u << c;
+  if (nipamd::estep_prefix_flag_launch(d_obs, n_obs, B, T, k, trivial, d_status, (hipStream_t)stream))
     return fail(NIPAMD_ERROR_DEVICE, "prefix flag launch failed");
   return 0;
 }

@@ -396,3 +396,95 @@ def test_general_chain_em_learn_matches_general_engine():
     assert curves[0][0] == curves[1][0]
     assert len(curves[0][1]) == len(curves[1][1])
     assert close(np.array(curves[0][1]), np.array(curves[1][1]), 1e-10)
+
+
+# ---------------------------------------------------------------------------
+# BAD_LUCK outside leading missing runs: the reference
+# rejects a series as soon as its running ll is > 0 (nip.c:1827-1829).  An
+# observed step adds log P(o_t | past) <= 0, so the test can only fire by
+# rounding while every step so far had probability 1 exactly -- deterministic
+# rows.  These models put the e_step there, in both kernel modes (proper: the
+# rows sum to 1, the ll from the final mass; general: per-step masses), and
+# compare every series' flag and ll with the reference's own code
+# (oracle/_ref).  Findings:
+#   * 0/1 and dyadic tables: the arithmetic is exact on both sides (ll 0, or
+#     log of the first observation's probability), so nothing is flagged by
+#     rounding and the flags agree;
+#   * a one-state child observed at every step carries no evidence: the
+#     reference's propagation is bit for bit the missing step's, so its
+#     rounding verdict is the leading-missing-run verdict (prefix.cpp), which
+#     the flag kernel applies to such columns too;
+#   * non-dyadic deterministic rows (probability 1 from inexact sums) put the
+#     running ll at +-1e-16 on the reference's side -- its verdict there is a
+#     rounding accident the kernels do not reproduce; the case below records
+#     the reference's outcome on it and checks the ll agree within 1e-15.
+def _det_spec(E, A, pi, proper):
+    """HMM-shaped slice M1 | P1, P1 | P0, P0 with the given tables (rows: parent
+    state); proper=True declares M1 first, so the reference's CPT
+    normalisation runs over the child (huginnet.y:635-636)."""
+    N, M = E.shape
+    nodes = [("P0", N, "P1"), ("P1", N, None), ("M1", M, None)]
+    if proper:
+        nodes = nodes[::-1]
+    pots = [("M1", ["P1"], np.asarray(E, np.float64).ravel()), ("P1", ["P0"], np.asarray(A, np.float64).ravel()),
+            ("P0", [], np.asarray(pi, np.float64))]
+    return nodes, pots
+
+
+def _det_cases():
+    T = 40
+    cyc = np.roll(np.eye(3), 1, axis=1)              # P1 = P0 + 1 mod 3
+    good = np.array([[(t + 1) % 3 for t in range(T)]] * 8, np.int32)
+    good[1, 5:12] = -1                                # a gap
+    good[2, :9] = -1                                  # a leading missing run
+    good[3, 17] = (good[3, 17] + 1) % 3               # an impossible step: zero mass
+    out = [("identity_onehot_proper", np.eye(3), cyc, [1.0, 0.0, 0.0], True, good)]
+    # 3 states, 2 symbols, states 0 and 1 emit symbol 0 (non-proper order: the
+    # emission normalised over P1, rows 0.5 / 0.5 / 1)
+    E2 = np.array([[1.0, 0.0], [1.0, 0.0], [0.0, 1.0]])
+    A2 = np.array([[0.5, 0.5, 0.0], [0.5, 0.5, 0.0], [0.0, 0.0, 1.0]])
+    obs2 = np.zeros((8, T), np.int32)
+    obs2[1, 3:9] = -1
+    obs2[2, :5] = -1
+    obs2[3, 11] = 1                                   # impossible: zero mass
+    out.append(("dyadic_nonproper", E2, A2, [0.25, 0.75, 0.0], False, obs2))
+    out.append(("dyadic_proper", E2, A2, [0.25, 0.75, 0.0], True, obs2))
+    # a one-state child: every observation is uninformative
+    E3 = np.ones((3, 1))
+    A3 = np.array([[0.1, 0.2, 0.7], [0.3, 0.3, 0.4], [0.5, 0.25, 0.25]])
+    obs3 = np.zeros((8, T), np.int32)
+    obs3[1, 4:10] = -1
+    obs3[2, :3] = -1
+    out.append(("one_state_child_proper", E3, A3, [0.2, 0.3, 0.5], True, obs3))
+    out.append(("one_state_child_nonproper", E3, A3, [0.2, 0.3, 0.5], False, obs3))
+    # non-dyadic transition and prior behind a deterministic emission: every
+    # observed step has probability 1 from inexact sums (the reference's ll
+    # ends at -1.1e-16 here, nothing flagged; a rounding accident either way)
+    A4 = np.array([[0.3, 0.7, 0.0], [0.6, 0.4, 0.0], [0.0, 0.0, 1.0]])
+    obs4 = np.zeros((8, T), np.int32)
+    obs4[1, 6:14] = -1
+    out.append(("deterministic_emission_nondyadic", E2, A4, [0.1, 0.9, 0.0], True, obs4))
+    return out
+
+
+@pytest.mark.parametrize("name,E,A,pi,proper,obs", _det_cases(), ids=[c[0] for c in _det_cases()])
+def test_bad_luck_on_deterministic_rows_vs_reference(name, E, A, pi, proper, obs):
+    from oracle import bind
+    if not bind.ref_available():
+        pytest.skip("oracle/_ref not built")
+    nodes, pots = _det_spec(E, A, pi, proper)
+    m = nip_amd.Model.from_spec(nodes, pots)
+    ov = [m.variable("M1")]
+    obs = obs[..., None]
+    cnt, ll, st = gpu_estep(m, obs, ov)
+    assert nip_amd.last_kernel().startswith("chain_estep16_kernel"), nip_amd.last_kernel()
+    ref = bind.RefHarness(synth.spec_to_replay(nodes, pots), cards=[n[1] for n in nodes])
+    rc, rl, rb = ref.estep(obs, [nodes.index(next(n for n in nodes if n[0] == "M1"))], np.ones(m.param_size()))
+    assert np.array_equal(st != 0, rb != 0), (st.tolist(), rb.tolist())
+    ok = rb == 0
+    assert np.all(np.abs(ll[ok] - rl[ok]) <= 1e-15 + 1e-12 * np.abs(rl[ok])), np.abs(ll[ok] - rl[ok]).max()
+    if ok.any():
+        c2, _, _ = gpu_estep(m, obs[ok], ov)
+        rc2, _, _ = ref.estep(obs[ok], [nodes.index(next(n for n in nodes if n[0] == "M1"))],
+                              np.ones(m.param_size()))
+        assert close(c2, rc2, CNT_RTOL), np.abs(c2 - rc2).max()
