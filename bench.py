@@ -130,8 +130,15 @@ WORKLOADS = {
     # D1 observed): the operator chain's e_step, and the general engine's
     "estep_opchain": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 5),
     "estep_opchain_jt": ("general", lambda a: synth.demo1_spec(6), ["A1", "B1", "D1"], "C1", 4096, 1024, 2),
+    # e_step of the opchain_wide request (demo1 @ 20 states, A1 B1 and the
+    # hidden parent D1 observed, 9261 evidence combinations): the wide operator
+    # chain's e_step (op_wide_msgs_kernel + op_wide_xi_kernel), and the general
+    # engine's on a smaller batch
+    "estep_opchain_wide": ("general", lambda a: synth.demo1_spec(20), ["A1", "B1", "D1"], "C1", 4096, 1024, 3),
+    "estep_opchain_wide_jt": ("general", lambda a: synth.demo1_spec(20), ["A1", "B1", "D1"], "C1", 256, 1024, 1),
 }
-ESTEP_WORKLOADS = ("estep", "estep_demo1", "estep_demo1_jt", "estep_config3", "estep_opchain", "estep_opchain_jt")
+ESTEP_WORKLOADS = ("estep", "estep_demo1", "estep_demo1_jt", "estep_config3", "estep_opchain", "estep_opchain_jt",
+                   "estep_opchain_wide", "estep_opchain_wide_jt")
 # the default line: the headline, then these under "secondary" 
 SECONDARY = ["config3", "em", "config5", "estep_config3"]
 
@@ -315,7 +322,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
     nodes, pots = spec(args)
     model = nip_amd.Model.from_spec(nodes, pots)
     ov, q = [model.variable(v) for v in ov_names], model.variable(q_name)
-    if name in ("jtree", "opchain_jt", "estep_demo1_jt", "estep_opchain_jt", "opchain_wide_jt"):
+    if name in ("jtree", "opchain_jt", "estep_demo1_jt", "estep_opchain_jt", "opchain_wide_jt", "estep_opchain_wide_jt"):
         model.set_engine(nip_amd.ENGINE_JTREE)     # the chain kernels would take it otherwise
     N, M = model.card(q), model.card(ov[0])
     obs_np = np.concatenate([synth.observations(B, T, model.card(v), seed=1 + 7919 * rank + 104729 * i)
@@ -470,6 +477,19 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         workload = ("e_step of demo1's structure, 6 states, A1 B1 and the hidden parent D1 observed, "
                     "B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
         metric = "sequence-timesteps/s batched e_step, demo1 with its hidden parent observed"
+    elif name in ("estep_opchain_wide", "estep_opchain_wide_jt"):
+        if kname.startswith("op_wide_msgs_kernel"):
+            NP = 32 if N <= 32 else 64
+            bpu = 2 * 4 * len(ov) + 4 * 8 * NP + 8
+            bnote = ("obs %d (read by the filters and op_wide_xi_kernel) + alpha^ and beta^ written and read back "
+                     "(4 x %d) + the forward scale exponent written and read 8; the xi sums are slab rows "
+                     "(one per 16 sequences), the operators L2 / MALL reads" % (2 * 4 * len(ov), 8 * NP))
+            kname += " + tree64 + map finalize"
+        else:
+            bpu, bnote = 4 * len(ov), "the request's input only: the engine is latency-bound (DESIGN.md 4)"
+        workload = ("e_step of demo1's structure, 20 states, A1 B1 and the hidden parent D1 observed (9261 "
+                    "evidence combinations), B=%d seq/GPU x T=%d (%s)" % (B, T, kname))
+        metric = "sequence-timesteps/s batched e_step, demo1 @ 20 with its hidden parent observed"
     elif name == "em":
         kname += " + tree64 + finalize"
         workload = ("config4: em_learn iterations of HMM-shaped DBN, %d hidden x %d observed, "

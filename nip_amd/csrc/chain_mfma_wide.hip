@@ -50,6 +50,9 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #ifndef NIPAMD_MW_SPARSE
 #define NIPAMD_MW_SPARSE 0     // timing-only builds: the filters rescale once per chunk (the ll is then wrong)
 #endif
+#ifndef NIPAMD_MW_ANALYTIC
+#define NIPAMD_MW_ANALYTIC 1   // smoothing: analytic posterior normalisation, the ll in the forward filter (0: A/B builds)
+#endif
 constexpr int kWSeq = 16;                  // sequences per group
 constexpr int kWGroups = 2;                // groups per block
 constexpr int kWThreads = 512;
@@ -172,6 +175,7 @@ struct Geo {
 };
 
 __host__ __device__ inline long wblock_scratch(int NT, int T) { return (long)(T + 2 * kWG) * kWSeq * 16 * NT; }
+__host__ __device__ inline long wblock_exps(int T) { return (long)(T + 2 * kWG) * kWSeq; }   // ints
 
 struct WCtx {
   const double* tab;       // LDS tables
@@ -183,19 +187,34 @@ struct WCtx {
   int ncol;
   double* out;             // this direction's ring [2][kSlot]
   double* zr;              // forward: z2 ring [2][CH][16]
+  int* er;                 // AN: this direction's exponent ring [2][CH][16]
   int wo[2][2];            // [tile][half] piece offsets of this lane
   bool zw;
+  int j;                   // this lane's chain
 };
 
 // NC: observed columns (1..4; 0 runs as 1, column 0 carrying the row sums),
 // a template parameter so that the per-step evidence gather is branch-free and
 // its LDS loads can be scheduled under the MFMAs
-template <bool FWD, int NT, int NC>
+// AN (smoothing, round 5): every step's accumulated exponent goes to the
+// exponent ring (alpha^_t = alpha_t 2^Ef_t, beta^_t = beta_t 2^Eb_t), so the
+// partners normalise the posteriors analytically (wpartner), and the forward
+// filter keeps the ll itself (nip.c:1458-1474: m2_t = z2_t, m1_{t+1} =
+// 2^sc_{t+1} alpha^_t . A s), off its recursion's dependency chain
+template <bool FWD, int NT, int NC, bool AN = false>
 struct WChain {
   using G = Geo<NT>;
   double Aop[NT][NT][4];
   v4d X[NT];
   int sc = 0;
+  int E = 0;                               // AN: the last message's accumulated exponent
+  double m2 = 1.0, m1 = 1.0, zmin = 1.0;   // AN, forward: ll mantissas (exponents apart)
+  int e2 = 0, e1 = 0;
+  v4d wv[NT];                              // AN, forward: this lane's states of w = A s_all
+  __device__ __forceinline__ void renorm() {
+    const int k2 = __builtin_amdgcn_frexp_exp(m2); m2 = __builtin_ldexp(m2, -k2); e2 += k2;
+    const int k1 = __builtin_amdgcn_frexp_exp(m1); m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+  }
 
   // column k's observation at t, raw (-1: missing, also outside 0..T-1)
   __device__ __forceinline__ int raw(const WCtx& c, int k, int t) const {
@@ -234,12 +253,13 @@ struct WChain {
   // one step with the evidence rows loaded at its start: the MFMAs first, the
   // evidence product after them (its LDS loads complete under the MFMAs)
   template <bool RS = true>
-  __device__ __forceinline__ void step_rows(const WCtx& c, double* L, double* Z, const v4d (&r)[NC][NT]) {
+  __device__ __forceinline__ void step_rows(const WCtx& c, double* L, double* Z, const v4d (&r)[NC][NT],
+                                            int* Ez = nullptr, bool last = false) {
     v4d d[NT];
     matvec(d);
     v4d e[NT];
     product(c, r, e);
-    finish<RS>(c, L, Z, d, e);
+    finish<RS>(c, L, Z, d, e, Ez, last);
   }
 
   __device__ __forceinline__ void step(const WCtx& c, double* L, double* Z, const v4d (&e)[NT]) {
@@ -272,8 +292,9 @@ struct WChain {
 
   template <bool RS = true>
   __device__ __forceinline__ void finish(const WCtx& c, double* L, double* Z, const v4d (&d)[NT],
-                                         const v4d (&e)[NT]) {
-    double part = 0.0;
+                                         const v4d (&e)[NT], int* Ez = nullptr, bool last = false) {
+    double part = 0.0, py = 0.0;
+    if (AN) E += sc;
 #pragma unroll
     for (int q = 0; q < NT; q++) {
       const v4d u = ldexp4(d[q], sc);
@@ -282,12 +303,24 @@ struct WChain {
       *reinterpret_cast<v2d*>(L + c.wo[q][0]) = v2d{keep.x, keep.y};
       *reinterpret_cast<v2d*>(L + c.wo[q][1]) = v2d{keep.z, keep.w};
       if (RS) part += (p.x + p.y) + (p.z + p.w);
+      if (AN && FWD) py += (p.x * wv[q].x + p.y * wv[q].y) + (p.z * wv[q].z + p.w * wv[q].w);
       X[q] = p;
     }
+    if (AN && c.zw) Ez[c.j] = E;
     if (!RS) { sc = 0; return; }
     const double z2 = swap16_sum(swap32_sum(part));
-    if (FWD && c.zw) *Z = z2;
-    sc = -__builtin_amdgcn_frexp_exp(z2);
+    const int k = __builtin_amdgcn_frexp_exp(z2);
+    if (AN && FWD) {
+      // m2_t = z2_t; m1_{t+1} = 2^sc_{t+1} y_t, y_t = alpha^_t . w
+      asm("" : "+v"(py));
+      const double y = swap16_sum(swap32_sum(py));
+      zmin = __builtin_fmin(zmin, z2);
+      m2 *= z2;
+      if (!last) { m1 *= y; e1 -= k; }
+      renorm();
+    }
+    if (!AN && FWD && c.zw) *Z = z2;
+    sc = -k;
   }
 
   // n steps from t0 in nch chunks; the codes of chunk ci + 2 are loaded from
@@ -305,7 +338,8 @@ struct WChain {
     };
     auto chunk = [&](int ci, int (&cc)[CH][NC]) {
       double* slot = c.out + (ci & 1) * G::kSlot;
-      double* zs = FWD ? c.zr + (ci & 1) * CH * kWSeq + (lane & 15) : nullptr;
+      double* zs = (FWD && !AN) ? c.zr + (ci & 1) * CH * kWSeq + (lane & 15) : nullptr;
+      int* es = AN ? c.er + (ci & 1) * CH * kWSeq : nullptr;
       const int base = ci * CH;
       const bool full = base + CH <= n;
 #pragma unroll
@@ -321,7 +355,8 @@ struct WChain {
         if (k == CH - 1) step_rows<true>(c, slot + k * G::kStep, zs + k * kWSeq, r);
         else step_rows<false>(c, slot + k * G::kStep, zs + k * kWSeq, r);
 #else
-        step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
+        if (AN) step_rows(c, slot + k * G::kStep, nullptr, r, es + k * kWSeq, t0 + dir * (base + k) == c.T - 1);
+        else step_rows(c, slot + k * G::kStep, zs + k * kWSeq, r);
 #endif
       }
       barrier_lds(&dg);
@@ -337,13 +372,13 @@ struct WChain {
   }
 };
 
-template <bool FWD, int NT, int NC>
-__device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, double* Sblk, int lane, long b0,
-                                        int nchA, int nchB) {
+template <bool FWD, int NT, int NC, bool AN>
+__device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, double* Sblk, int* Eblk, int lane,
+                                        long b0, int nchA, int nchB) {
   using G = Geo<NT>;
   const int j = lane & 15, g = lane >> 4;
   const int T = a.T, H = a.H;
-  WChain<FWD, NT, NC> ch;
+  WChain<FWD, NT, NC, AN> ch;
 #pragma unroll
   for (int qo = 0; qo < NT; qo++)
 #pragma unroll
@@ -354,8 +389,20 @@ __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, do
         ch.Aop[qo][qi][r] = FWD ? a.A[in * 64 + out] : a.A[out * 64 + in];
       }
   if (FWD) {
+    double py = 0.0;
 #pragma unroll
-    for (int q = 0; q < NT; q++) ch.X[q] = load4(a.pi + 16 * q + 2 * g);
+    for (int q = 0; q < NT; q++) {
+      ch.X[q] = load4(a.pi + 16 * q + 2 * g);
+      if (AN) {
+        ch.wv[q] = load4(a.w + 16 * q + 2 * g);
+        py += (ch.X[q].x * ch.wv[q].x + ch.X[q].y * ch.wv[q].y) + (ch.X[q].z * ch.wv[q].z + ch.X[q].w * ch.wv[q].w);
+      }
+    }
+    if (AN) {
+      asm("" : "+v"(py));
+      ch.m1 = swap16_sum(swap32_sum(py));                 // y_{-1} = prior . w
+      ch.renorm();
+    }
   } else {
     v4d e[NT];
     ch.evidence(c, T - 1, e);
@@ -371,6 +418,7 @@ __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, do
       ch.X[q] = e[q] * beta;
       part += (ch.X[q].x + ch.X[q].y) + (ch.X[q].z + ch.X[q].w);
     }
+    if (AN && g == 0) Eblk[(long)(T - 1) * kWSeq + j] = 0;     // its exponent
     ch.sc = -__builtin_amdgcn_frexp_exp(swap16_sum(swap32_sum(part)));
   }
   MwDiag dg;
@@ -382,6 +430,13 @@ __device__ __forceinline__ void wfilter(const WideMfmaArgs& a, const WCtx& c, do
   if (FWD) ch.run(c, T - H, nchB, H, lane, dg);
   else ch.run(c, H, nchB, H - 1, lane, dg);
   dg.write(a.diag, b0 / kWSeq, FWD ? 0 : 1, lane);
+  if (AN && FWD && g == 0 && b0 + j < a.B) {
+    double ll = log(ch.m2) - log(ch.m1) + (double)(ch.e2 - ch.e1) * 0.69314718055994530942;
+    const bool dead = ch.zmin == 0.0;
+    if (dead) ll = -DBL_MAX;
+    if (a.ll) a.ll[b0 + j] = ll;
+    if (a.status) a.status[b0 + j] = dead ? 1u : 0u;
+  }
 }
 
 // ll of the forward filter (nip.c:1461-1474), kept by the forward partner:
@@ -458,9 +513,18 @@ struct WLL {
 // even chunks, the backward partner (which has no ll of its own and waits at
 // the barriers otherwise) the odd ones; its partial products join the forward
 // partner's through LDS after the block's closing barrier.
-template <bool FWD, bool PVEC, int NT, bool FILT>
+// AN (smoothing, round 5): the filters publish each message's accumulated
+// exponent (alpha^_t = alpha_t 2^Ef_t, beta^_t = beta_t 2^Eb_t; phase A's go
+// to the scratch next to the messages), so sum_y alpha^_t beta^_t =
+// Z 2^(Ef_t + Eb_t) for every t: one sum per chain at the partner's first
+// phase-B step (c*, exponent E*, kept in LDS) normalises every posterior,
+//   posterior_t = alpha^_t o beta^_t 2^(E* - Ef_t - Eb_t) / c*
+// -- a multiply and an ldexp where each (chain, step) took a 16-lane DPP sum
+// and a Newton reciprocal.  The ll is the forward filter's (WChain).
+template <bool FWD, bool PVEC, int NT, bool FILT, bool AN = false>
 __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* out, const double* fring,
-                                         const double* zr, double* Sblk, int lane, long b0, int nchA, int nchB) {
+                                         const double* zr, double* Sblk, int lane, long b0, int nchA, int nchB,
+                                         const int* er = nullptr, int* Eblk = nullptr, double* cz = nullptr) {
   using G = Geo<NT>;
   constexpr int NP = G::NP, LPC = G::LPC, CH = G::CH, QN = G::QN;
   const int T = a.T, H = a.H;
@@ -536,7 +600,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   auto drainA = [&](int ci) {
     if (NIPAMD_MW_ABLATE == 1) return;
     const double* slot = out + (ci & 1) * G::kSlot;
-    if (FWD) ll_chunk(ci, nA, tA);
+    if (FWD && !AN) ll_chunk(ci, nA, tA);
     if constexpr (FILT) {
       if (!PVEC && !a.post) return;
       v2d ones[kWSeq];
@@ -556,6 +620,7 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
         const v2d v = *reinterpret_cast<const v2d*>(slot + k * G::kStep + G::piece_off(jj, p));
         store_pol<NIPAMD_WIDE_SCR_NT>(reinterpret_cast<v2d*>(Sblk + (long)t * G::kStep + 2 * u), v);
       }
+      if (AN && lane < kWSeq) Eblk[(long)t * kWSeq + lane] = er[((ci & 1) * CH + k) * kWSeq + lane];
     }
   };
   for (int ci = 0; ci < nchA; ci++) {
@@ -572,20 +637,73 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
     return;
   }
   v2d oa[kWSeq];
+  int eo[kWSeq];                                 // AN: the other direction's exponents
   auto load_other = [&](v2d (&o)[kWSeq], int ci) {
     if (NIPAMD_MW_ABLATE == 1) return;
     const double* q = Sblk + (long)(tlow(ci) + hi) * G::kStep + 2 * s;
 #pragma unroll
     for (int c = 0; c < kWSeq; c++) o[c] = load_pol<NIPAMD_SCR_NTLD>(reinterpret_cast<const v2d*>(q + c * NP));
+    if (AN) {
+      const int* qe = Eblk + (long)(tlow(ci) + hi) * kWSeq;
+#pragma unroll
+      for (int c = 0; c < kWSeq; c++) eo[c] = qe[c];
+    }
+  };
+  // AN: this ring step's posteriors, 2^(E* - Ef_t - Eb_t) / c* per chain
+  auto emit_an = [&](const double* slot, const int* es, int kk, int t, bool ok, const v2d (&o)[kWSeq]) {
+#pragma unroll
+    for (int q = 0; q < kWSeq; q++) {
+      const v2d v = *reinterpret_cast<const v2d*>(slot + kk * G::kStep + G::piece_off(q, s));
+      const v2d z = *reinterpret_cast<const v2d*>(cz + 2 * q);
+      const double f = __builtin_ldexp(z.x, (int)z.y - es[kk * kWSeq + q] - eo[q]);
+      const double px = v.x * o[q].x * f, py = v.y * o[q].y * f;
+      const long bb = b0 + q;
+      if constexpr (PVEC) {
+        double* p = (ok && bb < a.B) ? a.post + (size_t)bb * a.post_bstride + (long)t * NP + a.post_off + 2 * s : sink;
+        store_pol<NIPAMD_POST_NT>(reinterpret_cast<v2d*>(p), v2d{px, py});
+      } else {
+        if (ok && bb < a.B) {
+          double* p = a.post + (size_t)bb * a.post_bstride + (long)t * a.post_tstride + a.post_off + 2 * s;
+          if (st0) store_pol<NIPAMD_POST_NT>(p, px);
+          if (st1) store_pol<NIPAMD_POST_NT>(p + 1, py);
+        }
+      }
+    }
   };
   const int nBf = T - H;                         // the forward side's phase-B steps (from t = H)
   auto drainB = [&](int ci, const v2d (&o)[kWSeq]) {
     if (NIPAMD_MW_ABLATE == 1) return;
-    if (FWD == ((ci & 1) == 0) && ci * CH < nBf) ll_chunk(ci, nBf, H);
+    if (!AN && FWD == ((ci & 1) == 0) && ci * CH < nBf) ll_chunk(ci, nBf, H);
     if (!PVEC && !a.post) return;
     const double* slot = out + (ci & 1) * G::kSlot;
     const int nk = nB - ci * CH < CH ? nB - ci * CH : CH;
-    emit(slot, kB, tlow(ci) + hi, kB < nk, o);
+    if constexpr (AN) {
+      const int* es = er + (ci & 1) * CH * kWSeq;
+      if (ci == 0) {
+        // c* and E* of the 16 chains at this partner's first step (ring index 0:
+        // forward lanes hi = 0, backward hi = CH - 1)
+#pragma unroll
+        for (int q0 = 0; q0 < kWSeq; q0 += 8) {
+          double z[8];
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const v2d v = *reinterpret_cast<const v2d*>(slot + kB * G::kStep + G::piece_off(q0 + i, s));
+            z[i] = v.x * o[q0 + i].x + v.y * o[q0 + i].y;
+          }
+          sumL_n<LPC>(z);
+          double r[8];
+          recip_n(z, r);
+          if (kB == 0 && s == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+              *reinterpret_cast<v2d*>(cz + 2 * (q0 + i)) = v2d{r[i], (double)(es[q0 + i] + eo[q0 + i])};
+          }
+        }
+      }
+      emit_an(slot, es, kB, tlow(ci) + hi, kB < nk, o);
+    } else {
+      emit(slot, kB, tlow(ci) + hi, kB < nk, o);
+    }
   };
   // one buffer (two groups' partners share the register file with the
   // filters): the next chunk's vectors are requested as soon as this chunk's
@@ -602,9 +720,9 @@ __device__ __forceinline__ void wpartner(const WideMfmaArgs& a, const double* ou
   dg.write(a.diag, b0 / kWSeq, FWD ? 2 : 3, lane);
   // the forward ring slot the last chunk did not use (its readers passed the last loop barrier)
   double* share = const_cast<double*>(fring) + ((((nchB > 0 ? nchB : 1) - 1) & 1) ^ 1) * G::kSlot;
-  if (!FWD) ll.put(share, lane);
+  if (!AN && !FWD) ll.put(share, lane);
   barrier_lds();                                 // the block's closing barrier
-  if (FWD) {
+  if (!AN && FWD) {
     ll.take(share, lane);
     ll.write(a, b0, lane);
   }
@@ -627,9 +745,14 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   const int role = filter ? wave : wave - kWGroups * F;
   const int grp = role / F;
   const bool fwd = FILT || (role % F) == 0;
+  constexpr bool AN = !FILT && NIPAMD_MW_ANALYTIC;
   double* out = reinterpret_cast<double*>(smem) + grp * 4 * G::kSlot;   // this group's [2 dirs][2 slots][kSlot]
   double* zr = reinterpret_cast<double*>(smem) + kWGroups * 4 * G::kSlot + grp * 2 * G::CH * kWSeq;
+  // AN: the same area as the group's exponent rings [2 dirs][2 slots][CH][16] ints
+  int* er = reinterpret_cast<int*>(zr) + (fwd ? 0 : 2 * G::CH * kWSeq);
   double* tab = reinterpret_cast<double*>(smem) + kWGroups * (4 * G::kSlot + 2 * G::CH * kWSeq);
+  // AN: per partner (1/c*, E*) of its 16 chains, after the tables
+  double* cz = tab + a.tab_rows * G::NPS + (grp * 2 + (fwd ? 0 : 1)) * 2 * kWSeq;
   const int ncol = a.ncol > 0 ? a.ncol : 1;
   const int j = lane & 15, g = lane >> 4;
   const long b0 = (long)blockIdx.x * (kWGroups * kWSeq) + grp * kWSeq;
@@ -643,17 +766,21 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   const int nchA = (nA + G::CH - 1) / G::CH, nchB = FILT ? 0 : (nB + G::CH - 1) / G::CH;
   double* ring = out + (fwd ? 0 : 2 * G::kSlot);
   double* Sblk = FILT ? nullptr : a.S + (size_t)(b0 / kWSeq) * wblock_scratch(NT, T) + (size_t)kWG * G::kStep;
+  // AN: the phase-A messages' exponents [T + 2G][16] per group, after every group's messages and the sink group
+  int* Eblk = FILT ? nullptr
+                   : reinterpret_cast<int*>(a.S + (size_t)((a.B + kWSeq - 1) / kWSeq + 1) * wblock_scratch(NT, T)) +
+                         (size_t)(b0 / kWSeq) * wblock_exps(T) + (size_t)kWG * kWSeq;
   // A/B builds: static wave priority for the partners (1) or the filters (2)
   if ((NIPAMD_WIDE_PRIO == 1 && !filter) || (NIPAMD_WIDE_PRIO == 2 && filter)) __builtin_amdgcn_s_setprio(1);
   if (!filter) {
     const bool pvec = a.post && a.N == G::NP && a.post_tstride == G::NP && (a.post_off & 1) == 0 &&
                       (a.post_bstride & 1) == 0 && (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
     if (pvec) {
-      if (fwd) wpartner<true, true, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
-      else wpartner<false, true, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, true, NT, FILT, AN>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB, er, Eblk, cz);
+      else wpartner<false, true, NT, FILT, AN>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB, er, Eblk, cz);
     } else {
-      if (fwd) wpartner<true, false, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
-      else wpartner<false, false, NT, FILT>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB);
+      if (fwd) wpartner<true, false, NT, FILT, AN>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB, er, Eblk, cz);
+      else wpartner<false, false, NT, FILT, AN>(a, ring, out, zr, Sblk, lane, b0, nchA, nchB, er, Eblk, cz);
     }
     return;
   }
@@ -671,14 +798,16 @@ void chain_mfma_wide_kernel(WideMfmaArgs a) {
   }
   c.out = ring;
   c.zr = zr;
+  c.er = er;
   c.zw = g == 0;
+  c.j = j;
 #pragma unroll
   for (int q = 0; q < NT; q++) {
     c.wo[q][0] = Geo<NT>::piece_off(j, 8 * q + g);
     c.wo[q][1] = Geo<NT>::piece_off(j, 8 * q + 4 + g);
   }
-  if (fwd) wfilter<true, NT, NC>(a, c, Sblk, lane, b0, nchA, nchB);
-  else if (!FILT) wfilter<false, NT, NC>(a, c, Sblk, lane, b0, nchA, nchB);
+  if (fwd) wfilter<true, NT, NC, AN>(a, c, Sblk, Eblk, lane, b0, nchA, nchB);
+  else if (!FILT) wfilter<false, NT, NC, AN>(a, c, Sblk, Eblk, lane, b0, nchA, nchB);
   if (!FILT) barrier_lds();                       // the block's closing barrier (wpartner)
 }
 
@@ -688,11 +817,13 @@ size_t chain_mfma_wide_lds_bytes(int NT, int tab_rows, int ncol, int T) {
   (void)ncol; (void)T;                                       // codes are read from HBM
   const size_t slot = 2048;                                  // doubles per ring slot
   const size_t ch = 8 / NT;
-  return (kWGroups * (4 * slot + 2 * ch * kWSeq) + (size_t)tab_rows * (16 * NT + 2)) * sizeof(double);
+  return (kWGroups * (4 * slot + 2 * ch * kWSeq) + (size_t)tab_rows * (16 * NT + 2) +
+          kWGroups * 2 * 2 * kWSeq) * sizeof(double);        // + the partners' (1/c*, E*)
 }
 
 size_t chain_mfma_wide_scratch_bytes(int NT, long B, int T) {
-  return (size_t)((B + kWSeq - 1) / kWSeq + 1) * wblock_scratch(NT, T) * sizeof(double);
+  const long groups = (B + kWSeq - 1) / kWSeq + 1;
+  return (size_t)groups * wblock_scratch(NT, T) * sizeof(double) + (size_t)groups * wblock_exps(T) * sizeof(int);
 }
 
 namespace {

@@ -527,58 +527,108 @@ int stats_launch(const EWideArgs& a, hipStream_t stream) {
 //
 // op_fb_kernel's recursion (opchain.hip) with the wide e_step's layout: a
 // wave per direction holds 64 / NP sequences (lane = state), the step's
-// operator column (forward: T_c(x, y) for lane y) or row (backward: T_c(y,
-// x)) is read per step from HBM / L2 -- the combinations of the next 8 steps
-// a chunk ahead -- and the mat-vec takes the input by DPP row broadcasts.
-//   forward:  alpha_t = T_{c_t}^T alpha_{t-1}  (alpha_{-1} = prior), stored
-//   backward: beta_{t-1} = T_{c_t} beta_t     (beta_{T-1} = 1), stored
+// operator column (forward: T'(x, y) for lane y) or row (backward: T'(y, x))
+// is read per step -- from LDS when the operators fit (TL), else through the
+// caches -- one step ahead of its use, and the mat-vec takes the input by DPP
+// row broadcasts.  With the leaf factors e_t(y) = prod_j F_j[c_j,t](y):
+//   forward:  alpha_t = e_t o T'^T alpha_{t-1}  (alpha_{-1} = prior), stored
+//   backward: beta_{t-1} = T' (e_t o beta_t)   (beta_{T-1} = 1), stored
 //   ll = sum over steps with evidence of log m2_t - log m1_t (nip.c:1458-1474)
-template <int NP>
+// A step's evidence combination (opchain.h): each observed variable missing or
+// one of its states; an out-of-range state selects the all-zero operator ncomb.
+__device__ __forceinline__ int op_comb(const OpWideArgs& a, const int32_t* o) {
+  int c = 0;
+  for (int k = 0; k < a.nobs; k++) {
+    const int v = o[a.col[k]];
+    if (v >= a.card[k]) return a.ncomb;
+    if (v >= 0) c += (v + 1) * a.cstride[k];
+  }
+  return c;
+}
+
+// the step's operator index c' | (the step has evidence) << 30
+constexpr int kOpEv = 1 << 30;
+__device__ __forceinline__ int op_code(const OpWideArgs& a, const int32_t* o) {
+  int c = 0;
+  bool ev = false, oor = false;
+  for (int k = 0; k < a.onobs; k++) {
+    const int v = o[a.ocol[k]];
+    oor |= v >= a.ocard[k];
+    ev |= v >= 0;
+    if (v >= 0) c += (v + 1) * a.ocstride[k];
+  }
+  for (int j = 0; j < a.nleaf; j++) ev |= o[a.lcol[j]] >= 0;
+  return (oor ? a.oncomb : c) | (ev ? kOpEv : 0);
+}
+
+// the leaf factors' product at state y (1 without leaves)
+__device__ __forceinline__ double op_leaf_e(const OpWideArgs& a, const int32_t* o, int y) {
+  double e = 1.0;
+  for (int j = 0; j < a.nleaf; j++) {
+    const int v = o[a.lcol[j]], M = a.lcard[j];
+    const int r = v < 0 ? M : (v < M ? v : M + 1);
+    e *= a.ltab[a.loff[j] + r * a.K + y];
+  }
+  return e;
+}
+
+typedef __attribute__((address_space(3))) double op_lds_d;
+
+template <int NP, bool TL>
 __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char op_smem[];
   constexpr int SPW = 64 / NP, NB = NP / 16;
   constexpr int WD = kMsgWaves / 2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T, K = a.K, KK = K * K;
+  op_lds_d* const Tl = (op_lds_d*)(op_smem);                 // TL: [(oncomb + 1)][K][K]
+  if (TL) {
+    for (int i = tid; i < (a.oncomb + 1) * KK; i += kMsgWaves * 64) Tl[i] = a.Ttab[i];
+    __syncthreads();
+  }
   const bool fwd = wave < WD;
   if (!fwd && a.filter) return;
   const int s = lane / NP, y = lane % NP;
   const long b = (long)blockIdx.x * (WD * SPW) + (wave % WD) * SPW + s;
   const bool active = b < a.B;
   const long bb = active ? b : 0;
-  const int T = a.T, K = a.K, KK = K * K;
   const bool ys = y < K;
+  const int yc = ys ? y : 0;
   const int32_t* obs = a.obs ? a.obs + bb * a.obs_bstride : nullptr;
-  auto comb = [&](int t) {
-    int c = 0;
+  const bool est = a.estep != 0;
+  int* const scrow = est ? a.sc + (size_t)bb * T : nullptr;
+  // a chunk's steps: operator codes and leaf factors, a chunk ahead
+  auto prep = [&](int t, int& code, double& e) {
+    code = 0;
+    e = 1.0;
     if (obs && t >= 0 && t < T) {
       const int32_t* o = obs + (long)t * a.obs_tstride;
-      for (int k = 0; k < a.nobs; k++) {
-        const int v = o[a.col[k]];
-        if (v >= a.card[k]) { c = a.ncomb; break; }
-        if (v >= 0) c += (v + 1) * a.cstride[k];
-      }
+      code = op_code(a, o);
+      if (a.nleaf) e = op_leaf_e(a, o, yc);
     }
-    return c;
   };
-  // this lane's column (forward) / row (backward) of T_c, in 16-state blocks
-  auto coef = [&](int c, double (&C)[NB][16]) {
-    const double* t = a.Ttab + (size_t)c * KK;
+  // this lane's column (forward) / row (backward) of T'_c, in 16-state blocks
+  auto coef = [&](int code, double (&C)[NB][16]) {
+    const int c = code & (kOpEv - 1);
 #pragma unroll
     for (int k = 0; k < NB; k++)
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const int x = 16 * k + j;
-        C[k][j] = (x < K && ys) ? (fwd ? t[x * K + y] : t[y * K + x]) : 0.0;
+        const int i = c * KK + (fwd ? x * K + y : y * K + x);
+        C[k][j] = (x < K && ys) ? (TL ? (double)Tl[i] : a.Ttab[i]) : 0.0;
       }
   };
   int cc[kMsgChunk], cn[kMsgChunk];
+  double ec[kMsgChunk], en[kMsgChunk];
   const int dir = fwd ? 1 : -1, t0 = fwd ? 0 : T - 1;
 #pragma unroll
-  for (int k = 0; k < kMsgChunk; k++) cc[k] = comb(t0 + dir * k);
+  for (int k = 0; k < kMsgChunk; k++) prep(t0 + dir * k, cc[k], ec[k]);
   double x;
   int sc = 0;
   double m2 = 1.0, m1 = 1.0;
   int e2 = 0, e1 = 0;
-  bool dead = false;
+  bool dead = false, bad = false;
   const double wy = ys ? a.w[y] : 0.0;
   double* const Srow = (fwd ? a.Sa : a.Sb) + (size_t)bb * T * NP + y;
   if (fwd) {
@@ -587,31 +637,37 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
     x = ys ? 1.0 : 0.0;                                 // beta_{T-1}
     if (active) Srow[(size_t)(T - 1) * NP] = x;
   }
+  double C[NB][16];
+  coef(cc[0], C);
   // forward: steps t = 0..T-1; backward: t = T-1..1 (each making beta_{t-1})
   const int n = fwd ? T : T - 1;
   for (int j0 = 0; j0 < n; j0 += kMsgChunk) {
 #pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) cn[k] = comb(t0 + dir * (j0 + kMsgChunk + k));
+    for (int k = 0; k < kMsgChunk; k++) prep(t0 + dir * (j0 + kMsgChunk + k), cn[k], en[k]);
 #pragma unroll
     for (int k = 0; k < kMsgChunk; k++) {
       const int j = j0 + k;
       if (j >= n) break;
       const int t = t0 + dir * j;
-      double C[NB][16];
-      coef(cc[k], C);
       const double m1v = fwd ? group_sum<NP>(x * wy) : 0.0;
-      const double u = __builtin_ldexp(matvec_dpp<NB>(x, C), sc);
+      const double acc = matvec_dpp<NB>(fwd ? x : x * ec[k], C);
+      coef(k + 1 < kMsgChunk ? cc[k + 1] : cn[0], C);   // the next step's operator, under this step's work
+      double u = __builtin_ldexp(acc, sc);
+      if (fwd) u *= ec[k];
       const double z = group_sum<NP>(u);
       if (fwd) {
-        if (cc[k] != 0) {                               // a step with evidence
+        if (cc[k] & kOpEv) {                            // a step with evidence
           m2 *= z;
           m1 *= __builtin_ldexp(m1v, sc);
           const int k2 = m2 != 0.0 ? __builtin_amdgcn_frexp_exp(m2) : 0;
           const int k1 = m1 != 0.0 ? __builtin_amdgcn_frexp_exp(m1) : 0;
           m2 = __builtin_ldexp(m2, -k2); e2 += k2;
           m1 = __builtin_ldexp(m1, -k1); e1 += k1;
+          // e_step's BAD_LUCK (nip.c:1827-1854), as op_fb_kernel checks it
+          if (est && (m2 <= 0.0 || m1 <= 0.0 || e2 > e1 || (e2 == e1 && m2 > m1))) bad = true;
         }
         dead |= z == 0.0;
+        if (est && active && y == 0) scrow[t] = sc;
         if (active) store_pol<NIPAMD_MSG_NT>(Srow + (size_t)t * NP, u);   // alpha^_t
       } else {
         if (active) store_pol<NIPAMD_MSG_NT>(Srow + (size_t)(t - 1) * NP, u);   // beta^_{t-1}
@@ -620,13 +676,17 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
       x = u;
     }
 #pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) cc[k] = cn[k];
+    for (int k = 0; k < kMsgChunk; k++) {
+      cc[k] = cn[k];
+      ec[k] = en[k];
+    }
   }
   if (fwd && active && y == 0) {
     double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
     if (dead) ll = -DBL_MAX;
     if (a.ll) a.ll[b] = ll;
-    if (a.status) a.status[b] = dead ? 1u : 0u;       // NIPAMD_STATUS_ZERO_MASS
+    // NIPAMD_STATUS_ZERO_MASS (1); in e_step mode also NIPAMD_STATUS_BAD_LUCK (2)
+    if (a.status) a.status[b] = (dead ? 1u : 0u) | (est && (dead || bad) ? 2u : 0u);
   }
 }
 
@@ -650,24 +710,217 @@ __global__ __launch_bounds__(256) void op_wide_post_kernel(OpWideArgs a) {
   }
 }
 
+// The operator chain's e_step at 17..64 states: op_xi_sort_kernel's sums
+// (opchain.hip) from the stored messages.  Step t's xi weights are
+//   W_t(x, y) = alpha^_{t-1}(x) beta^_t(y) f_t,  f_t = 2^sc_t / sum_y alpha^_t(y) beta^_t(y)
+// (alpha^_t = 2^sc_t T_{c_t}^T alpha^_{t-1}, so f_t = 1 / Z'_t, the step's xi
+// mass; alpha^_{-1} = the prior), the same products as op_fb_kernel's xi_row.
+// A block owns 16 sequences and one slab row: Xi_c [K][K] for every
+// combination c, then P0 [K].  The group's steps (sequence-major; at most
+// kXwTileMax at a time, the whole group when T <= 1024) are sorted by
+// (combination, position) in LDS -- a bitonic sort of packed keys, so every
+// combination's steps keep their stream order -- then staged kXwBatch at a
+// time (the weights' two vectors per step in LDS, f_t by a wave sum) and
+// summed by a thread per cell, CPT cells each, in sorted order: a fixed
+// summation order, independent of the launch (shard invariance).  A
+// combination's sum leaves for the slab row when the sorted stream moves on:
+// a plain store in the first tile (each combination once; the row was zeroed
+// by the same thread before), read-add-write in later ones.
+constexpr int kXwTileBits = 14;
+constexpr int kXwTileMax = 1 << kXwTileBits;   // steps per sorted tile (the key's low bits)
+constexpr int kXwBatch = 32;                 // sorted steps staged per pass (8 per wave)
+constexpr int kXwThreads = 256;
+
+// the sorted tile's length: the group's stream rounded up to a power of two
+__host__ __device__ inline int op_xi_tile(int T) {
+  const long n = (long)kOpXiSeqs * T;
+  int L = 64;
+  while (L < n && L < kXwTileMax) L <<= 1;
+  return L;
+}
+
+template <int NP, int CPT>
+__global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned key[];   // [op_xi_tile(T)]
+  __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP];
+  __shared__ int kb[kXwBatch];
+  __shared__ double p0s[kOpXiSeqs][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K = a.K, KK = K * K, T = a.T;
+  const int L = op_xi_tile(T);
+  const long b0 = (long)blockIdx.x * kOpXiSeqs;
+  const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
+  const long n = (long)nseq * T;
+  const size_t R = (size_t)op_xi_row(K, a.ncomb);
+  double* const out = a.slab + (size_t)blockIdx.x * R;
+  int cx[CPT], cy[CPT];
+  bool con[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; k++) {
+    const int cell = tid + kXwThreads * k;
+    con[k] = cell < KK;
+    cx[k] = con[k] ? cell / K : 0;
+    cy[k] = con[k] ? cell - cx[k] * K : 0;
+  }
+  // the row's Xi part zeroed by the threads that own the cells (each cell is
+  // later written, or read and written, by the same thread only)
+  for (int c = 0; c <= a.ncomb; c++)
+#pragma unroll
+    for (int k = 0; k < CPT; k++)
+      if (con[k]) out[(size_t)c * KK + tid + kXwThreads * k] = 0.0;
+
+  double acc[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; k++) acc[k] = 0.0;
+  int cur = -1;
+  auto flush = [&](bool first) {
+    if (cur >= 0) {
+#pragma unroll
+      for (int k = 0; k < CPT; k++) {
+        double* o = out + (size_t)cur * KK + tid + kXwThreads * k;
+        if (con[k]) *o = first ? acc[k] : *o + acc[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CPT; k++) acc[k] = 0.0;
+    cur = -1;
+  };
+  constexpr int SPW = 64 / NP;
+  const int y = lane % NP;
+  const bool ys = y < K;
+  for (long i0 = 0; i0 < n; i0 += L) {
+    const int m = (int)((n - i0) < L ? (n - i0) : L);
+    for (int i = tid; i < L; i += kXwThreads) {
+      unsigned v = 0xFFFFFFFFu;                       // padding sorts last
+      if (i < m) {
+        const long g = i0 + i;
+        const long s = g / T, t = g - s * T;
+        const int c = a.obs ? op_comb(a, a.obs + (b0 + s) * a.obs_bstride + t * a.obs_tstride) : 0;
+        v = ((unsigned)c << kXwTileBits) | (unsigned)i;
+      }
+      key[i] = v;
+    }
+    __syncthreads();
+    for (int k2 = 2; k2 <= L; k2 <<= 1)
+      for (int j = k2 >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < L; i += kXwThreads) {
+          const int p = i ^ j;
+          if (p > i) {
+            const unsigned u = key[i], w = key[p];
+            if ((u > w) == ((i & k2) == 0)) { key[i] = w; key[p] = u; }
+          }
+        }
+        __syncthreads();
+      }
+    for (int j0 = 0; j0 < m; j0 += kXwBatch) {
+      // stage: wave w the batch slots 8w .. 8w + 7, 64 / NP of them per pass
+#pragma unroll
+      for (int q = 0; q < kXwBatch / 4; q += SPW) {
+        const int jj = wave * (kXwBatch / 4) + q + lane / NP;
+        const int j = j0 + jj;
+        const bool ok = j < m;
+        const unsigned v = key[ok ? j : 0];
+        const long g = i0 + (v & (kXwTileMax - 1));
+        const long s = g / T, t = g - s * T, b = b0 + s;
+        const double* sa = a.Sa + ((size_t)b * T + t) * NP + y;
+        const double* sb = a.Sb + ((size_t)b * T + t) * NP + y;
+        const bool on = ok && ys;
+        const double at = on ? sa[0] : 0.0, bt = on ? sb[0] : 0.0;
+        const double ap = on ? (t > 0 ? sa[-NP] : a.pi[y]) : 0.0;
+        const double z = group_sum<NP>(at * bt);
+        const int sc = ok ? a.sc[(size_t)b * T + t] : 0;
+        const double f = z != 0.0 ? __builtin_ldexp(1.0 / z, sc) : 0.0;
+        Ab[jj][y] = ap;
+        Gb[jj][y] = bt * f;
+        if (y == 0) kb[jj] = ok ? (int)(v >> kXwTileBits) : -1;
+      }
+      __syncthreads();
+      const int nj = (m - j0) < kXwBatch ? (m - j0) : kXwBatch;
+      for (int jj = 0; jj < nj; jj++) {
+        const int c = kb[jj];
+        if (c != cur) { flush(i0 == 0); cur = c; }
+#pragma unroll
+        for (int k = 0; k < CPT; k++) acc[k] = __builtin_fma(Ab[jj][cx[k]], Gb[jj][cy[k]], acc[k]);
+      }
+      __syncthreads();
+    }
+    flush(i0 == 0);
+  }
+  // P0 per sequence: normalise(prior o T_{c_0} beta^_0), as op_fb_kernel's
+  // extra backward step; then summed over the group in sequence order
+  for (int s = wave; s < nseq; s += 4) {
+    const long b = b0 + s;
+    const int32_t* o0 = a.obs ? a.obs + b * a.obs_bstride : nullptr;
+    const int c0 = o0 ? (op_code(a, o0) & (kOpEv - 1)) : 0;
+    const double* Tc = a.Ttab + (size_t)c0 * KK;
+    const double* bz = a.Sb + (size_t)b * T * NP;
+    const bool xs = lane < K;
+    double u = 0.0;
+    if (xs)
+      for (int k = 0; k < K; k++)
+        u = __builtin_fma(Tc[lane * K + k], (o0 && a.nleaf ? op_leaf_e(a, o0, k) : 1.0) * bz[k], u);
+    const double pr = xs ? a.pi[lane] * u : 0.0;
+    const double z = group_sum<64>(pr);
+    p0s[s][lane] = z != 0.0 ? pr / z : pr;
+  }
+  __syncthreads();
+  if (tid < K) {
+    double p = 0.0;
+    for (int s = 0; s < nseq; s++) p += p0s[s][tid];
+    out[(size_t)(a.ncomb + 1) * KK + tid] = p;
+  }
+}
+
 }  // namespace
+
+// the operators in LDS while two blocks per CU still fit (op_wide_msgs_kernel
+// runs two waves per SIMD)
+constexpr size_t kOpWideTl = 76 * 1024;
+
+template <int NP>
+int msgs_launch(const OpWideArgs& a, hipStream_t stream) {
+  const int spb = kMsgWaves / 2 * (64 / NP);
+  const dim3 g((unsigned)((a.B + spb - 1) / spb)), th(kMsgWaves * 64);
+  const size_t tl = (size_t)(a.oncomb + 1) * a.K * a.K * sizeof(double);
+  if (tl <= kOpWideTl) {
+    static size_t set[kMaxDevices] = {};
+    if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_msgs_kernel<NP, true>), tl, set)) return -1;
+    hipLaunchKernelGGL((op_wide_msgs_kernel<NP, true>), g, th, tl, stream, a);
+  } else {
+    hipLaunchKernelGGL((op_wide_msgs_kernel<NP, false>), g, th, 0, stream, a);
+  }
+  if (a.post) {
+    const long prow = (a.B * a.T + 4 * (64 / NP) - 1) / (4 * (64 / NP));
+    hipLaunchKernelGGL(op_wide_post_kernel<NP>, dim3((unsigned)prow), dim3(256), 0, stream, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int op_wide_launch(const OpWideArgs& a, hipStream_t stream) {
   if (a.B <= 0) return 0;
-  if (a.K > 64 || a.K < 1) return -2;
-  const int NP = op_wide_np(a.K);
-  const int spb = kMsgWaves / 2 * (64 / NP);
-  const int blocks = (int)((a.B + spb - 1) / spb);
-  const long prow = (a.B * a.T + 4 * (64 / NP) - 1) / (4 * (64 / NP));
-  if (NP == 32) {
-    hipLaunchKernelGGL(op_wide_msgs_kernel<32>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
-    if (a.post) hipLaunchKernelGGL(op_wide_post_kernel<32>, dim3((unsigned)prow), dim3(256), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(op_wide_msgs_kernel<64>, dim3(blocks), dim3(kMsgWaves * 64), 0, stream, a);
-    if (a.post) hipLaunchKernelGGL(op_wide_post_kernel<64>, dim3((unsigned)prow), dim3(256), 0, stream, a);
-  }
+  if (a.K > 64 || a.K < 1 || a.nleaf > kOpMaxLeaf) return -2;
   g_last_kernel = "op_wide_msgs_kernel + op_wide_post_kernel";
+  return op_wide_np(a.K) == 32 ? msgs_launch<32>(a, stream) : msgs_launch<64>(a, stream);
+}
+
+template <int NP, int CPT>
+int xi_launch(const OpWideArgs& a, hipStream_t stream) {
+  const size_t lds = (size_t)op_xi_tile(a.T) * sizeof(unsigned);
+  static size_t set[kMaxDevices] = {};
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP, CPT>), lds, set)) return -1;
+  const dim3 g((unsigned)((a.B + kOpXiSeqs - 1) / kOpXiSeqs)), th(kXwThreads);
+  hipLaunchKernelGGL((op_wide_xi_kernel<NP, CPT>), g, th, lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int op_wide_xi_launch(const OpWideArgs& a, hipStream_t stream) {
+  if (a.B <= 0) return 0;
+  if (a.K > 64 || a.K < 17 || a.ncomb > 65534 || !a.sc || !a.slab) return -2;
+  const int KK = a.K * a.K;
+  if (KK <= 2 * kXwThreads) return xi_launch<32, 2>(a, stream);
+  if (KK <= 4 * kXwThreads) return xi_launch<32, 4>(a, stream);
+  if (KK <= 8 * kXwThreads) return xi_launch<64, 8>(a, stream);
+  return xi_launch<64, 16>(a, stream);
 }
 
 int estep_wide_np(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 0; }

@@ -33,6 +33,7 @@ namespace {
 
 constexpr long kOpMaxWork = 1L << 26;     // assignments x consistent combinations
 constexpr size_t kOpMaxTableBytes = 64L << 20;   // operators in HBM (LDS when <= 96 KB)
+constexpr size_t kOpMaxWideRow = 32L << 20;      // 17..64 states: an e_step slab row (16 sequences)
 
 struct OpPlan {
   std::vector<int> ov;
@@ -42,10 +43,17 @@ struct OpPlan {
   std::string why;
   int K = 0, ncomb = 0;
   std::vector<int> card, stride;
-  std::vector<double> T, w, pi;
+  // the operators' index (K > 16: the observed variables that are not leaf
+  // factors, opchain.h) and the leaf factors' tables
+  int oncomb = 0;
+  std::vector<int> oi, ostride;      // positions in ov, radix
+  std::vector<int> li, loff;         // positions in ov, offsets into lt
+  std::vector<double> lt;
+  std::vector<double> T, w, pi;      // T: [(oncomb + 1)][K][K]
   double* dT = nullptr;
   double* dw = nullptr;
   double* dpi = nullptr;
+  double* dlt = nullptr;
   double* S = nullptr;
   size_t S_bytes = 0;
   // e_step: the projection of the per-combination xi sums onto the em_learn
@@ -60,7 +68,7 @@ struct OpPlan {
   double* E = nullptr;
   size_t E_bytes = 0;
   ~OpPlan() {
-    (void)hipFree(dT); (void)hipFree(dw); (void)hipFree(dpi); (void)hipFree(S);
+    (void)hipFree(dT); (void)hipFree(dw); (void)hipFree(dpi); (void)hipFree(dlt); (void)hipFree(S);
     (void)hipFree(d_mptr); (void)hipFree(d_midx); (void)hipFree(d_mcoef); (void)hipFree(E);
   }
 };
@@ -73,6 +81,9 @@ OpCache* cache_of(nipamd_model* mm) {
   if (!mm->op) mm->op = new OpCache();
   return static_cast<OpCache*>(mm->op);
 }
+
+template <typename V>
+bool has(const V& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); }
 
 bool build(const Model& m, OpPlan& P) {
   const auto& prev = m.previous_outgoing;
@@ -96,33 +107,70 @@ bool build(const Model& m, OpPlan& P) {
     P.stride.push_back((int)ncomb);
     ncomb *= m.vars[v].card + 1;
   }
-  if (ncomb > 65534 || (size_t)(ncomb + 1) * K * K * sizeof(double) > kOpMaxTableBytes) {
+  if (ncomb > 65534) { P.why = "too many evidence combinations"; return false; }
+  std::vector<int> pri;
+  for (int v : m.independent)
+    if (m.vars[v].has_prior && !(m.vars[v].ifs & IF_OLD_OUTGOING)) pri.push_back(v);
+  // Leaf factors (17..64 states, op_wide_msgs_kernel): an observed variable
+  // in exactly one clique whose other variables are all current-interface
+  // ones carries every factor it appears in within that clique, so summing it
+  // out under its evidence leaves a function of y alone, F[c_v](y), and
+  // T_c = T'_{c'} diag(prod F) -- c' over the other observed variables.
+  std::vector<char> leaf(no, 0);
+  std::vector<int> lcl;
+  if (K > 16)
+    for (int i = 0; i < no && (int)lcl.size() < kOpMaxLeaf; i++) {
+      const int v = P.ov[i];
+      if (has(cur, v) || has(prev, v) || has(pri, v)) continue;
+      int cl = -1, nc = 0;
+      for (size_t c = 0; c < m.cliques.size(); c++)
+        if (has(m.cliques[c].vars, v)) { cl = (int)c; nc++; }
+      if (nc != 1 || has(lcl, cl)) continue;
+      bool ok = true;
+      for (int u : m.cliques[cl].vars) ok = ok && (u == v || has(cur, u));
+      if (!ok) continue;
+      leaf[i] = 1;
+      lcl.push_back(cl);
+    }
+  long oncomb = 1;
+  for (int i = 0; i < no; i++)
+    if (!leaf[i]) {
+      P.oi.push_back(i);
+      P.ostride.push_back((int)oncomb);
+      oncomb *= P.card[i] + 1;
+    }
+  if ((size_t)(oncomb + 1) * K * K * sizeof(double) > kOpMaxTableBytes) {
     P.why = "too many evidence combinations";
     return false;
   }
+  std::vector<char> skip(nv, 0);                        // leaf variables: not enumerated
+  for (int i = 0; i < no; i++) if (leaf[i]) skip[P.ov[i]] = 1;
   long total = 1;
-  for (const Var& V : m.vars) {
-    total *= V.card;
+  for (int v = 0; v < nv; v++) {
+    if (skip[v]) continue;
+    total *= m.vars[v].card;
     if (total > kOpMaxWork) break;
   }
-  if (total * (1L << no) > kOpMaxWork) { P.why = "slice too large to enumerate"; return false; }
+  if (total * (1L << P.oi.size()) > kOpMaxWork) { P.why = "slice too large to enumerate"; return false; }
 
   P.K = (int)K;
   P.ncomb = (int)ncomb;
-  P.T.assign((size_t)(ncomb + 1) * K * K, 0.0);     // + the zero operator of an out-of-range state
+  P.oncomb = (int)oncomb;
+  P.T.assign((size_t)(oncomb + 1) * K * K, 0.0);    // + the zero operator of an out-of-range state
   // per clique: the flat-index stride of every variable (dimension 0 fastest)
   std::vector<std::vector<std::pair<int, long>>> cst(m.cliques.size());
   for (size_t c = 0; c < m.cliques.size(); c++) {
     long st = 1;
     for (int v : m.cliques[c].vars) { cst[c].push_back({v, st}); st *= m.vars[v].card; }
   }
-  std::vector<int> pri;
-  for (int v : m.independent)
-    if (m.vars[v].has_prior && !(m.vars[v].ifs & IF_OLD_OUTGOING)) pri.push_back(v);
+  std::vector<char> lc(m.cliques.size(), 0);
+  for (int c : lcl) lc[c] = 1;
+  const int nop = (int)P.oi.size();
   std::vector<int> a(nv, 0);
   for (long it = 0; it < total; it++) {
     double W = 1.0;
     for (size_t c = 0; c < m.cliques.size() && W != 0.0; c++) {
+      if (lc[c]) continue;
       long idx = 0;
       for (const auto& e : cst[c]) idx += a[e.first] * e.second;
       W *= m.cliques[c].original[(size_t)idx];
@@ -134,21 +182,49 @@ bool build(const Model& m, OpPlan& P) {
         x += a[prev[i]] * sx; sx *= m.vars[prev[i]].card;
         y += a[cur[i]] * sy; sy *= m.vars[cur[i]].card;
       }
-      for (long mask = 0; mask < (1L << no); mask++) {
+      for (long mask = 0; mask < (1L << nop); mask++) {
         long c = 0;
-        for (int i = 0; i < no; i++)
-          if (mask >> i & 1) c += (long)(a[P.ov[i]] + 1) * P.stride[i];
+        for (int q = 0; q < nop; q++)
+          if (mask >> q & 1) c += (long)(a[P.ov[P.oi[q]]] + 1) * P.ostride[q];
         P.T[(size_t)c * K * K + x * K + y] += W;
       }
     }
     for (int v = 0; v < nv; v++) {                      // odometer, variable 0 fastest
+      if (skip[v]) continue;
       if (++a[v] < m.vars[v].card) break;
       a[v] = 0;
     }
   }
+  // the leaf tables: F[r][y] = the clique's entry at (v = r, y's components),
+  // row M the sum over r (a missing value), row M + 1 zero (out of range)
+  std::vector<double> eall(K, 1.0);                     // prod_j F_j[missing](y)
+  for (size_t j = 0; j < lcl.size(); j++) {
+    int i = 0;
+    for (int q = 0, n = 0; q < no; q++) if (leaf[q] && n++ == (int)j) i = q;
+    const int v = P.ov[i], M = P.card[i], cl = lcl[j];
+    P.li.push_back(i);
+    P.loff.push_back((int)P.lt.size());
+    const size_t base = P.lt.size();
+    P.lt.resize(base + (size_t)(M + 2) * K, 0.0);
+    for (long y = 0; y < K; y++) {
+      std::vector<int> comp(nv, 0);
+      long r = y;
+      for (int u : cur) { comp[u] = (int)(r % m.vars[u].card); r /= m.vars[u].card; }
+      double sum = 0.0;
+      for (int val = 0; val < M; val++) {
+        long idx = 0;
+        for (const auto& e : cst[cl]) idx += (e.first == v ? val : comp[e.first]) * e.second;
+        const double f = m.cliques[cl].original[(size_t)idx];
+        P.lt[base + (size_t)val * K + y] = f;
+        sum += f;
+      }
+      P.lt[base + (size_t)M * K + y] = sum;
+      eall[y] *= sum;
+    }
+  }
   P.w.assign(K, 0.0);
   for (long x = 0; x < K; x++)
-    for (long y = 0; y < K; y++) P.w[x] += P.T[x * K + y];
+    for (long y = 0; y < K; y++) P.w[x] += P.T[x * K + y] * eall[y];
   P.pi.assign(K, 1.0);
   for (long x = 0; x < K; x++) {
     long r = x;
@@ -179,6 +255,24 @@ int upload(double** dst, const V& v) {
   if (v.size() && hipMemcpy(*dst, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
     return -1;
   return 0;
+}
+
+// the wide kernels' request fields: the full combination, the operator index
+// and the leaf factors (opchain.h OpWideArgs)
+void fill_wide(const OpPlan* P, int n_obs, OpWideArgs& w) {
+  w.nobs = n_obs;
+  for (int i = 0; i < n_obs; i++) { w.col[i] = i; w.card[i] = P->card[i]; w.cstride[i] = P->stride[i]; }
+  w.K = P->K;
+  w.ncomb = P->ncomb;
+  w.onobs = (int)P->oi.size();
+  for (int q = 0; q < w.onobs; q++) {
+    w.ocol[q] = P->oi[q]; w.ocard[q] = P->card[P->oi[q]]; w.ocstride[q] = P->ostride[q];
+  }
+  w.oncomb = P->oncomb;
+  w.nleaf = (int)P->li.size();
+  for (int j = 0; j < w.nleaf; j++) { w.lcol[j] = P->li[j]; w.lcard[j] = P->card[P->li[j]]; w.loff[j] = P->loff[j]; }
+  w.ltab = P->dlt;
+  w.Ttab = P->dT; w.w = P->dw; w.pi = P->dpi;
 }
 
 }  // namespace
@@ -214,10 +308,10 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) { err = "no device"; return NIPAMD_ERROR_DEVICE; }
   if (P->device != dev || !P->dT) {
-    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->S);
-    P->dT = P->dw = P->dpi = P->S = nullptr;
+    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->dlt); (void)hipFree(P->S);
+    P->dT = P->dw = P->dpi = P->dlt = P->S = nullptr;
     P->S_bytes = 0;
-    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi)) {
+    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi) || upload(&P->dlt, P->lt)) {
       err = "device tables";
       return NIPAMD_ERROR_DEVICE;
     }
@@ -244,11 +338,9 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
       w.obs = d_obs ? d_obs + b0 * T * ocols : nullptr;
       w.obs_bstride = (long)T * ocols;
       w.obs_tstride = (int)ocols;
-      w.nobs = n_obs;
-      for (int i = 0; i < n_obs; i++) { w.col[i] = i; w.card[i] = P->card[i]; w.cstride[i] = P->stride[i]; }
-      w.B = nb; w.T = T; w.K = P->K; w.ncomb = P->ncomb;
+      fill_wide(P, n_obs, w);
+      w.B = nb; w.T = T;
       w.filter = filt ? 1 : 0;
-      w.Ttab = P->dT; w.w = P->dw; w.pi = P->dpi;
       w.Sa = P->S;
       w.Sb = P->S + (size_t)nb * T * op_wide_np(P->K);
       w.post = d_joint ? d_joint + b0 * jbs : nullptr;
@@ -432,14 +524,99 @@ long op_estep_chunk(int K, int T) {
   return c;
 }
 
+// 17..64 states: op_wide_msgs_kernel in e_step mode stores every message and
+// scale exponent, op_wide_xi_kernel sums the xi weights per combination into
+// one slab row per 16 sequences, and the fixed-order tree reduces the rows --
+// per launch a power-of-two chunk of sequences whose messages stay within
+// ~4 GB and slab rows within ~8 GB (a row holds (ncomb + 1) K^2 + K doubles:
+// 29.6 MB at 20 states and 9261 combinations, so 256 rows fill the chip).
+int op_wide_estep(OpPlan* P, const int32_t* d_obs, int n_obs, int B, int T, double* out, double* d_ll,
+                  uint32_t* d_status, hipStream_t st, std::string& err) {
+  const int K = P->K;
+  const long R = op_xi_row(K, P->ncomb);
+  const size_t per = op_wide_scratch_bytes(K, 1, T) + (size_t)T * sizeof(int);
+  long chunk = 16;
+  while (chunk < 65536 && (size_t)(chunk * 2) * per <= ((size_t)4 << 30) &&
+         (size_t)(chunk * 2 / kOpXiSeqs) * R * sizeof(double) <= ((size_t)8 << 30))
+    chunk *= 2;
+  chunk = std::min<long>(chunk, std::max(16, B));
+  const long nchunks = (B + chunk - 1) / chunk;
+  const long rows = (chunk + kOpXiSeqs - 1) / kOpXiSeqs;
+  const long lvl = (rows + 63) / 64;
+  const size_t nsc = ((size_t)chunk * T * sizeof(int) + sizeof(double) - 1) / sizeof(double);
+  const size_t nE = nsc + (size_t)(rows + 2 * lvl + nchunks + 2 * ((nchunks + 63) / 64) + 1) * R;
+  const size_t need = op_wide_scratch_bytes(K, chunk, T);
+  if (P->S_bytes < need) {
+    (void)hipFree(P->S);
+    P->S = nullptr;
+    P->S_bytes = 0;
+    if (hipMalloc(&P->S, need) != hipSuccess) { err = "scratch"; return NIPAMD_ERROR_DEVICE; }
+    P->S_bytes = need;
+  }
+  if (P->E_bytes < nE * sizeof(double)) {
+    (void)hipFree(P->E);
+    P->E = nullptr;
+    P->E_bytes = 0;
+    if (hipMalloc(&P->E, nE * sizeof(double)) != hipSuccess) { err = "e_step buffers"; return NIPAMD_ERROR_DEVICE; }
+    P->E_bytes = nE * sizeof(double);
+  }
+  int* sc = reinterpret_cast<int*>(P->E);
+  double* slab = P->E + nsc;
+  double* work = slab + (size_t)rows * R;
+  double* cres = work + (size_t)2 * lvl * R;
+  double* cwork = cres + (size_t)nchunks * R;
+  const long ocols = n_obs > 0 ? n_obs : 1;
+  for (long c = 0; c < nchunks; c++) {
+    const long b0 = c * chunk;
+    const long nb = std::min<long>(chunk, B - b0);
+    OpWideArgs w{};
+    w.obs = d_obs ? d_obs + b0 * T * ocols : nullptr;
+    w.obs_bstride = (long)T * ocols;
+    w.obs_tstride = (int)ocols;
+    fill_wide(P, n_obs, w);
+    w.B = nb; w.T = T;
+    w.filter = 0;
+    w.Sa = P->S;
+    w.Sb = P->S + (size_t)nb * T * op_wide_np(K);
+    w.post = nullptr;
+    w.ll = d_ll ? d_ll + b0 : nullptr;
+    w.status = d_status ? d_status + b0 : nullptr;
+    w.estep = 1;
+    w.sc = sc;
+    w.slab = slab;
+    if (op_wide_launch(w, st) || op_wide_xi_launch(w, st)) {
+      err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError());
+      return NIPAMD_ERROR_DEVICE;
+    }
+    const long nr = (nb + kOpXiSeqs - 1) / kOpXiSeqs;
+    if (nipamd_tree_sum(slab, nr, (int)R, work, nchunks == 1 ? out : cres + (size_t)c * R, st)) {
+      err = "tree launch failed";
+      return NIPAMD_ERROR_DEVICE;
+    }
+  }
+  if (nchunks > 1 && nipamd_tree_sum(cres, nchunks, (int)R, cwork, out, st)) {
+    err = "tree launch failed";
+    return NIPAMD_ERROR_DEVICE;
+  }
+  g_last_kernel = "op_wide_msgs_kernel (e_step) + op_wide_xi_kernel";
+  return 0;
+}
+
 }  // namespace
 
 bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T, std::string& why) {
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
   if (!P->ok) { why = P->why; return false; }
-  if (P->K > 16) { why = "the operator chain's e_step covers joint interfaces of up to 16 states"; return false; }
-  if (!op_fits(mm, n_obs, obs_vars, T)) { why = "sequence too long for the operator chain's LDS codes"; return false; }
-  if (!op_xi_fits(P->K, P->ncomb) && !op_xi_sort_fits(P->ncomb, T)) {
+  if (P->K > 16) {
+    // op_wide_msgs_kernel + op_wide_xi_kernel: one slab row per 16 sequences
+    if ((size_t)op_xi_row(P->K, P->ncomb) * sizeof(double) > kOpMaxWideRow) {
+      why = "too many evidence combinations for the wide e_step's slab rows";
+      return false;
+    }
+  } else if (!op_fits(mm, n_obs, obs_vars, T)) {
+    why = "sequence too long for the operator chain's LDS codes";
+    return false;
+  } else if (!op_xi_fits(P->K, P->ncomb) && !op_xi_sort_fits(P->ncomb, T)) {
     why = "too many evidence combinations for the e_step's LDS sums";
     return false;
   }
@@ -483,15 +660,17 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) { err = "no device"; return NIPAMD_ERROR_DEVICE; }
   if (P->device != dev || !P->dT) {
-    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->S); (void)hipFree(P->E);
-    P->dT = P->dw = P->dpi = P->S = P->E = nullptr;
+    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->dlt); (void)hipFree(P->S);
+    (void)hipFree(P->E);
+    P->dT = P->dw = P->dpi = P->dlt = P->S = P->E = nullptr;
     P->S_bytes = P->E_bytes = 0;
-    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi)) {
+    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi) || upload(&P->dlt, P->lt)) {
       err = "device tables";
       return NIPAMD_ERROR_DEVICE;
     }
     P->device = dev;
   }
+  if (K > 16) return op_wide_estep(P, d_obs, n_obs, B, T, out, d_ll, d_status, st, err);
   const long chunk = std::min<long>(op_estep_chunk(K, T), std::max(16, B));
   const long nchunks = (B + chunk - 1) / chunk;
   const long rows = (chunk + kOpXiSeqs - 1) / kOpXiSeqs;

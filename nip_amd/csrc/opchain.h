@@ -83,25 +83,44 @@ constexpr int kOpXiSeqs = 16;
 __host__ __device__ inline int op_xi_row(int K, int ncomb) { return (ncomb + 1) * K * K + K; }
 bool op_xi_fits(int K, int ncomb);
 
-// 17 <= K <= 64 joint interface states (estep_wide.hip op_wide_*): the
-// operators stay in HBM / L2; one wave per direction holds 64 / NP
-// sequences (NP = 32 or 64 lanes each, lane = state), the step's column
-// (forward) or row (backward) of T_c read per step, the mat-vec by DPP row
-// broadcasts.  Every message is stored (alpha^_t in Sa, beta^_t in Sb), then
-// op_wide_post_kernel normalises alpha^ beta^ (or alpha^ alone, filtering)
-// into the caller's joint rows.
+// 17 <= K <= 64 joint interface states (estep_wide.hip op_wide_*): one
+// wave per direction holds 64 / NP sequences (NP = 32 or 64 lanes each, lane
+// = state), the step's column (forward) or row (backward) of its operator
+// read per step (from LDS when the operators fit, else through the caches),
+// the mat-vec by DPP row broadcasts.  Every message is stored (alpha^_t in
+// Sa, beta^_t in Sb), then op_wide_post_kernel normalises alpha^ beta^ (or
+// alpha^ alone, filtering) into the caller's joint rows.
+//
+// Leaf factorisation (opchain.cpp build): an observed variable that appears
+// in one clique only, over itself and current-interface variables, factors
+// out of the operators, T_c(x, y) = T'_{c'}(x, y) prod_j F_j[c_j](y): c' indexes
+// the other observed variables only (onobs, ocol, ...), and leaf j selects
+// row c_j of its table F_j (its state, card_j: missing = the row sum,
+// card_j + 1: out of range = 0).  The full combination c (nobs, col, ...,
+// ncomb) still keys the e_step's sums.
+constexpr int kOpMaxLeaf = 4;
 struct OpWideArgs {
   const int32_t* obs;
   long obs_bstride;
   int obs_tstride;
-  int nobs;
+  int nobs;                // the full combination (e_step keys, the ll's evidence test)
   int col[kOpMaxObs];
   int card[kOpMaxObs];
   int cstride[kOpMaxObs];
   long B;
   int T, K, ncomb;
   int filter;
-  const double* Ttab;      // [(ncomb + 1)][K][K]
+  int onobs;               // the operator index c'
+  int ocol[kOpMaxObs];
+  int ocard[kOpMaxObs];
+  int ocstride[kOpMaxObs];
+  int oncomb;              // operators: oncomb + 1 (the last all zero)
+  int nleaf;               // leaf factors
+  int lcol[kOpMaxLeaf];
+  int lcard[kOpMaxLeaf];
+  int loff[kOpMaxLeaf];    // F_j at ltab + loff[j]: [(lcard[j] + 2)][K]
+  const double* ltab;
+  const double* Ttab;      // [(oncomb + 1)][K][K]
   const double* w;         // [K]
   const double* pi;        // [K]
   double* Sa;              // [B][T][NP]
@@ -112,12 +131,20 @@ struct OpWideArgs {
   int post_off;
   double* ll;
   unsigned* status;
+  // e_step (estep = 1): the forward filter also writes every step's scale
+  // exponent sc [B][T] (alpha^_t = 2^sc_t T_{c_t}^T alpha^_{t-1}) and the
+  // e_step's BAD_LUCK status; op_wide_xi_launch then sums the steps' xi
+  // weights per evidence combination into slab rows (op_xi_kernel's layout)
+  int estep;
+  int* sc;
+  double* slab;
 };
 inline int op_wide_np(int K) { return K <= 32 ? 32 : 64; }
 inline size_t op_wide_scratch_bytes(int K, long B, int T) {
   return (size_t)2 * B * T * op_wide_np(K) * sizeof(double);
 }
 int op_wide_launch(const OpWideArgs& a, hipStream_t stream);
+int op_wide_xi_launch(const OpWideArgs& a, hipStream_t stream);
 bool op_xi_sort_fits(int ncomb, int T);
 int op_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef, double* counts,
                        hipStream_t stream);
