@@ -282,6 +282,17 @@ int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double*
                     void* stream);
 
 /*
+ * The scalars an em_learn iteration exchanges with its counts (nip_amd/em.py):
+ * d_out2[0] = nipamd_tree_sum of the n = B per-sequence log-likelihoods
+ * d_ll[B], d_out2[1] = the number of nonzero status words d_status[B] (the
+ * series nip.c:2182-2198 fails on).  Written next to the partial (d_out2 =
+ * d_partial + size), the pack needs no copy.  d_work as nipamd_tree_sum with
+ * S = 1.  Queued on stream, no synchronisation.
+ */
+int nipamd_estep_tail(const double* d_ll, const uint32_t* d_status, long B, double* d_work, double* d_out2,
+                      void* stream);
+
+/*
  * The e_step's verdict on a leading run of missing observations: the first
  * step k < T at which the reference's e_step rejects (BAD_LUCK, nip.c:1836-
  * 1840) a series that observed nothing at steps 0..k -- its running ll of pure

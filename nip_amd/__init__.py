@@ -51,7 +51,7 @@ EXPORTS = [
     "nipamd_model_original", "nipamd_model_prior", "nipamd_last_error", "nipamd_last_kernel",
     "nipamd_graph_cliques", "nipamd_estep_partial_size", "nipamd_estep_partial_size_req", "nipamd_estep_partial",
     "nipamd_estep_partial_ex",
-    "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_tree_sum", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
+    "nipamd_estep_finalize", "nipamd_estep_prefix_first_bad", "nipamd_tree_sum", "nipamd_estep_tail", "nipamd_estep_host", "nipamd_filter", "nipamd_filter_host",
     "nipamd_model_state_name", "nipamd_read_timeseries", "nipamd_series_count",
     "nipamd_series_num_observed", "nipamd_series_observed", "nipamd_series_length",
     "nipamd_series_data", "nipamd_series_free", "nipamd_write_uncertainseries",
@@ -110,6 +110,8 @@ def lib():
         L.nipamd_estep_finalize.argtypes = [vp, vp, vp, vp]
         L.nipamd_estep_prefix_first_bad.argtypes = [vp, C.c_int]
         L.nipamd_tree_sum.argtypes = [vp, C.c_long, C.c_int, vp, vp, vp]
+        if hasattr(L, "nipamd_estep_tail"):                  # (absent from A/B builds of older revisions)
+            L.nipamd_estep_tail.argtypes = [vp, vp, C.c_long, vp, vp, vp]
         L.nipamd_estep_host.argtypes = [vp, vp, C.c_int, ip, C.c_int, C.c_int, vp, vp, vp]
         L.nipamd_m_step.argtypes = [vp, dp]
         L.nipamd_model_original.argtypes = [vp, C.c_int, dp, C.c_int]
@@ -577,6 +579,23 @@ def tree_sum(rows, out=None, stream=None):
     _check(lib().nipamd_tree_sum(C.c_void_p(x.data_ptr()), n, S,
                                  C.c_void_p(work.data_ptr() if work is not None else 0),
                                  C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return out
+
+
+def estep_tail(ll, status, out=None, stream=None):
+    """out [2] = [nipamd_tree_sum of ll [B], number of nonzero status words]
+    (nipamd_estep_tail): the scalars em_learn exchanges with its counts,
+    written on the GPU next to them (em.py).  Returns out."""
+    import torch
+    B = int(ll.numel())
+    out = _out_buf(out, (2,), torch.float64, ll.device, "out")
+    if ll.dtype != torch.float64 or not ll.is_contiguous() or status.numel() != B or status.element_size() != 4 \
+            or not status.is_contiguous():
+        raise NipError(NIP_ERROR_INVALID_ARGUMENT, "ll must be contiguous float64 [B], status contiguous 32-bit [B]")
+    work = torch.empty((2 * ((B + 63) // 64),), dtype=torch.float64, device=ll.device) if B > 64 else None
+    _check(lib().nipamd_estep_tail(C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()), B,
+                                   C.c_void_p(work.data_ptr() if work is not None else 0),
+                                   C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
     return out
 
 

@@ -1070,6 +1070,26 @@ int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stre
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// out[0] = the number of nonzero status words (an exact integer as a double):
+// one block, per-thread counts, a fixed tree over the block
+__global__ __launch_bounds__(256) void count_failed_kernel(const uint32_t* status, long B, double* out) {
+  __shared__ long part[256];
+  long n = 0;
+  for (long i = threadIdx.x; i < B; i += 256) n += status[i] != 0u;
+  part[threadIdx.x] = n;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (double)part[0];
+}
+
+int count_failed_launch(const uint32_t* status, long B, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(count_failed_kernel, dim3(1), dim3(256), 0, stream, status, B, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // The e_step's verdict on a leading missing run (prefix.cpp): a sequence
 // whose observations at steps 0..first_bad are all missing (< 0) gets
 // BAD_LUCK.  One thread per sequence; almost every sequence leaves at its

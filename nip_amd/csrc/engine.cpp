@@ -1494,6 +1494,20 @@ int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double*
   return 0;
 }
 
+int nipamd_estep_tail(const double* d_ll, const uint32_t* d_status, long B, double* d_work, double* d_out2,
+                      void* stream) {
+  if (B < 0 || !d_out2 || (B > 0 && (!d_ll || !d_status)) || (B > 64 && !d_work))
+    return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
+  if (int rc = nipamd_tree_sum(d_ll, B, 1, d_work, d_out2, stream)) return rc;
+  if (B == 0) {
+    HIP_OK(hipMemsetAsync(d_out2 + 1, 0, sizeof(double), (hipStream_t)stream));
+    return 0;
+  }
+  if (nipamd::count_failed_launch(d_status, B, d_out2 + 1, (hipStream_t)stream))
+    return fail(NIPAMD_ERROR_DEVICE, "count launch failed");
+  return 0;
+}
+
 int nipamd_estep_prefix_first_bad(nipamd_model* mm, int T) {
   if (!mm || T < 1) { fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments"); return -2; }
   if (nipamd::estep_prefix_entries(mm->m) > kPrefixMaxEntries) return -2;

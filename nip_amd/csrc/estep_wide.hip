@@ -598,14 +598,48 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
   const bool est = a.estep != 0;
   int* const scrow = est ? a.sc + (size_t)bb * T : nullptr;
   // a chunk's steps: operator codes and leaf factors, a chunk ahead
-  auto prep = [&](int t, int& code, double& e) {
-    code = 0;
-    e = 1.0;
-    if (obs && t >= 0 && t < T) {
-      const int32_t* o = obs + (long)t * a.obs_tstride;
-      code = op_code(a, o);
-      if (a.nleaf) e = op_leaf_e(a, o, yc);
+  const int dir = fwd ? 1 : -1, t0 = fwd ? 0 : T - 1;
+  // a chunk's 8 steps at once (t = t0 + dir * (j + k)): each observed
+  // column's 8 loads issue together, then the leaves' table loads -- two
+  // waits per column and chunk, not a chain of dependent loads per step
+  auto prep = [&](int j, int (&code)[kMsgChunk], double (&e)[kMsgChunk]) {
+    int c[kMsgChunk];
+    bool ev[kMsgChunk], oor[kMsgChunk], in[kMsgChunk];
+    const int32_t* o[kMsgChunk];
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) {
+      const int t = t0 + dir * (j + k);
+      in[k] = obs && t >= 0 && t < T;
+      o[k] = obs + (long)(in[k] ? t : 0) * a.obs_tstride;
+      c[k] = 0; ev[k] = false; oor[k] = false; e[k] = 1.0;
     }
+    for (int q = 0; q < a.onobs; q++) {
+      const int col = a.ocol[q], card = a.ocard[q], st = a.ocstride[q];
+      int v[kMsgChunk];
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) v[k] = in[k] ? o[k][col] : -1;
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) {
+        oor[k] |= v[k] >= card;
+        ev[k] |= v[k] >= 0;
+        if (v[k] >= 0) c[k] += (v[k] + 1) * st;
+      }
+    }
+    for (int q = 0; q < a.nleaf; q++) {
+      const int col = a.lcol[q], M = a.lcard[q];
+      const double* lt = a.ltab + a.loff[q] + yc;
+      int v[kMsgChunk];
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) v[k] = in[k] ? o[k][col] : -1;
+#pragma unroll
+      for (int k = 0; k < kMsgChunk; k++) {
+        ev[k] |= v[k] >= 0;
+        const int r = v[k] < 0 ? M : (v[k] < M ? v[k] : M + 1);
+        e[k] *= in[k] ? lt[r * K] : 1.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kMsgChunk; k++) code[k] = (oor[k] ? a.oncomb : c[k]) | (ev[k] ? kOpEv : 0);
   };
   // this lane's column (forward) / row (backward) of T'_c, in 16-state blocks
   auto coef = [&](int code, double (&C)[NB][16]) {
@@ -621,9 +655,7 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
   };
   int cc[kMsgChunk], cn[kMsgChunk];
   double ec[kMsgChunk], en[kMsgChunk];
-  const int dir = fwd ? 1 : -1, t0 = fwd ? 0 : T - 1;
-#pragma unroll
-  for (int k = 0; k < kMsgChunk; k++) prep(t0 + dir * k, cc[k], ec[k]);
+  prep(0, cc, ec);
   double x;
   int sc = 0;
   double m2 = 1.0, m1 = 1.0;
@@ -642,8 +674,7 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
   // forward: steps t = 0..T-1; backward: t = T-1..1 (each making beta_{t-1})
   const int n = fwd ? T : T - 1;
   for (int j0 = 0; j0 < n; j0 += kMsgChunk) {
-#pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) prep(t0 + dir * (j0 + kMsgChunk + k), cn[k], en[k]);
+    prep(j0 + kMsgChunk, cn, en);
 #pragma unroll
     for (int k = 0; k < kMsgChunk; k++) {
       const int j = j0 + k;
@@ -712,24 +743,29 @@ __global__ __launch_bounds__(256) void op_wide_post_kernel(OpWideArgs a) {
 
 // The operator chain's e_step at 17..64 states: op_xi_sort_kernel's sums
 // (opchain.hip) from the stored messages.  Step t's xi weights are
-//   W_t(x, y) = alpha^_{t-1}(x) beta^_t(y) f_t,  f_t = 2^sc_t / sum_y alpha^_t(y) beta^_t(y)
-// (alpha^_t = 2^sc_t T_{c_t}^T alpha^_{t-1}, so f_t = 1 / Z'_t, the step's xi
-// mass; alpha^_{-1} = the prior), the same products as op_fb_kernel's xi_row.
-// A block owns 16 sequences and one slab row: Xi_c [K][K] for every
-// combination c, then P0 [K].  The group's steps (sequence-major; at most
-// kXwTileMax at a time, the whole group when T <= 1024) are sorted by
-// (combination, position) in LDS -- a bitonic sort of packed keys, so every
-// combination's steps keep their stream order -- then staged kXwBatch at a
-// time (the weights' two vectors per step in LDS, f_t by a wave sum) and
-// summed by a thread per cell, CPT cells each, in sorted order: a fixed
-// summation order, independent of the launch (shard invariance).  A
-// combination's sum leaves for the slab row when the sorted stream moves on:
-// a plain store in the first tile (each combination once; the row was zeroed
-// by the same thread before), read-add-write in later ones.
+//   W_t(x, y) = alpha^_{t-1}(x) e_t(y) beta^_t(y) f_t,  f_t = 2^sc_t / sum_y alpha^_t(y) beta^_t(y)
+// (alpha^_t = 2^sc_t e_t o T'^T alpha^_{t-1}, so f_t = 1 / Z'_t, the step's xi
+// mass; alpha^_{-1} = the prior; e_t the leaf factors, 1 without leaves), the
+// same products as op_fb_kernel's xi_row.  They are summed per operator index
+// c' (Xi'); each leaf's count rows sum the interface posterior gamma_t(y) =
+// alpha^_t beta^_t / sum by the leaf's code at t.
+// A block owns 16 sequences and one slab row (opchain.h).  The group's steps
+// (sequence-major; at most kXwTileMax at a time, the whole group when T <=
+// 1024) are sorted by (key, position) in LDS -- a bitonic sort of packed
+// keys, so every key's steps keep their stream order -- then staged kXwBatch
+// at a time (the weights' two vectors and gamma per step in LDS, f_t by a
+// wave sum) and summed in sorted order: Xi' by a thread per cell (CPT cells
+// each), the leaf rows by a thread per state y.  A fixed summation order,
+// independent of the launch (shard invariance).  An operator index's Xi' sum
+// leaves for the slab row when the sorted stream moves on: a plain store in
+// the first tile (each index once; the row was zeroed by the same thread
+// before), read-add-write in later ones; a key's gamma sum is added to its
+// leaf rows in LDS, written out at the end.
 constexpr int kXwTileBits = 14;
 constexpr int kXwTileMax = 1 << kXwTileBits;   // steps per sorted tile (the key's low bits)
 constexpr int kXwBatch = 32;                 // sorted steps staged per pass (8 per wave)
 constexpr int kXwThreads = 256;
+static_assert(kXwTileBits + kOpWideKeyBits <= 32, "packed sort key");
 
 // the sorted tile's length: the group's stream rounded up to a power of two
 __host__ __device__ inline int op_xi_tile(int T) {
@@ -739,20 +775,36 @@ __host__ __device__ inline int op_xi_tile(int T) {
   return L;
 }
 
+// a step's sort key c' * Lr + sum_j code_j lrad_j (code: state, M missing,
+// M + 1 out of range) and its leaf codes packed a byte each
+__device__ __forceinline__ int op_key(const OpWideArgs& a, const int32_t* o, unsigned& lc) {
+  int k = (op_code(a, o) & (kOpEv - 1)) * a.Lr;
+  lc = 0;
+  for (int j = 0; j < a.nleaf; j++) {
+    const int v = o[a.lcol[j]], M = a.lcard[j];
+    const int r = v < 0 ? M : (v < M ? v : M + 1);
+    k += r * a.lrad[j];
+    lc |= (unsigned)r << (8 * j);
+  }
+  return k;
+}
+
 template <int NP, int CPT>
 __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned key[];   // [op_xi_tile(T)]
-  __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP];
+  __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP], Gm[kXwBatch][NP];
   __shared__ int kb[kXwBatch];
+  __shared__ unsigned lb[kXwBatch];
   __shared__ double p0s[kOpXiSeqs][64];
+  __shared__ double Hl[kOpWideMaxH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = a.K, KK = K * K, T = a.T;
   const int L = op_xi_tile(T);
   const long b0 = (long)blockIdx.x * kOpXiSeqs;
   const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
   const long n = (long)nseq * T;
-  const size_t R = (size_t)op_xi_row(K, a.ncomb);
-  double* const out = a.slab + (size_t)blockIdx.x * R;
+  double* const out = a.slab + (size_t)blockIdx.x * a.xrow;
+  const int hsize = a.xrow - K - (a.oncomb + 1) * KK;
   int cx[CPT], cy[CPT];
   bool con[CPT];
 #pragma unroll
@@ -762,17 +814,23 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     cx[k] = con[k] ? cell / K : 0;
     cy[k] = con[k] ? cell - cx[k] * K : 0;
   }
-  // the row's Xi part zeroed by the threads that own the cells (each cell is
-  // later written, or read and written, by the same thread only)
-  for (int c = 0; c <= a.ncomb; c++)
+  // the row's Xi' part zeroed by the threads that own the cells (each cell is
+  // later written, or read and written, by the same thread only); the leaf
+  // rows in LDS by their column's thread
+  for (int c = 0; c <= a.oncomb; c++)
 #pragma unroll
     for (int k = 0; k < CPT; k++)
       if (con[k]) out[(size_t)c * KK + tid + kXwThreads * k] = 0.0;
+  const bool hy = tid < K;                            // this thread: column y = tid of the leaf rows
+  if (hy)
+    for (int i = tid; i < hsize; i += K) Hl[i] = 0.0;
 
   double acc[CPT];
 #pragma unroll
   for (int k = 0; k < CPT; k++) acc[k] = 0.0;
-  int cur = -1;
+  double hacc = 0.0;
+  int cur = -1, curk = -1;
+  unsigned curl = 0;
   auto flush = [&](bool first) {
     if (cur >= 0) {
 #pragma unroll
@@ -785,6 +843,12 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     for (int k = 0; k < CPT; k++) acc[k] = 0.0;
     cur = -1;
   };
+  auto flush_h = [&] {
+    if (hy && curk >= 0)
+      for (int j = 0; j < a.nleaf; j++) Hl[a.hoff[j] - (a.oncomb + 1) * KK + (int)((curl >> (8 * j)) & 0xff) * K + tid] += hacc;
+    hacc = 0.0;
+    curk = -1;
+  };
   constexpr int SPW = 64 / NP;
   const int y = lane % NP;
   const bool ys = y < K;
@@ -795,7 +859,8 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
       if (i < m) {
         const long g = i0 + i;
         const long s = g / T, t = g - s * T;
-        const int c = a.obs ? op_comb(a, a.obs + (b0 + s) * a.obs_bstride + t * a.obs_tstride) : 0;
+        unsigned lc;
+        const int c = a.obs ? op_key(a, a.obs + (b0 + s) * a.obs_bstride + t * a.obs_tstride, lc) : 0;
         v = ((unsigned)c << kXwTileBits) | (unsigned)i;
       }
       key[i] = v;
@@ -827,26 +892,49 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
         const bool on = ok && ys;
         const double at = on ? sa[0] : 0.0, bt = on ? sb[0] : 0.0;
         const double ap = on ? (t > 0 ? sa[-NP] : a.pi[y]) : 0.0;
-        const double z = group_sum<NP>(at * bt);
+        const double pr = at * bt;
+        const double z = group_sum<NP>(pr);
         const int sc = ok ? a.sc[(size_t)b * T + t] : 0;
         const double f = z != 0.0 ? __builtin_ldexp(1.0 / z, sc) : 0.0;
+        // the leaf codes from the sort key (no observation re-read), their
+        // factors as op_leaf_e multiplies them
+        double e = 1.0;
+        unsigned lc = 0;
+        const int kc = (int)(v >> kXwTileBits);
+        for (int q2 = 0; q2 < a.nleaf; q2++) {
+          const int r = (kc / a.lrad[q2]) % (a.lcard[q2] + 2);
+          lc |= (unsigned)r << (8 * q2);
+          e *= a.ltab[a.loff[q2] + r * K + (ys ? y : 0)];
+        }
         Ab[jj][y] = ap;
-        Gb[jj][y] = bt * f;
-        if (y == 0) kb[jj] = ok ? (int)(v >> kXwTileBits) : -1;
+        Gb[jj][y] = bt * e * f;
+        Gm[jj][y] = z != 0.0 ? pr / z : 0.0;
+        if (y == 0) {
+          kb[jj] = ok ? (int)(v >> kXwTileBits) : -1;
+          lb[jj] = lc;
+        }
       }
       __syncthreads();
       const int nj = (m - j0) < kXwBatch ? (m - j0) : kXwBatch;
       for (int jj = 0; jj < nj; jj++) {
-        const int c = kb[jj];
+        const int kc = kb[jj];
+        if (kc != curk) {
+          flush_h();
+          curk = kc;
+          curl = lb[jj];
+        }
+        const int c = kc / a.Lr;
         if (c != cur) { flush(i0 == 0); cur = c; }
 #pragma unroll
         for (int k = 0; k < CPT; k++) acc[k] = __builtin_fma(Ab[jj][cx[k]], Gb[jj][cy[k]], acc[k]);
+        if (hy) hacc += Gm[jj][tid];
       }
       __syncthreads();
     }
     flush(i0 == 0);
+    flush_h();
   }
-  // P0 per sequence: normalise(prior o T_{c_0} beta^_0), as op_fb_kernel's
+  // P0 per sequence: normalise(prior o T_{c_0} (e_0 o beta^_0)), as op_fb_kernel's
   // extra backward step; then summed over the group in sequence order
   for (int s = wave; s < nseq; s += 4) {
     const long b = b0 + s;
@@ -864,10 +952,11 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     p0s[s][lane] = z != 0.0 ? pr / z : pr;
   }
   __syncthreads();
-  if (tid < K) {
+  if (hy) {
     double p = 0.0;
     for (int s = 0; s < nseq; s++) p += p0s[s][tid];
-    out[(size_t)(a.ncomb + 1) * KK + tid] = p;
+    out[a.xrow - K + tid] = p;
+    for (int i = tid; i < hsize; i += K) out[(size_t)(a.oncomb + 1) * KK + i] = Hl[i];
   }
 }
 
@@ -915,7 +1004,9 @@ int xi_launch(const OpWideArgs& a, hipStream_t stream) {
 
 int op_wide_xi_launch(const OpWideArgs& a, hipStream_t stream) {
   if (a.B <= 0) return 0;
-  if (a.K > 64 || a.K < 17 || a.ncomb > 65534 || !a.sc || !a.slab) return -2;
+  if (a.K > 64 || a.K < 17 || a.oncomb > 65534 || !a.sc || !a.slab || a.Lr < 1 ||
+      (long)(a.oncomb + 1) * a.Lr >= (1L << kOpWideKeyBits) || a.xrow - a.K - (a.oncomb + 1) * a.K * a.K > kOpWideMaxH)
+    return -2;
   const int KK = a.K * a.K;
   if (KK <= 2 * kXwThreads) return xi_launch<32, 2>(a, stream);
   if (KK <= 4 * kXwThreads) return xi_launch<32, 4>(a, stream);

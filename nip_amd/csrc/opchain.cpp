@@ -48,6 +48,12 @@ struct OpPlan {
   int oncomb = 0;
   std::vector<int> oi, ostride;      // positions in ov, radix
   std::vector<int> li, loff;         // positions in ov, offsets into lt
+  std::vector<int> lcl;              // the leaves' cliques
+  // the e_step's slab row (opchain.h OpWideArgs): sort-key radix, leaf count
+  // rows' offsets, row size
+  int Lr = 1;
+  std::vector<int> lrad, hoff;
+  long xrow = 0;
   std::vector<double> lt;
   std::vector<double> T, w, pi;      // T: [(oncomb + 1)][K][K]
   double* dT = nullptr;
@@ -118,10 +124,14 @@ bool build(const Model& m, OpPlan& P) {
   // T_c = T'_{c'} diag(prod F) -- c' over the other observed variables.
   std::vector<char> leaf(no, 0);
   std::vector<int> lcl;
+  // (the e_step's limits: leaf codes a byte each, the leaf count rows within
+  // kOpWideMaxH doubles, sort keys below 2^kOpWideKeyBits)
+  long hsz = 0;
   if (K > 16)
     for (int i = 0; i < no && (int)lcl.size() < kOpMaxLeaf; i++) {
       const int v = P.ov[i];
-      if (has(cur, v) || has(prev, v) || has(pri, v)) continue;
+      if (has(cur, v) || has(prev, v) || has(pri, v) || P.card[i] + 2 > 255) continue;
+      if (hsz + (long)(P.card[i] + 2) * K > kOpWideMaxH) continue;
       int cl = -1, nc = 0;
       for (size_t c = 0; c < m.cliques.size(); c++)
         if (has(m.cliques[c].vars, v)) { cl = (int)c; nc++; }
@@ -131,7 +141,19 @@ bool build(const Model& m, OpPlan& P) {
       if (!ok) continue;
       leaf[i] = 1;
       lcl.push_back(cl);
+      hsz += (long)(P.card[i] + 2) * K;
     }
+  // the sort key c' * Lr + leaf codes must fit: drop leaves from the back
+  for (;;) {
+    long oc = 1, lr = 1;
+    for (int i = 0; i < no; i++) {
+      if (leaf[i]) lr *= P.card[i] + 2;
+      else oc *= P.card[i] + 1;
+    }
+    if ((oc + 1) * lr < (1L << kOpWideKeyBits) || lcl.empty()) break;
+    for (int i = no - 1; i >= 0; i--)
+      if (leaf[i]) { leaf[i] = 0; lcl.pop_back(); break; }
+  }
   long oncomb = 1;
   for (int i = 0; i < no; i++)
     if (!leaf[i]) {
@@ -143,6 +165,7 @@ bool build(const Model& m, OpPlan& P) {
     P.why = "too many evidence combinations";
     return false;
   }
+  P.lcl = lcl;
   std::vector<char> skip(nv, 0);                        // leaf variables: not enumerated
   for (int i = 0; i < no; i++) if (leaf[i]) skip[P.ov[i]] = 1;
   long total = 1;
@@ -222,6 +245,15 @@ bool build(const Model& m, OpPlan& P) {
       eall[y] *= sum;
     }
   }
+  P.Lr = 1;
+  P.xrow = (long)(oncomb + 1) * K * K;
+  for (size_t j = 0; j < P.li.size(); j++) {
+    P.lrad.push_back(P.Lr);
+    P.Lr *= P.card[P.li[j]] + 2;
+    P.hoff.push_back((int)P.xrow);
+    P.xrow += (long)(P.card[P.li[j]] + 2) * K;
+  }
+  P.xrow += K;
   P.w.assign(K, 0.0);
   for (long x = 0; x < K; x++)
     for (long y = 0; y < K; y++) P.w[x] += P.T[x * K + y] * eall[y];
@@ -273,6 +305,9 @@ void fill_wide(const OpPlan* P, int n_obs, OpWideArgs& w) {
   for (int j = 0; j < w.nleaf; j++) { w.lcol[j] = P->li[j]; w.lcard[j] = P->card[P->li[j]]; w.loff[j] = P->loff[j]; }
   w.ltab = P->dlt;
   w.Ttab = P->dT; w.w = P->dw; w.pi = P->dpi;
+  w.Lr = P->Lr;
+  for (int j = 0; j < w.nleaf; j++) { w.lrad[j] = P->lrad[j]; w.hoff[j] = P->hoff[j]; }
+  w.xrow = (int)P->xrow;
 }
 
 }  // namespace
@@ -442,16 +477,32 @@ bool build_map(const Model& m, OpPlan& P) {
   std::vector<int> pri;
   for (int v : m.independent)
     if (m.vars[v].has_prior && !(m.vars[v].ifs & IF_OLD_OUTGOING)) pri.push_back(v);
-  std::vector<int> cnt;                               // the counted variables (every step)
+  // the leaf factors (K > 16, build()): their variables are not enumerated
+  // and their cliques leave the product; a counted variable whose family holds
+  // a leaf takes its counts from that leaf's count rows instead of Xi'
+  std::vector<char> skip(nv, 0), lc(m.cliques.size(), 0);
+  for (int i : P.li) skip[P.ov[i]] = 1;
+  for (int c : P.lcl) lc[c] = 1;
+  auto leaf_of = [&](int v) {                         // the leaf in v's family, -1: none
+    for (size_t j = 0; j < P.li.size(); j++) {
+      const int l = P.ov[P.li[j]];
+      if (v == l || has(m.vars[v].parents, l)) return (int)j;
+    }
+    return -1;
+  };
+  std::vector<int> cnt;                               // the counted variables (every step), via Xi'
   for (int v = 0; v < nv; v++)
-    if (!(m.vars[v].ifs & IF_OLD_OUTGOING)) cnt.push_back(v);
+    if (!(m.vars[v].ifs & IF_OLD_OUTGOING) && leaf_of(v) < 0) cnt.push_back(v);
   long total = 1;
-  for (const Var& V : m.vars) total *= V.card;
+  for (int v = 0; v < nv; v++)
+    if (!skip[v]) total *= m.vars[v].card;
+  const int nop = (int)P.oi.size();
   std::vector<int> a(nv, 0);
   const long KK = (long)K * K;
   for (long it = 0; it < total; it++) {
     double W = 1.0;                                   // the same product, in the same order, as build()
     for (size_t c = 0; c < m.cliques.size() && W != 0.0; c++) {
+      if (lc[c]) continue;
       long idx = 0;
       for (const auto& e : cst[c]) idx += a[e.first] * e.second;
       W *= m.cliques[c].original[(size_t)idx];
@@ -463,10 +514,10 @@ bool build_map(const Model& m, OpPlan& P) {
         x += a[prev[i]] * sx; sx *= m.vars[prev[i]].card;
         y += a[cur[i]] * sy; sy *= m.vars[cur[i]].card;
       }
-      for (long mask = 0; mask < (1L << no); mask++) {
+      for (long mask = 0; mask < (1L << nop); mask++) {
         long c = 0;
-        for (int i = 0; i < no; i++)
-          if (mask >> i & 1) c += (long)(a[P.ov[i]] + 1) * P.stride[i];
+        for (int q = 0; q < nop; q++)
+          if (mask >> q & 1) c += (long)(a[P.ov[P.oi[q]]] + 1) * P.ostride[q];
         const int idx = (int)(c * KK + x * K + y);
         for (int v : cnt) {
           long cell = a[v], st = m.vars[v].card;
@@ -477,12 +528,36 @@ bool build_map(const Model& m, OpPlan& P) {
       }
     }
     for (int v = 0; v < nv; v++) {                    // odometer, variable 0 fastest
+      if (skip[v]) continue;
       if (++a[v] < m.vars[v].card) break;
       a[v] = 0;
     }
   }
+  // families holding leaf j: sum_t gamma_t(y) P(leaf = r | y, its code at t)
+  // -- the count row of code r (observed r), plus the missing row times
+  // F_j[r](y) / F_j[missing](y)
+  for (size_t j = 0; j < P.li.size(); j++) {
+    const int l = P.ov[P.li[j]], M = P.card[P.li[j]];
+    const double* F = P.lt.data() + P.loff[j];
+    for (int v = 0; v < nv; v++) {
+      if ((m.vars[v].ifs & IF_OLD_OUTGOING) || leaf_of(v) != (int)j) continue;
+      for (long y = 0; y < K; y++) {
+        std::vector<int> comp(nv, 0);
+        long r = y;
+        for (int u : cur) { comp[u] = (int)(r % m.vars[u].card); r /= m.vars[u].card; }
+        for (int val = 0; val < M; val++) {
+          comp[l] = val;
+          long cell = comp[v], st = m.vars[v].card;
+          for (int q : m.vars[v].parents) { cell += (long)comp[q] * st; st *= m.vars[q].card; }
+          ents.push_back({off[v] + cell, (int)(P.hoff[j] + (long)val * K + y), 1.0});
+          const double miss = F[(size_t)M * K + y];
+          if (miss != 0.0) ents.push_back({off[v] + cell, (int)(P.hoff[j] + (long)M * K + y), F[(size_t)val * K + y] / miss});
+        }
+      }
+    }
+  }
   // the previous interface at t = 0: P0 digits
-  const int p0 = (int)((P.ncomb + 1) * KK);
+  const int p0 = (int)(P.xrow - K);
   for (int x = 0; x < K; x++) {
     long r = x;
     for (int v : prev) {
@@ -533,7 +608,7 @@ long op_estep_chunk(int K, int T) {
 int op_wide_estep(OpPlan* P, const int32_t* d_obs, int n_obs, int B, int T, double* out, double* d_ll,
                   uint32_t* d_status, hipStream_t st, std::string& err) {
   const int K = P->K;
-  const long R = op_xi_row(K, P->ncomb);
+  const long R = P->xrow;
   const size_t per = op_wide_scratch_bytes(K, 1, T) + (size_t)T * sizeof(int);
   long chunk = 16;
   while (chunk < 65536 && (size_t)(chunk * 2) * per <= ((size_t)4 << 30) &&
@@ -609,7 +684,7 @@ bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T,
   if (!P->ok) { why = P->why; return false; }
   if (P->K > 16) {
     // op_wide_msgs_kernel + op_wide_xi_kernel: one slab row per 16 sequences
-    if ((size_t)op_xi_row(P->K, P->ncomb) * sizeof(double) > kOpMaxWideRow) {
+    if ((size_t)P->xrow * sizeof(double) > kOpMaxWideRow) {
       why = "too many evidence combinations for the wide e_step's slab rows";
       return false;
     }
@@ -631,7 +706,7 @@ bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T,
 long op_estep_section(nipamd_model* mm, int n_obs, const int* obs_vars) {
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
   if (!P->ok) return 0;
-  return kOpHdr + op_xi_row(P->K, P->ncomb);
+  return kOpHdr + P->xrow;
 }
 
 int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars, int B, int T,
@@ -639,7 +714,7 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
   if (!P->ok) { err = P->why; return NIPAMD_ERROR_UNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
-  const int K = P->K, R = op_xi_row(K, P->ncomb);
+  const int K = P->K, R = (int)P->xrow;
   // the header (pageable host source: staged before the call returns)
   double hdr[kOpHdr];
   hdr[0] = 1.0;

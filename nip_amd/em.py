@@ -21,6 +21,8 @@ to the single-GPU run.  That all-gather (partial_size + 2 doubles per rank,
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 MIN_EM_ITERATIONS = 3          # src/nip.c:29
@@ -92,17 +94,48 @@ class GpuEStep:
         from . import estep_finalize
         return estep_finalize(model, partial, counts)
 
+    def packed(self, model, obs, obs_vars):
+        """The e_step partial written straight into the exchange buffer
+        [partial | ll tree sum | failed series] (nipamd_estep_tail fills the
+        two scalars on the GPU): no pack kernels, no host round trip before the
+        collective.  Returns (packed, partial size)."""
+        import torch
+        from . import _ints, _obs3, estep_partial, estep_tail, lib
+        o = _obs3(obs, obs_vars)
+        S = lib().nipamd_estep_partial_size_req(model._h, int(o.shape[2]), _ints(obs_vars), int(o.shape[1]))
+        buf = torch.empty((S + 2,), dtype=torch.float64, device=obs.device)
+        _, ll, status = estep_partial(model, o, obs_vars, partial=buf[:S])
+        estep_tail(ll, status, out=buf[S:])
+        return buf, S
+
 
 def iteration(model, params, obs, obs_vars, group=None, backend=None, timing=None):
     """One em_learn iteration (src/nip.c:2154-2207): m_step(params), e_step
     of this rank's shard with pseudo-counts 1.0, the one exchange, finalize.
     Returns (new params (host), global ll, number of failed sequences).
-    ``timing``: optional dict; 'exchange_ms' receives the collective's time."""
+    ``timing``: optional dict; 'exchange_ms' receives the collective's time
+    (events on the stream: no synchronisation inside the iteration)."""
     import time
     import torch
     be = backend or GpuEStep()
     P = model.param_size()
     model.m_step(params)                          # nip.c:2154
+    if isinstance(be, GpuEStep) and obs.is_cuda and os.environ.get("NIPAMD_EM_PACKED", "1") != "0":
+        # the product path: one buffer from the e_step to the finalize, and
+        # one device-to-host synchronisation per iteration (the counts)
+        packed, S = be.packed(model, obs, obs_vars)
+        if timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        comb = combine_partials(packed, group)
+        if timing is not None:
+            e1.record()
+        counts = be.finalize(model, comb[:S], None)   # pseudo-counts 1.0 (nip.c:2172) + the families
+        host = counts.cpu().numpy()
+        tail = comb[S:].cpu()
+        if timing is not None:
+            timing["exchange_ms"] = e0.elapsed_time(e1)
+        return host, float(tail[0]), int(round(float(tail[1])))
     counts = torch.ones((P,), dtype=torch.float64, device=obs.device)   # nip.c:2172
     partial, ll, status = be.partial(model, obs, obs_vars)
     if timing is not None and obs.is_cuda:

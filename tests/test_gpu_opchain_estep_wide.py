@@ -84,6 +84,28 @@ def test_wide_op_estep_many_combinations_and_tiles():
     assert np.array_equal(a[2], b[2])
 
 
+def test_wide_op_estep_two_leaf_factors():
+    """A1 and B1 observed with D1 (the estep_opchain_wide request): both
+    children are leaf factors of the operators, so the sums are keyed by D1's
+    22 operator indices and A1's / B1's counts come from their count rows
+    (gamma by code, the missing row weighted by the table) -- against the
+    general engine and the oracle."""
+    m, ov, obs = demo1_20(30, 21, seed=8, names=("A1", "B1", "D1"))
+    obs[5, 7, 1] = m.card(ov[1])                     # an out-of-range leaf state: a zero-mass series
+    a = estep(m, obs, ov)
+    assert a[3] == WIDE, a[3]
+    b = estep(m, obs, ov, nip_amd.ENGINE_JTREE)
+    assert close_cnt(a[0], b[0]), np.abs(a[0] - b[0]).max()
+    assert close_ll(a[1], b[1])
+    assert np.array_equal(a[2], b[2]) and a[2][5] == 3
+    # the oracle on live series (its e_step stops counting at a failed one)
+    rc, rl, rb = PortOracle(m.desc()).estep(obs[:5], ov, np.ones(m.param_size()))
+    c5, l5, s5, _ = estep(m, obs[:5], ov)
+    assert np.array_equal(s5 != 0, rb != 0)
+    assert close_ll(l5, rl)
+    assert close_cnt(c5, rc), np.abs(c5 - rc).max()
+
+
 def test_wide_op_estep_vs_oracle():
     m, ov, obs = demo1_20(20, 12, seed=4)
     c, ll, st, k = estep(m, obs, ov)
