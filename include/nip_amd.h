@@ -286,8 +286,9 @@ int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double*
  * d_out2[0] = nipamd_tree_sum of the n = B per-sequence log-likelihoods
  * d_ll[B], d_out2[1] = the number of nonzero status words d_status[B] (the
  * series nip.c:2182-2198 fails on).  Written next to the partial (d_out2 =
- * d_partial + size), the pack needs no copy.  d_work as nipamd_tree_sum with
- * S = 1.  Queued on stream, no synchronisation.
+ * d_partial + size), the pack needs no copy.  d_work: at least
+ * 2 * ceil(B / 64) + ceil(B / 4096) doubles of device workspace (B > 0).
+ * Queued on stream, no synchronisation.
  */
 int nipamd_estep_tail(const double* d_ll, const uint32_t* d_status, long B, double* d_work, double* d_out2,
                       void* stream);

@@ -592,10 +592,9 @@ def estep_tail(ll, status, out=None, stream=None):
     if ll.dtype != torch.float64 or not ll.is_contiguous() or status.numel() != B or status.element_size() != 4 \
             or not status.is_contiguous():
         raise NipError(NIP_ERROR_INVALID_ARGUMENT, "ll must be contiguous float64 [B], status contiguous 32-bit [B]")
-    work = torch.empty((2 * ((B + 63) // 64),), dtype=torch.float64, device=ll.device) if B > 64 else None
+    work = torch.empty((2 * ((B + 63) // 64) + (B + 4095) // 4096 + 1,), dtype=torch.float64, device=ll.device)
     _check(lib().nipamd_estep_tail(C.c_void_p(ll.data_ptr()), C.c_void_p(status.data_ptr()), B,
-                                   C.c_void_p(work.data_ptr() if work is not None else 0),
-                                   C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+                                   C.c_void_p(work.data_ptr()), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
     return out
 
 

@@ -334,7 +334,9 @@ int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
 // the e_step partial's route tag: tag[0] = a, tag[1] = b, tag[2] = c
 int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stream);
-int count_failed_launch(const uint32_t* status, long B, double* out, hipStream_t stream);
+// nonzero status words -> out[0]; work: count_failed_work(B) doubles
+long count_failed_work(long B);
+int count_failed_launch(const uint32_t* status, long B, double* work, double* out, hipStream_t stream);
 // BAD_LUCK for sequences missing every observation at steps 0..first_bad (prefix.cpp)
 // trivial: bit c set when column c observes a one-state variable (no evidence)
 int estep_prefix_flag_launch(const int32_t* obs, int n_obs, int B, int T, int first_bad, unsigned trivial,

@@ -1071,22 +1071,46 @@ int estep_tag_launch(double* tag, double a, double b, double c, hipStream_t stre
 }
 
 // out[0] = the number of nonzero status words (an exact integer as a double):
-// one block, per-thread counts, a fixed tree over the block
-__global__ __launch_bounds__(256) void count_failed_kernel(const uint32_t* status, long B, double* out) {
-  __shared__ long part[256];
-  long n = 0;
-  for (long i = threadIdx.x; i < B; i += 256) n += status[i] != 0u;
-  part[threadIdx.x] = n;
+// blocks of 4096 words (16 independent loads per thread) count into part[],
+// then one block adds the parts; integer sums, so the order does not matter
+constexpr int kCountPer = 4096;
+__global__ __launch_bounds__(256) void count_failed_kernel(const uint32_t* status, long B, double* part) {
+  __shared__ int red[256];
+  const long base = (long)blockIdx.x * kCountPer;
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < kCountPer / 256; k++) {
+    const long i = base + k * 256 + threadIdx.x;
+    n += (i < B && status[i] != 0u) ? 1 : 0;
+  }
+  red[threadIdx.x] = n;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = (double)part[0];
+  if (threadIdx.x == 0) part[blockIdx.x] = (double)red[0];
 }
 
-int count_failed_launch(const uint32_t* status, long B, double* out, hipStream_t stream) {
-  hipLaunchKernelGGL(count_failed_kernel, dim3(1), dim3(256), 0, stream, status, B, out);
+__global__ __launch_bounds__(256) void count_sum_kernel(const double* part, long n, double* out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+long count_failed_work(long B) { return (B + kCountPer - 1) / kCountPer; }
+
+int count_failed_launch(const uint32_t* status, long B, double* work, double* out, hipStream_t stream) {
+  const long nb = count_failed_work(B);
+  hipLaunchKernelGGL(count_failed_kernel, dim3((unsigned)nb), dim3(256), 0, stream, status, B, work);
+  hipLaunchKernelGGL(count_sum_kernel, dim3(1), dim3(256), 0, stream, work, nb, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

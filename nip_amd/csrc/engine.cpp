@@ -1496,14 +1496,16 @@ int nipamd_tree_sum(const double* d_rows, long n, int S, double* d_work, double*
 
 int nipamd_estep_tail(const double* d_ll, const uint32_t* d_status, long B, double* d_work, double* d_out2,
                       void* stream) {
-  if (B < 0 || !d_out2 || (B > 0 && (!d_ll || !d_status)) || (B > 64 && !d_work))
+  if (B < 0 || !d_out2 || (B > 0 && (!d_ll || !d_status || !d_work)))
     return fail(NIP_ERROR_INVALID_ARGUMENT, "bad arguments");
   if (int rc = nipamd_tree_sum(d_ll, B, 1, d_work, d_out2, stream)) return rc;
   if (B == 0) {
     HIP_OK(hipMemsetAsync(d_out2 + 1, 0, sizeof(double), (hipStream_t)stream));
     return 0;
   }
-  if (nipamd::count_failed_launch(d_status, B, d_out2 + 1, (hipStream_t)stream))
+  // the count's block parts after the tree's levels in the workspace
+  double* cw = d_work + (B > 64 ? 2 * ((B + 63) / 64) : 0);
+  if (nipamd::count_failed_launch(d_status, B, cw, d_out2 + 1, (hipStream_t)stream))
     return fail(NIPAMD_ERROR_DEVICE, "count launch failed");
   return 0;
 }

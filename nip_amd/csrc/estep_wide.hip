@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdint>
+#include <type_traits>
 
 #include "chain_kernels.h"
 #include "dpp_row.h"
@@ -534,18 +535,6 @@ int stats_launch(const EWideArgs& a, hipStream_t stream) {
 //   forward:  alpha_t = e_t o T'^T alpha_{t-1}  (alpha_{-1} = prior), stored
 //   backward: beta_{t-1} = T' (e_t o beta_t)   (beta_{T-1} = 1), stored
 //   ll = sum over steps with evidence of log m2_t - log m1_t (nip.c:1458-1474)
-// A step's evidence combination (opchain.h): each observed variable missing or
-// one of its states; an out-of-range state selects the all-zero operator ncomb.
-__device__ __forceinline__ int op_comb(const OpWideArgs& a, const int32_t* o) {
-  int c = 0;
-  for (int k = 0; k < a.nobs; k++) {
-    const int v = o[a.col[k]];
-    if (v >= a.card[k]) return a.ncomb;
-    if (v >= 0) c += (v + 1) * a.cstride[k];
-  }
-  return c;
-}
-
 // the step's operator index c' | (the step has evidence) << 30
 constexpr int kOpEv = 1 << 30;
 __device__ __forceinline__ int op_code(const OpWideArgs& a, const int32_t* o) {
@@ -761,10 +750,14 @@ __global__ __launch_bounds__(256) void op_wide_post_kernel(OpWideArgs a) {
 // the first tile (each index once; the row was zeroed by the same thread
 // before), read-add-write in later ones; a key's gamma sum is added to its
 // leaf rows in LDS, written out at the end.
+#ifndef NIPAMD_XI_SKIP
+#define NIPAMD_XI_SKIP 0   // timing-only builds (wrong results): 1 no sort, 2 no sums, 3 no message loads, 4 no keys
+#endif
 constexpr int kXwTileBits = 14;
 constexpr int kXwTileMax = 1 << kXwTileBits;   // steps per sorted tile (the key's low bits)
-constexpr int kXwBatch = 32;                 // sorted steps staged per pass (8 per wave)
-constexpr int kXwThreads = 256;
+constexpr int kXwBatch = 32;                 // sorted steps staged per pass (4 per wave)
+constexpr int kXwThreads = 512;
+constexpr int kXwWaves = kXwThreads / 64;
 static_assert(kXwTileBits + kOpWideKeyBits <= 32, "packed sort key");
 
 // the sorted tile's length: the group's stream rounded up to a power of two
@@ -775,98 +768,135 @@ __host__ __device__ inline int op_xi_tile(int T) {
   return L;
 }
 
-// a step's sort key c' * Lr + sum_j code_j lrad_j (code: state, M missing,
-// M + 1 out of range) and its leaf codes packed a byte each
-__device__ __forceinline__ int op_key(const OpWideArgs& a, const int32_t* o, unsigned& lc) {
-  int k = (op_code(a, o) & (kOpEv - 1)) * a.Lr;
-  lc = 0;
+// a step's sort key c' << Lbits | code_j << lsh[j] (code: state, M missing,
+// M + 1 out of range)
+__device__ __forceinline__ int op_key(const OpWideArgs& a, const int32_t* o) {
+  int k = (op_code(a, o) & (kOpEv - 1)) << a.Lbits;
   for (int j = 0; j < a.nleaf; j++) {
     const int v = o[a.lcol[j]], M = a.lcard[j];
-    const int r = v < 0 ? M : (v < M ? v : M + 1);
-    k += r * a.lrad[j];
-    lc |= (unsigned)r << (8 * j);
+    k |= (v < 0 ? M : (v < M ? v : M + 1)) << a.lsh[j];
   }
   return k;
 }
 
-template <int NP, int CPT>
+template <int NP>
 __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned key[];   // [op_xi_tile(T)]
   __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP], Gm[kXwBatch][NP];
   __shared__ int kb[kXwBatch];
-  __shared__ unsigned lb[kXwBatch];
   __shared__ double p0s[kOpXiSeqs][64];
-  __shared__ double Hl[kOpWideMaxH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = a.K, KK = K * K, T = a.T;
   const int L = op_xi_tile(T);
   const long b0 = (long)blockIdx.x * kOpXiSeqs;
   const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
-  const long n = (long)nseq * T;
+  const int n = nseq * T;
   double* const out = a.slab + (size_t)blockIdx.x * a.xrow;
-  const int hsize = a.xrow - K - (a.oncomb + 1) * KK;
-  int cx[CPT], cy[CPT];
-  bool con[CPT];
+  // The sums on the matrix cores (v_mfma_f64_16x16x4, the steps as the inner
+  // dimension, four per MFMA): Xi' tiles D[x][y] += sum_k A_k(x) G_k(y)
+  // (NT x NT tiles of 16 x 16), the leaf count rows D[r][y] += sum_k
+  // [code_j,k = r] gamma_k(y) (a one-hot A operand; RT_j x NT tiles per leaf).
+  // Tile w + 8 i goes to wave w's accumulator i: the Xi' tiles first, then
+  // the leaves' in leaf order.  An MFMA ignores EXEC, so steps outside a sum
+  // enter as zero A operands, never by branching.
+  constexpr int NT = NP / 16;
+  constexpr int TPW = NT == 2 ? 4 : 6;
+  int tkind[TPW], tx[TPW], ty[TPW], tj[TPW];      // kind 0 none, 1 Xi' (x tile, y tile), 2 leaf (j, row tile, y tile)
 #pragma unroll
-  for (int k = 0; k < CPT; k++) {
-    const int cell = tid + kXwThreads * k;
-    con[k] = cell < KK;
-    cx[k] = con[k] ? cell / K : 0;
-    cy[k] = con[k] ? cell - cx[k] * K : 0;
-  }
-  // the row's Xi' part zeroed by the threads that own the cells (each cell is
-  // later written, or read and written, by the same thread only); the leaf
-  // rows in LDS by their column's thread
-  for (int c = 0; c <= a.oncomb; c++)
-#pragma unroll
-    for (int k = 0; k < CPT; k++)
-      if (con[k]) out[(size_t)c * KK + tid + kXwThreads * k] = 0.0;
-  const bool hy = tid < K;                            // this thread: column y = tid of the leaf rows
-  if (hy)
-    for (int i = tid; i < hsize; i += K) Hl[i] = 0.0;
-
-  double acc[CPT];
-#pragma unroll
-  for (int k = 0; k < CPT; k++) acc[k] = 0.0;
-  double hacc = 0.0;
-  int cur = -1, curk = -1;
-  unsigned curl = 0;
-  auto flush = [&](bool first) {
-    if (cur >= 0) {
-#pragma unroll
-      for (int k = 0; k < CPT; k++) {
-        double* o = out + (size_t)cur * KK + tid + kXwThreads * k;
-        if (con[k]) *o = first ? acc[k] : *o + acc[k];
+  for (int i = 0; i < TPW; i++) {
+    int ti = wave + kXwWaves * i;
+    tkind[i] = 0; tx[i] = 0; ty[i] = 0; tj[i] = 0;
+    if (ti < NT * NT) {
+      tkind[i] = 1; tx[i] = ti / NT; ty[i] = ti % NT;
+    } else {
+      ti -= NT * NT;
+      for (int j = 0; j < a.nleaf; j++) {
+        const int rt = (a.lcard[j] + 2 + 15) / 16;
+        if (tkind[i] == 0 && ti < rt * NT) { tkind[i] = 2; tj[i] = j; tx[i] = ti / NT; ty[i] = ti % NT; }
+        ti -= rt * NT;
       }
     }
+  }
+  // a leaf tile's code field, row count and row offset (static-index copies:
+  // an argument array indexed by a lane-varying value would live in scratch)
+  int tsh[TPW], tmk[TPW], trows[TPW], thoff[TPW];
 #pragma unroll
-    for (int k = 0; k < CPT; k++) acc[k] = 0.0;
+  for (int i = 0; i < TPW; i++) {
+    tsh[i] = 0; tmk[i] = 0; trows[i] = 0; thoff[i] = 0;
+#pragma unroll
+    for (int j = 0; j < kOpMaxLeaf; j++)
+      if (tkind[i] == 2 && tj[i] == j) {
+        tsh[i] = a.lsh[j]; tmk[i] = (1 << a.lbits[j]) - 1; trows[i] = a.lcard[j] + 2; thoff[i] = a.hoff[j];
+      }
+  }
+  v4d D[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; i++) D[i] = v4d{0.0, 0.0, 0.0, 0.0};
+  const int li = lane & 15, lk = lane >> 4;
+  // the row's Xi' part zeroed by the lanes that own its cells (each cell is
+  // later written, or read and written, by the same lane only)
+  for (int c = 0; c <= a.oncomb; c++)
+#pragma unroll
+    for (int i = 0; i < TPW; i++)
+      if (tkind[i] == 1)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int x = 16 * tx[i] + lk + 4 * r, yy = 16 * ty[i] + li;
+          if (x < K && yy < K) out[(size_t)c * KK + x * K + yy] = 0.0;
+        }
+  int cur = -1;
+  auto flush = [&](bool first) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TPW; i++)
+      if (tkind[i] == 1) {
+        if (cur >= 0)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int x = 16 * tx[i] + lk + 4 * r, yy = 16 * ty[i] + li;
+            double* o = out + (size_t)cur * KK + x * K + yy;
+            if (x < K && yy < K) *o = first ? D[i][r] : *o + D[i][r];
+          }
+        D[i] = v4d{0.0, 0.0, 0.0, 0.0};
+      }
     cur = -1;
   };
-  auto flush_h = [&] {
-    if (hy && curk >= 0)
-      for (int j = 0; j < a.nleaf; j++) Hl[a.hoff[j] - (a.oncomb + 1) * KK + (int)((curl >> (8 * j)) & 0xff) * K + tid] += hacc;
-    hacc = 0.0;
-    curk = -1;
+  // the MFMAs of the batch's steps [k0, k1): Xi' tiles (xi) and / or leaf tiles (h)
+  constexpr int GU = NT == 2 ? 8 : 2;              // step groups unrolled (registers at 64 lanes)
+  auto mfma_pass = [&](int k0, int k1, bool xi, bool h) __attribute__((always_inline)) {
+#pragma unroll GU
+    for (int g = 0; g < kXwBatch / 4; g++) {
+      const int k = 4 * g + lk;
+      const bool in = k >= k0 && k < k1;
+      const int kc = kb[k];
+#pragma unroll
+      for (int i = 0; i < TPW; i++) {
+        if (xi && tkind[i] == 1) {
+          const double av = Ab[k][16 * tx[i] + li], bv = Gb[k][16 * ty[i] + li];
+          D[i] = mfma(in ? av : 0.0, bv, D[i]);
+        } else if (h && tkind[i] == 2) {
+          const int r = (kc >> tsh[i]) & tmk[i];
+          const double bv = Gm[k][16 * ty[i] + li];
+          D[i] = mfma(in && r == 16 * tx[i] + li ? 1.0 : 0.0, bv, D[i]);
+        }
+      }
+    }
   };
   constexpr int SPW = 64 / NP;
   const int y = lane % NP;
   const bool ys = y < K;
-  for (long i0 = 0; i0 < n; i0 += L) {
-    const int m = (int)((n - i0) < L ? (n - i0) : L);
+  for (int i0 = 0; i0 < n; i0 += L) {
+    const int m = (n - i0) < L ? (n - i0) : L;
     for (int i = tid; i < L; i += kXwThreads) {
       unsigned v = 0xFFFFFFFFu;                       // padding sorts last
       if (i < m) {
-        const long g = i0 + i;
-        const long s = g / T, t = g - s * T;
-        unsigned lc;
-        const int c = a.obs ? op_key(a, a.obs + (b0 + s) * a.obs_bstride + t * a.obs_tstride, lc) : 0;
+        const int g = i0 + i, s = g / T, t = g - s * T;
+        const int c = (a.obs && NIPAMD_XI_SKIP != 4) ? op_key(a, a.obs + (b0 + s) * a.obs_bstride + (long)t * a.obs_tstride) : 0;
         v = ((unsigned)c << kXwTileBits) | (unsigned)i;
       }
       key[i] = v;
     }
     __syncthreads();
-    for (int k2 = 2; k2 <= L; k2 <<= 1)
+    for (int k2 = 2; k2 <= (NIPAMD_XI_SKIP == 1 ? 1 : L); k2 <<= 1)
       for (int j = k2 >> 1; j > 0; j >>= 1) {
         for (int i = tid; i < L; i += kXwThreads) {
           const int p = i ^ j;
@@ -877,66 +907,109 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
         }
         __syncthreads();
       }
-    for (int j0 = 0; j0 < m; j0 += kXwBatch) {
-      // stage: wave w the batch slots 8w .. 8w + 7, 64 / NP of them per pass
+    // Staging, software-pipelined: the next batch's loads (messages, scale
+    // exponent, leaf factors -- all addressed from the sorted key alone) are
+    // issued before this batch's sums and land in LDS after them.  Wave w
+    // stages slots SL_w .. SL_w + SL - 1, 64 / NP per pass.
+    constexpr int SL = kXwBatch / kXwWaves / SPW;
+    // two batches in flight: the one in LDS is summed while the next one's
+    // loads land in one register set and the one after that is issued into
+    // the other (the random-order message reads are latency-bound)
+    // (register sets indexed by a compile-time buffer number: a struct passed
+    // by reference would live in scratch)
+    double P_at[2][SL], P_bt[2][SL], P_ap[2][SL], P_e[2][SL];
+    int P_sc[2][SL], P_kc[2][SL];
+    bool P_ok[2][SL];
+    auto load_batch = [&](int j0, auto buf) __attribute__((always_inline)) {
+      constexpr int u = decltype(buf)::value;
 #pragma unroll
-      for (int q = 0; q < kXwBatch / 4; q += SPW) {
-        const int jj = wave * (kXwBatch / 4) + q + lane / NP;
+      for (int q = 0; q < SL; q++) {
+        const int jj = wave * (kXwBatch / kXwWaves) + q * SPW + lane / NP;
         const int j = j0 + jj;
         const bool ok = j < m;
         const unsigned v = key[ok ? j : 0];
-        const long g = i0 + (v & (kXwTileMax - 1));
-        const long s = g / T, t = g - s * T, b = b0 + s;
+        const int g = i0 + (int)(v & (kXwTileMax - 1)), s = g / T, t = g - s * T;
+        const long b = b0 + s;
         const double* sa = a.Sa + ((size_t)b * T + t) * NP + y;
         const double* sb = a.Sb + ((size_t)b * T + t) * NP + y;
-        const bool on = ok && ys;
-        const double at = on ? sa[0] : 0.0, bt = on ? sb[0] : 0.0;
-        const double ap = on ? (t > 0 ? sa[-NP] : a.pi[y]) : 0.0;
-        const double pr = at * bt;
-        const double z = group_sum<NP>(pr);
-        const int sc = ok ? a.sc[(size_t)b * T + t] : 0;
-        const double f = z != 0.0 ? __builtin_ldexp(1.0 / z, sc) : 0.0;
-        // the leaf codes from the sort key (no observation re-read), their
-        // factors as op_leaf_e multiplies them
-        double e = 1.0;
-        unsigned lc = 0;
+        const bool on = ok && ys && NIPAMD_XI_SKIP != 3;
+        P_at[u][q] = on ? sa[0] : 0.0;
+        P_bt[u][q] = on ? sb[0] : 0.0;
+        P_ap[u][q] = on ? (t > 0 ? sa[-NP] : a.pi[y]) : 0.0;
+        P_sc[u][q] = ok ? a.sc[(size_t)b * T + t] : 0;
         const int kc = (int)(v >> kXwTileBits);
-        for (int q2 = 0; q2 < a.nleaf; q2++) {
-          const int r = (kc / a.lrad[q2]) % (a.lcard[q2] + 2);
-          lc |= (unsigned)r << (8 * q2);
-          e *= a.ltab[a.loff[q2] + r * K + (ys ? y : 0)];
-        }
-        Ab[jj][y] = ap;
-        Gb[jj][y] = bt * e * f;
-        Gm[jj][y] = z != 0.0 ? pr / z : 0.0;
-        if (y == 0) {
-          kb[jj] = ok ? (int)(v >> kXwTileBits) : -1;
-          lb[jj] = lc;
-        }
-      }
-      __syncthreads();
-      const int nj = (m - j0) < kXwBatch ? (m - j0) : kXwBatch;
-      for (int jj = 0; jj < nj; jj++) {
-        const int kc = kb[jj];
-        if (kc != curk) {
-          flush_h();
-          curk = kc;
-          curl = lb[jj];
-        }
-        const int c = kc / a.Lr;
-        if (c != cur) { flush(i0 == 0); cur = c; }
+        P_kc[u][q] = kc;
+        P_ok[u][q] = ok;
+        // the leaf factors from the key's codes (no observation re-read), in
+        // op_leaf_e's order
+        double e = 1.0;
 #pragma unroll
-        for (int k = 0; k < CPT; k++) acc[k] = __builtin_fma(Ab[jj][cx[k]], Gb[jj][cy[k]], acc[k]);
-        if (hy) hacc += Gm[jj][tid];
+        for (int q2 = 0; q2 < kOpMaxLeaf; q2++)
+          if (q2 < a.nleaf)
+            e *= a.ltab[a.loff[q2] + ((kc >> a.lsh[q2]) & ((1 << a.lbits[q2]) - 1)) * K + (ys ? y : 0)];
+        P_e[u][q] = e;
       }
+    };
+    auto store_batch = [&](auto buf) __attribute__((always_inline)) {
+      constexpr int u = decltype(buf)::value;
+#pragma unroll
+      for (int q = 0; q < SL; q++) {
+        const int jj = wave * (kXwBatch / kXwWaves) + q * SPW + lane / NP;
+        const double pr = P_at[u][q] * P_bt[u][q];
+        const double z = group_sum<NP>(pr);
+        const double rz = z != 0.0 ? 1.0 / z : 0.0;
+        Ab[jj][y] = P_ap[u][q];
+        Gb[jj][y] = P_bt[u][q] * P_e[u][q] * __builtin_ldexp(rz, P_sc[u][q]);
+        Gm[jj][y] = pr * rz;
+        if (y == 0) kb[jj] = P_ok[u][q] ? P_kc[u][q] : -1;
+      }
+    };
+    auto accumulate = [&](int j0) __attribute__((always_inline)) {
+      const int nj = (m - j0) < kXwBatch ? (m - j0) : kXwBatch;
+      if (NIPAMD_XI_SKIP == 2) return;
+      const int cl = kb[nj - 1] >> a.Lbits;
+      if ((kb[0] >> a.Lbits) == cl) {
+        // one operator index over the batch (the common case: runs are long)
+        if (cl != cur) { flush(i0 == 0); cur = cl; }
+        mfma_pass(0, nj, true, true);
+        return;
+      }
+      mfma_pass(0, nj, false, true);
+      int k0 = 0;
+      while (k0 < nj) {
+        const int c = kb[k0] >> a.Lbits;
+        int k1 = k0 + 1;
+        while (k1 < nj && (kb[k1] >> a.Lbits) == c) k1++;
+        if (c != cur) { flush(i0 == 0); cur = c; }
+        mfma_pass(k0, k1, true, false);
+        k0 = k1;
+      }
+    };
+    const std::integral_constant<int, 0> pa{};
+    const std::integral_constant<int, 1> pb{};
+    load_batch(0, pa);
+    store_batch(pa);
+    if (kXwBatch < m) load_batch(kXwBatch, pa);
+    for (int j0 = 0; j0 < m; j0 += 2 * kXwBatch) {
+      // batch j0 in LDS, batch j0 + 32 in register set 0
       __syncthreads();
+      if (j0 + 2 * kXwBatch < m) load_batch(j0 + 2 * kXwBatch, pb);
+      accumulate(j0);
+      __syncthreads();
+      if (j0 + kXwBatch >= m) break;
+      store_batch(pa);
+      // batch j0 + 32 in LDS, batch j0 + 64 in register set 1
+      __syncthreads();
+      if (j0 + 3 * kXwBatch < m) load_batch(j0 + 3 * kXwBatch, pa);
+      accumulate(j0 + kXwBatch);
+      __syncthreads();
+      if (j0 + 2 * kXwBatch < m) store_batch(pb);
     }
     flush(i0 == 0);
-    flush_h();
   }
   // P0 per sequence: normalise(prior o T_{c_0} (e_0 o beta^_0)), as op_fb_kernel's
   // extra backward step; then summed over the group in sequence order
-  for (int s = wave; s < nseq; s += 4) {
+  for (int s = wave; s < nseq; s += kXwWaves) {
     const long b = b0 + s;
     const int32_t* o0 = a.obs ? a.obs + b * a.obs_bstride : nullptr;
     const int c0 = o0 ? (op_code(a, o0) & (kOpEv - 1)) : 0;
@@ -952,12 +1025,19 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     p0s[s][lane] = z != 0.0 ? pr / z : pr;
   }
   __syncthreads();
-  if (hy) {
+  if (tid < K) {
     double p = 0.0;
     for (int s = 0; s < nseq; s++) p += p0s[s][tid];
     out[a.xrow - K + tid] = p;
-    for (int i = tid; i < hsize; i += K) out[(size_t)(a.oncomb + 1) * KK + i] = Hl[i];
   }
+#pragma unroll
+  for (int i = 0; i < TPW; i++)
+    if (tkind[i] == 2)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 16 * tx[i] + lk + 4 * r, yy = 16 * ty[i] + li;
+        if (row < trows[i] && yy < K) out[(size_t)thoff[i] + row * K + yy] = D[i][r];
+      }
 }
 
 }  // namespace
@@ -992,26 +1072,28 @@ int op_wide_launch(const OpWideArgs& a, hipStream_t stream) {
   return op_wide_np(a.K) == 32 ? msgs_launch<32>(a, stream) : msgs_launch<64>(a, stream);
 }
 
-template <int NP, int CPT>
+template <int NP>
 int xi_launch(const OpWideArgs& a, hipStream_t stream) {
+  // every MFMA tile needs an accumulator slot: NT^2 Xi' tiles + the leaves'
+  constexpr int NT = NP / 16, TPW = NT == 2 ? 4 : 6;
+  int tiles = NT * NT;
+  for (int j = 0; j < a.nleaf; j++) tiles += (a.lcard[j] + 2 + 15) / 16 * NT;
+  if (tiles > kXwWaves * TPW) return -2;
   const size_t lds = (size_t)op_xi_tile(a.T) * sizeof(unsigned);
   static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP, CPT>), lds, set)) return -1;
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP>), lds, set)) return -1;
   const dim3 g((unsigned)((a.B + kOpXiSeqs - 1) / kOpXiSeqs)), th(kXwThreads);
-  hipLaunchKernelGGL((op_wide_xi_kernel<NP, CPT>), g, th, lds, stream, a);
+  hipLaunchKernelGGL((op_wide_xi_kernel<NP>), g, th, lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int op_wide_xi_launch(const OpWideArgs& a, hipStream_t stream) {
   if (a.B <= 0) return 0;
-  if (a.K > 64 || a.K < 17 || a.oncomb > 65534 || !a.sc || !a.slab || a.Lr < 1 ||
-      (long)(a.oncomb + 1) * a.Lr >= (1L << kOpWideKeyBits) || a.xrow - a.K - (a.oncomb + 1) * a.K * a.K > kOpWideMaxH)
+  if (a.K > 64 || a.K < 17 || a.oncomb > 65534 || !a.sc || !a.slab || a.Lbits < 0 ||
+      ((long)(a.oncomb + 1) << a.Lbits) > (1L << kOpWideKeyBits) ||
+      a.xrow - a.K - (a.oncomb + 1) * a.K * a.K > kOpWideMaxH || (long)kOpXiSeqs * a.T >= (1L << 31))
     return -2;
-  const int KK = a.K * a.K;
-  if (KK <= 2 * kXwThreads) return xi_launch<32, 2>(a, stream);
-  if (KK <= 4 * kXwThreads) return xi_launch<32, 4>(a, stream);
-  if (KK <= 8 * kXwThreads) return xi_launch<64, 8>(a, stream);
-  return xi_launch<64, 16>(a, stream);
+  return op_wide_np(a.K) == 32 ? xi_launch<32>(a, stream) : xi_launch<64>(a, stream);
 }
 
 int estep_wide_np(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 0; }

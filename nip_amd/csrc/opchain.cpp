@@ -51,8 +51,8 @@ struct OpPlan {
   std::vector<int> lcl;              // the leaves' cliques
   // the e_step's slab row (opchain.h OpWideArgs): sort-key radix, leaf count
   // rows' offsets, row size
-  int Lr = 1;
-  std::vector<int> lrad, hoff;
+  int Lbits = 0;
+  std::vector<int> lsh, lbits, hoff;
   long xrow = 0;
   std::vector<double> lt;
   std::vector<double> T, w, pi;      // T: [(oncomb + 1)][K][K]
@@ -143,14 +143,16 @@ bool build(const Model& m, OpPlan& P) {
       lcl.push_back(cl);
       hsz += (long)(P.card[i] + 2) * K;
     }
-  // the sort key c' * Lr + leaf codes must fit: drop leaves from the back
+  // the sort key c' << Lbits | leaf codes must fit: drop leaves from the back
+  auto code_bits = [](int card) { int b = 0; while ((1 << b) < card + 2) b++; return b; };
   for (;;) {
-    long oc = 1, lr = 1;
+    long oc = 1;
+    int lb = 0;
     for (int i = 0; i < no; i++) {
-      if (leaf[i]) lr *= P.card[i] + 2;
+      if (leaf[i]) lb += code_bits(P.card[i]);
       else oc *= P.card[i] + 1;
     }
-    if ((oc + 1) * lr < (1L << kOpWideKeyBits) || lcl.empty()) break;
+    if (((oc + 1) << lb) <= (1L << kOpWideKeyBits) || lcl.empty()) break;
     for (int i = no - 1; i >= 0; i--)
       if (leaf[i]) { leaf[i] = 0; lcl.pop_back(); break; }
   }
@@ -245,11 +247,14 @@ bool build(const Model& m, OpPlan& P) {
       eall[y] *= sum;
     }
   }
-  P.Lr = 1;
+  P.Lbits = 0;
   P.xrow = (long)(oncomb + 1) * K * K;
   for (size_t j = 0; j < P.li.size(); j++) {
-    P.lrad.push_back(P.Lr);
-    P.Lr *= P.card[P.li[j]] + 2;
+    int b = 0;
+    while ((1 << b) < P.card[P.li[j]] + 2) b++;
+    P.lsh.push_back(P.Lbits);
+    P.lbits.push_back(b);
+    P.Lbits += b;
     P.hoff.push_back((int)P.xrow);
     P.xrow += (long)(P.card[P.li[j]] + 2) * K;
   }
@@ -305,8 +310,8 @@ void fill_wide(const OpPlan* P, int n_obs, OpWideArgs& w) {
   for (int j = 0; j < w.nleaf; j++) { w.lcol[j] = P->li[j]; w.lcard[j] = P->card[P->li[j]]; w.loff[j] = P->loff[j]; }
   w.ltab = P->dlt;
   w.Ttab = P->dT; w.w = P->dw; w.pi = P->dpi;
-  w.Lr = P->Lr;
-  for (int j = 0; j < w.nleaf; j++) { w.lrad[j] = P->lrad[j]; w.hoff[j] = P->hoff[j]; }
+  w.Lbits = P->Lbits;
+  for (int j = 0; j < w.nleaf; j++) { w.lsh[j] = P->lsh[j]; w.lbits[j] = P->lbits[j]; w.hoff[j] = P->hoff[j]; }
   w.xrow = (int)P->xrow;
 }
 

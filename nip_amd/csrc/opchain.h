@@ -141,14 +141,15 @@ struct OpWideArgs {
   // the e_step's slab row (op_wide_xi_kernel): Xi' [(oncomb + 1)][K][K] keyed
   // by the operator index, then per leaf j its count rows H_j [(lcard[j] + 2)][K]
   // at hoff[j] (gamma_t summed by the leaf's code), then P0 [K] at xrow - K.
-  // Sort key of a step: c' * Lr + sum_j code_j * lrad[j]
-  int Lr;
-  int lrad[kOpMaxLeaf];
+  // Sort key of a step: c' << Lbits | code_j << lsh[j] (code_j in lbits[j] bits)
+  int Lbits;
+  int lsh[kOpMaxLeaf];
+  int lbits[kOpMaxLeaf];
   int hoff[kOpMaxLeaf];
   int xrow;
 };
 constexpr int kOpWideMaxH = 2048;      // doubles of leaf count rows (op_wide_xi_kernel's LDS)
-constexpr int kOpWideKeyBits = 18;     // (oncomb + 1) * Lr < 2^18
+constexpr int kOpWideKeyBits = 18;     // (oncomb + 1) << Lbits <= 2^18
 inline int op_wide_np(int K) { return K <= 32 ? 32 : 64; }
 inline size_t op_wide_scratch_bytes(int K, long B, int T) {
   return (size_t)2 * B * T * op_wide_np(K) * sizeof(double);

@@ -21,8 +21,6 @@ to the single-GPU run.  That all-gather (partial_size + 2 doubles per rank,
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 
 MIN_EM_ITERATIONS = 3          # src/nip.c:29
@@ -120,7 +118,7 @@ def iteration(model, params, obs, obs_vars, group=None, backend=None, timing=Non
     be = backend or GpuEStep()
     P = model.param_size()
     model.m_step(params)                          # nip.c:2154
-    if isinstance(be, GpuEStep) and obs.is_cuda and os.environ.get("NIPAMD_EM_PACKED", "1") != "0":
+    if isinstance(be, GpuEStep) and obs.is_cuda:
         # the product path: one buffer from the e_step to the finalize, and
         # one device-to-host synchronisation per iteration (the counts)
         packed, S = be.packed(model, obs, obs_vars)
