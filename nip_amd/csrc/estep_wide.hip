@@ -567,18 +567,24 @@ template <int NP, bool TL>
 __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char op_smem[];
   constexpr int SPW = 64 / NP, NB = NP / 16;
-  constexpr int WD = kMsgWaves / 2;
+  constexpr int SPB = kMsgWaves * SPW;                      // sequences per block
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T, K = a.K, KK = K * K;
-  op_lds_d* const Tl = (op_lds_d*)(op_smem);                 // TL: [(oncomb + 1)][K][K]
+  // blocks [0, nbd) run forward filters, [nbd, 2 nbd) backward ones: each
+  // block stages one orientation of the operators, every state's row
+  // contiguous -- forward T'^T (TtabT), backward T' -- so a lane reads its
+  // step's coefficients at fixed offsets from one base, with no predicate
+  const int nbd = (int)((a.B + SPB - 1) / SPB);
+  const bool fwd = (int)blockIdx.x < nbd;
+  const int blk = fwd ? (int)blockIdx.x : (int)blockIdx.x - nbd;
+  const double* const src = fwd ? a.TtabT : a.Ttab;         // [(oncomb + 1)][K][K] + NP zeros
+  op_lds_d* const Tl = (op_lds_d*)(op_smem);                 // TL: the same in LDS
   if (TL) {
-    for (int i = tid; i < (a.oncomb + 1) * KK; i += kMsgWaves * 64) Tl[i] = a.Ttab[i];
+    for (int i = tid; i < (a.oncomb + 1) * KK + NP; i += kMsgWaves * 64) Tl[i] = src[i];
     __syncthreads();
   }
-  const bool fwd = wave < WD;
-  if (!fwd && a.filter) return;
   const int s = lane / NP, y = lane % NP;
-  const long b = (long)blockIdx.x * (WD * SPW) + (wave % WD) * SPW + s;
+  const long b = (long)blk * SPB + wave * SPW + s;
   const bool active = b < a.B;
   const long bb = active ? b : 0;
   const bool ys = y < K;
@@ -630,17 +636,15 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
 #pragma unroll
     for (int k = 0; k < kMsgChunk; k++) code[k] = (oor[k] ? a.oncomb : c[k]) | (ev[k] ? kOpEv : 0);
   };
-  // this lane's column (forward) / row (backward) of T'_c, in 16-state blocks
+  // this lane's column (forward) / row (backward) of T'_c, in 16-state
+  // blocks: entries x >= K read the next row or the padding (finite), and
+  // meet x = 0 in the mat-vec; lanes y >= K read row 0 and are zeroed after
   auto coef = [&](int code, double (&C)[NB][16]) {
-    const int c = code & (kOpEv - 1);
+    const int base = (code & (kOpEv - 1)) * KK + yc * K;
 #pragma unroll
     for (int k = 0; k < NB; k++)
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int x = 16 * k + j;
-        const int i = c * KK + (fwd ? x * K + y : y * K + x);
-        C[k][j] = (x < K && ys) ? (TL ? (double)Tl[i] : a.Ttab[i]) : 0.0;
-      }
+      for (int j = 0; j < 16; j++) C[k][j] = TL ? (double)Tl[base + 16 * k + j] : src[base + 16 * k + j];
   };
   int cc[kMsgChunk], cn[kMsgChunk];
   double ec[kMsgChunk], en[kMsgChunk];
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
       const double m1v = fwd ? group_sum<NP>(x * wy) : 0.0;
       const double acc = matvec_dpp<NB>(fwd ? x : x * ec[k], C);
       coef(k + 1 < kMsgChunk ? cc[k + 1] : cn[0], C);   // the next step's operator, under this step's work
-      double u = __builtin_ldexp(acc, sc);
+      double u = ys ? __builtin_ldexp(acc, sc) : 0.0;
       if (fwd) u *= ec[k];
       const double z = group_sum<NP>(u);
       if (fwd) {
@@ -1048,9 +1052,10 @@ constexpr size_t kOpWideTl = 76 * 1024;
 
 template <int NP>
 int msgs_launch(const OpWideArgs& a, hipStream_t stream) {
-  const int spb = kMsgWaves / 2 * (64 / NP);
-  const dim3 g((unsigned)((a.B + spb - 1) / spb)), th(kMsgWaves * 64);
-  const size_t tl = (size_t)(a.oncomb + 1) * a.K * a.K * sizeof(double);
+  const int spb = kMsgWaves * (64 / NP);
+  const int nbd = (int)((a.B + spb - 1) / spb);
+  const dim3 g((unsigned)(a.filter ? nbd : 2 * nbd)), th(kMsgWaves * 64);
+  const size_t tl = ((size_t)(a.oncomb + 1) * a.K * a.K + NP) * sizeof(double);
   if (tl <= kOpWideTl) {
     static size_t set[kMaxDevices] = {};
     if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_msgs_kernel<NP, true>), tl, set)) return -1;

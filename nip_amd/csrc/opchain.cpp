@@ -55,8 +55,10 @@ struct OpPlan {
   std::vector<int> lsh, lbits, hoff;
   long xrow = 0;
   std::vector<double> lt;
-  std::vector<double> T, w, pi;      // T: [(oncomb + 1)][K][K]
+  std::vector<double> T, w, pi;      // T: [(oncomb + 1)][K][K] + 64 zeros (the wide kernels' over-reads)
+  std::vector<double> TT;            // K > 16: T transposed per operator, + 64 zeros
   double* dT = nullptr;
+  double* dTT = nullptr;
   double* dw = nullptr;
   double* dpi = nullptr;
   double* dlt = nullptr;
@@ -74,7 +76,7 @@ struct OpPlan {
   double* E = nullptr;
   size_t E_bytes = 0;
   ~OpPlan() {
-    (void)hipFree(dT); (void)hipFree(dw); (void)hipFree(dpi); (void)hipFree(dlt); (void)hipFree(S);
+    (void)hipFree(dT); (void)hipFree(dTT); (void)hipFree(dw); (void)hipFree(dpi); (void)hipFree(dlt); (void)hipFree(S);
     (void)hipFree(d_mptr); (void)hipFree(d_midx); (void)hipFree(d_mcoef); (void)hipFree(E);
   }
 };
@@ -267,6 +269,13 @@ bool build(const Model& m, OpPlan& P) {
     long r = x;
     for (int v : prev) { P.pi[x] *= m.vars[v].prior[r % m.vars[v].card]; r /= m.vars[v].card; }
   }
+  P.T.resize(P.T.size() + 64, 0.0);
+  if (K > 16) {
+    P.TT.assign(P.T.size(), 0.0);
+    for (long c = 0; c <= oncomb; c++)
+      for (long x = 0; x < K; x++)
+        for (long y = 0; y < K; y++) P.TT[(size_t)c * K * K + y * K + x] = P.T[(size_t)c * K * K + x * K + y];
+  }
   return true;
 }
 
@@ -309,7 +318,7 @@ void fill_wide(const OpPlan* P, int n_obs, OpWideArgs& w) {
   w.nleaf = (int)P->li.size();
   for (int j = 0; j < w.nleaf; j++) { w.lcol[j] = P->li[j]; w.lcard[j] = P->card[P->li[j]]; w.loff[j] = P->loff[j]; }
   w.ltab = P->dlt;
-  w.Ttab = P->dT; w.w = P->dw; w.pi = P->dpi;
+  w.Ttab = P->dT; w.TtabT = P->dTT; w.w = P->dw; w.pi = P->dpi;
   w.Lbits = P->Lbits;
   for (int j = 0; j < w.nleaf; j++) { w.lsh[j] = P->lsh[j]; w.lbits[j] = P->lbits[j]; w.hoff[j] = P->hoff[j]; }
   w.xrow = (int)P->xrow;
@@ -348,10 +357,12 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) { err = "no device"; return NIPAMD_ERROR_DEVICE; }
   if (P->device != dev || !P->dT) {
-    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->dlt); (void)hipFree(P->S);
-    P->dT = P->dw = P->dpi = P->dlt = P->S = nullptr;
+    (void)hipFree(P->dT); (void)hipFree(P->dTT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->dlt);
+    (void)hipFree(P->S);
+    P->dT = P->dTT = P->dw = P->dpi = P->dlt = P->S = nullptr;
     P->S_bytes = 0;
-    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi) || upload(&P->dlt, P->lt)) {
+    if (upload(&P->dT, P->T) || upload(&P->dTT, P->TT) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi) ||
+        upload(&P->dlt, P->lt)) {
       err = "device tables";
       return NIPAMD_ERROR_DEVICE;
     }
@@ -740,11 +751,12 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) { err = "no device"; return NIPAMD_ERROR_DEVICE; }
   if (P->device != dev || !P->dT) {
-    (void)hipFree(P->dT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->dlt); (void)hipFree(P->S);
-    (void)hipFree(P->E);
-    P->dT = P->dw = P->dpi = P->dlt = P->S = P->E = nullptr;
+    (void)hipFree(P->dT); (void)hipFree(P->dTT); (void)hipFree(P->dw); (void)hipFree(P->dpi); (void)hipFree(P->dlt);
+    (void)hipFree(P->S); (void)hipFree(P->E);
+    P->dT = P->dTT = P->dw = P->dpi = P->dlt = P->S = P->E = nullptr;
     P->S_bytes = P->E_bytes = 0;
-    if (upload(&P->dT, P->T) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi) || upload(&P->dlt, P->lt)) {
+    if (upload(&P->dT, P->T) || upload(&P->dTT, P->TT) || upload(&P->dw, P->w) || upload(&P->dpi, P->pi) ||
+        upload(&P->dlt, P->lt)) {
       err = "device tables";
       return NIPAMD_ERROR_DEVICE;
     }

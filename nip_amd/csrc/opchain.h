@@ -120,7 +120,8 @@ struct OpWideArgs {
   int lcard[kOpMaxLeaf];
   int loff[kOpMaxLeaf];    // F_j at ltab + loff[j]: [(lcard[j] + 2)][K]
   const double* ltab;
-  const double* Ttab;      // [(oncomb + 1)][K][K]
+  const double* Ttab;      // [(oncomb + 1)][K][K] + 64 zeros: T'_c(x, y) at c K^2 + x K + y
+  const double* TtabT;     // the same transposed per operator: T'_c(x, y) at c K^2 + y K + x
   const double* w;         // [K]
   const double* pi;        // [K]
   double* Sa;              // [B][T][NP]
