@@ -474,8 +474,9 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
     return;
   }
   // A/B builds: static wave priority for the recompute waves (1) or the partners (2)
-  if ((NIPAMD_CK_PRIO == 1 && wave >= 6) || (NIPAMD_CK_PRIO == 2 && role >= 2 && wave < 4))
+  if ((NIPAMD_CK_PRIO == 1 && wave >= 6) || ((NIPAMD_CK_PRIO == 2 || NIPAMD_CK_PRIO == 3) && role >= 2 && wave < 4))
     __builtin_amdgcn_s_setprio(1);
+  if (NIPAMD_CK_PRIO == 3 && wave < 2) __builtin_amdgcn_s_setprio(2);   // A/B: the filters above their SIMD's posterior wave
   if (role >= 2 && wave < 4) {
     if (fwd) ck_partner<true, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
     else ck_partner<false, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
