@@ -38,9 +38,6 @@ namespace nipamd {
 
 namespace {
 
-#ifndef NIPAMD_CK_SPLIT
-#define NIPAMD_CK_SPLIT 0   // 1: waves 4 / 5 recompute the second sub-chain of every chunk, the partners take every posterior
-#endif
 constexpr int kCThreads = 512;   // 8 waves, two per SIMD
 // Evidence rows 144 B apart: row r starts at bank 36r mod 64, so sixteen
 // chains reading sixteen different rows (16 B per lane) conflict at most
@@ -98,9 +95,7 @@ struct CkDiag {
 // relies on four); the posterior normalisation removes the scale.  The next
 // chunk's evidence vectors and the checkpoints two chunks ahead are loaded
 // while a chunk runs.
-// HS: -1 both sub-chains of every chunk (interleaved); 0 / 1 only that one
-// (NIPAMD_CK_SPLIT: the two halves on two waves of different SIMDs)
-template <bool FWD, int HS = -1>
+template <bool FWD>
 __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx& c, const double* Sw, int lane,
                                                int nchA, int nchB, CkDiag& dg) {
   const int j = lane & 15, g = lane >> 4;
@@ -161,8 +156,7 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
   };
   auto norm_exp = [](const v4d& v) { return -__builtin_amdgcn_frexp_exp(chain_sum(v)); };
 
-  constexpr int h0 = HS < 0 ? 0 : HS, h1 = HS < 0 ? 1 : HS;   // the sub-chains of this wave
-  v4d P0 = ld(0, h0), P1 = ld(0, h1), Q0 = ld(1, h0), Q1 = ld(1, h1);
+  v4d P0 = ld(0, 0), P1 = ld(0, 1), Q0 = ld(1, 0), Q1 = ld(1, 1);
   v4d Ea[kE], Eb[kE];
   int Ca[kE], Cb[kE];
   ldC(0, Ca);
@@ -174,8 +168,8 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
     dg.lap(nullptr);
     double* slot = c.out + (ci & 1) * kSlotD;
     const v4d cur0 = R0, cur1 = R1;
-    R0 = ld(ci + 2, h0);
-    if (HS < 0) R1 = ld(ci + 2, 1);
+    R0 = ld(ci + 2, 0);
+    R1 = ld(ci + 2, 1);
     // chunk ci + 1's evidence and chunk ci + 2's codes, issued after the
     // first step pair so that no step waits behind them
     auto issue = [&] {
@@ -187,33 +181,23 @@ __device__ __forceinline__ void recompute_wave(const ChainArgs& a, const WaveCtx
       // the checkpoints are rows 3 and 7 (they sum to ~1, beta_{T-1} = 1 to
       // N: three evidence factors per sub-chain at most, no rescale); rows
       // 2..0 and 6..4 follow, forward in increasing t, backward in decreasing t
-      if (HS < 0) {
-        row(slot, 3, cur0);
-        row(slot, 7, cur1);
-        v4d X0 = FWD ? cur0 : cur0 * E[3], X1 = FWD ? cur1 : cur1 * E[7];
-        dg.lap(&dg.x1);
-        issue();
+      row(slot, 3, cur0);
+      row(slot, 7, cur1);
+      v4d X0 = FWD ? cur0 : cur0 * E[3], X1 = FWD ? cur1 : cur1 * E[7];
+      dg.lap(&dg.x1);
+      issue();
 #pragma unroll
-        for (int q = 2; q >= 0; q--) {
-          step(X0, 0, slot, q, E[q]);
-          step(X1, 0, slot, q + 4, E[q + 4]);
-        }
-      } else {
-        constexpr int o = 4 * h0;
-        row(slot, 3 + o, cur0);
-        v4d X0 = FWD ? cur0 : cur0 * E[3 + o];
-        dg.lap(&dg.x1);
-        issue();
-#pragma unroll
-        for (int q = 2; q >= 0; q--) step(X0, 0, slot, q + o, E[q + o]);
+      for (int q = 2; q >= 0; q--) {
+        step(X0, 0, slot, q, E[q]);
+        step(X1, 0, slot, q + 4, E[q + 4]);
       }
     } else if (rem > 0) {
       issue();
       // the phase's last chunk: short, or reaching t = T - 1 (rare; plain loops)
 #pragma unroll
-      for (int h = h0; h <= h1; h++) {
+      for (int h = 0; h < 2; h++) {
         const int ts = start(ci, h);
-        const v4d cur = h == h0 ? cur0 : cur1;
+        const v4d cur = h ? cur1 : cur0;
         if (FWD) {
           const int hiT = H - 1 - 8 * ci;
           if (hiT - 4 * h < 0) continue;          // no valid row
@@ -431,8 +415,6 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
       ll.renorm();
     }
     norm_store<FWD, PROJ>(a, out + (ci & 1) * kSlotD, rring + (ci & 1) * kSlotD, 0, lane, b0, ci, sink);
-    if (NIPAMD_CK_SPLIT)
-      norm_store<FWD, PROJ>(a, out + (ci & 1) * kSlotD, rring + (ci & 1) * kSlotD, 1, lane, b0, ci, sink);
   }
   if (FWD) ll.write(a, b0, lane, 1u);
   barrier_lds();                                     // the block's closing barrier
@@ -440,7 +422,11 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
 
 template <int PROJ>
 #ifndef NIPAMD_CK_PRIO
-#define NIPAMD_CK_PRIO 2   // the partners at s_setprio 1: -1% mean over 12 interleaved A/B rounds on 3 boxes (within noise; r04y, r04zd, r04f)
+// 3: the partners at s_setprio 1 and the filters at 2, above the posterior
+// wave sharing their SIMD: -3.6% (0.2476 vs 0.2569 ms) in 5 of 5 interleaved
+// pairs and 4 of 4 on a second box (profiles/r05/gpu/r05q_ab_fb.txt,
+// r05o_ab_fb_ckprio3.txt); 2: the partners only (round 4)
+#define NIPAMD_CK_PRIO 3
 #endif
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -475,31 +461,6 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   // waves 4 and 5 (the filters' SIMDs): chains 8-15 of the other side's
   // posteriors -- wave 4 the backward side's, wave 5 the forward side's
   double* const sink = a.S + (size_t)((a.B + kMSeq - 1) / kMSeq) * block_scratch(T) + 2 * (lane & 7);
-  if (NIPAMD_CK_SPLIT && (wave == 4 || wave == 5)) {
-    // wave 4 (the forward filter's SIMD): alpha rows of the backward side's
-    // chunks, sub-chain 1; wave 5: beta rows of the forward side's, sub-chain 1
-    WaveCtx c;
-    c.Et = Et + 2 * g;
-    c.es = kEtStride;
-    c.codes = codes + j * Tr + kMG;
-    c.zr = zr;
-    c.scr = nullptr;
-    c.wo0 = ck_off(0, j, g);
-    c.wo1 = ck_off(0, j, 4 + g);
-    c.wodd = ck_off(1, j, g) - kStepD - c.wo0;
-    c.zw = false;
-    const double* Sw = Sblk + j * 16 + 2 * g;
-    if (wave == 4) {
-      c.out = rr + 2 * kSlotD;
-      recompute_wave<true, 1>(a, c, Sw, lane, nchA, nchB, dg);
-    } else {
-      c.out = rr;
-      recompute_wave<false, 1>(a, c, Sw, lane, nchA, nchB, dg);
-    }
-    barrier_lds();
-    dg.write(a, wave, lane);
-    return;
-  }
   if (wave == 4 || wave == 5) {
     const bool f = wave == 5;
     for (int ci = 0; ci < nchA; ci++) barrier_lds();
@@ -519,7 +480,7 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   // A/B builds: static wave priority for the recompute waves (1) or the partners (2)
   if ((NIPAMD_CK_PRIO == 1 && wave >= 6) || ((NIPAMD_CK_PRIO == 2 || NIPAMD_CK_PRIO == 3) && role >= 2 && wave < 4))
     __builtin_amdgcn_s_setprio(1);
-  if (NIPAMD_CK_PRIO == 3 && wave < 2) __builtin_amdgcn_s_setprio(2);   // A/B: the filters above their SIMD's posterior wave
+  if (NIPAMD_CK_PRIO == 3 && wave < 2) __builtin_amdgcn_s_setprio(2);
   if (role >= 2 && wave < 4) {
     if (fwd) ck_partner<true, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
     else ck_partner<false, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
@@ -539,14 +500,8 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
   if (wave >= 6) {
     c.out = rring;
     c.zw = false;
-    if (NIPAMD_CK_SPLIT) {
-      if (fwd) recompute_wave<false, 0>(a, c, Sw, lane, nchA, nchB, dg);   // wave 6: beta, sub-chain 0
-      else recompute_wave<true, 0>(a, c, Sw, lane, nchA, nchB, dg);        // wave 7: alpha, sub-chain 0
-    } else if (fwd) {
-      recompute_wave<false>(a, c, Sw, lane, nchA, nchB, dg);   // wave 6: beta for the forward side
-    } else {
-      recompute_wave<true>(a, c, Sw, lane, nchA, nchB, dg);    // wave 7: alpha for the backward side
-    }
+    if (fwd) recompute_wave<false>(a, c, Sw, lane, nchA, nchB, dg);   // wave 6: beta for the forward side
+    else recompute_wave<true>(a, c, Sw, lane, nchA, nchB, dg);        // wave 7: alpha for the backward side
     barrier_lds();
     dg.write(a, wave, lane);
     return;

@@ -692,6 +692,10 @@ __global__ __launch_bounds__(kThreads, 1) void chain_estep_mw_kernel(EMwArgs a) 
 
   for (int i = tid; i < a.tab_rows * NP; i += kThreads) tab[(i / NP) * NPS + i % NP] = a.tab[i];
   __syncthreads();
+#ifndef NIPAMD_MW_PRIO
+#define NIPAMD_MW_PRIO 0   // A/B builds: 1 the filters above the partners sharing their SIMDs
+#endif
+  if (NIPAMD_MW_PRIO == 1 && filter) __builtin_amdgcn_s_setprio(1);
 
   const int nA = H > T - 1 - H ? H : T - 1 - H, nB = T - H > H + 1 ? T - H : H + 1;
   const int nchA = (nA + CH - 1) / CH, nchB = (nB + CH - 1) / CH;

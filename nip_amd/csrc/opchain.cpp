@@ -20,10 +20,12 @@
 #include "model.h"
 
 #include "chain_kernels.h"
+#include "diag.h"
 #include "nip_amd.h"
 #include "opchain.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -626,8 +628,12 @@ int op_wide_estep(OpPlan* P, const int32_t* d_obs, int n_obs, int B, int T, doub
   const int K = P->K;
   const long R = P->xrow;
   const size_t per = op_wide_scratch_bytes(K, 1, T) + (size_t)T * sizeof(int);
+  size_t budget = (size_t)4 << 30;
+  // diagnostics builds: a smaller message budget, so that tests run one batch
+  // as several launch chunks
+  if (const char* e = diag_env("NIPAMD_OP_WIDE_BYTES")) budget = (size_t)std::atoll(e);
   long chunk = 16;
-  while (chunk < 65536 && (size_t)(chunk * 2) * per <= ((size_t)4 << 30) &&
+  while (chunk < 65536 && (size_t)(chunk * 2) * per <= budget &&
          (size_t)(chunk * 2 / kOpXiSeqs) * R * sizeof(double) <= ((size_t)8 << 30))
     chunk *= 2;
   chunk = std::min<long>(chunk, std::max(16, B));

@@ -152,6 +152,20 @@ def test_gpu_tree_sum_bit_identical_to_pairwise_tree(n, S):
     assert torch.equal(got, want.reshape(-1))
 
 
+@pytest.mark.parametrize("B", [0, 1, 64, 65, 4096, 4097, 131072, 130001])
+def test_estep_tail_is_the_exchange_pack(B):
+    """nipamd_estep_tail (em.iteration's pack): [the pairwise-tree sum of ll,
+    the number of nonzero status words], bit for bit what exchange() packs."""
+    import torch
+    rng = np.random.default_rng(B)
+    ll = torch.tensor(-rng.random(B) * 10.0 ** rng.integers(0, 4, B), dtype=torch.float64)
+    st = torch.tensor(rng.integers(0, 4, B) * (rng.random(B) < 0.01), dtype=torch.int32)
+    out = nip_amd.estep_tail(ll.cuda(), st.cuda()).cpu()
+    want = nem.tree_sum(ll.reshape(-1, 1)).reshape(-1)[0] if B else torch.tensor(0.0, dtype=torch.float64)
+    assert out[0].item() == want.item()
+    assert out[1].item() == float(int((st != 0).sum()))
+
+
 def test_config4_full_shard_counts_vs_textbook():
     """The whole config-4 shard (131072 x 1024) element by element: the
     e_step counts of the full launch (8 chunks of 16384 sequences, the

@@ -151,6 +151,21 @@ def test_wide_op_partial_shard_invariant():
     assert np.array_equal(c1, c4)
 
 
+def test_wide_op_estep_over_launch_chunks():
+    """Several launch chunks per batch (the diagnostics build's lowered message
+    budget, _opwide_chunk_worker.py): the chunk trees combine into the batch
+    tree bit for bit and the counts match the general engine's."""
+    import os
+    import subprocess
+    import sys
+    from nip_amd import build as nb
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "_opwide_chunk_worker.py")],
+                       env=dict(os.environ, NIPAMD_LIB=nb.DIAG_LIB), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "all passed" in r.stdout
+
+
 def test_wide_op_em_learn_matches_general_engine():
     """em_learn on demo1 @ 20 with D1 observed runs its e_step on the wide
     operator chain (no join-tree kernel) and follows the general engine's
