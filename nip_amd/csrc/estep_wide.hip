@@ -742,18 +742,14 @@ __global__ __launch_bounds__(256) void op_wide_post_kernel(OpWideArgs a) {
 // same products as op_fb_kernel's xi_row.  They are summed per operator index
 // c' (Xi'); each leaf's count rows sum the interface posterior gamma_t(y) =
 // alpha^_t beta^_t / sum by the leaf's code at t.
-// A block owns 16 sequences and one slab row (opchain.h).  The group's steps
-// (sequence-major; at most kXwTileMax at a time, the whole group when T <=
-// 1024) are sorted by (key, position) in LDS -- a bitonic sort of packed
-// keys, so every key's steps keep their stream order -- then staged kXwBatch
-// at a time (the weights' two vectors and gamma per step in LDS, f_t by a
-// wave sum) and summed in sorted order: Xi' by a thread per cell (CPT cells
-// each), the leaf rows by a thread per state y.  A fixed summation order,
-// independent of the launch (shard invariance).  An operator index's Xi' sum
-// leaves for the slab row when the sorted stream moves on: a plain store in
-// the first tile (each index once; the row was zeroed by the same thread
-// before), read-add-write in later ones; a key's gamma sum is added to its
-// leaf rows in LDS, written out at the end.
+// A block owns kOpWideSeqs = 8 sequences and one slab row (opchain.h; two
+// blocks per CU).  The group's steps (sequence-major; at most kXwTileMax at a
+// time, the whole group when T <= 2048) are sorted by (key, position) in LDS
+// -- a bitonic sort of packed keys, so every key's steps keep their stream
+// order -- then staged kXwBatch at a time, two batches in flight (the weights'
+// two vectors and gamma per step in LDS, f_t by a wave sum), and summed in
+// sorted order on the matrix cores (below).  A fixed summation order,
+// independent of the launch (shard invariance).
 #ifndef NIPAMD_XI_SKIP
 #define NIPAMD_XI_SKIP 0   // timing-only builds (wrong results): 1 no sort, 2 no sums, 3 no message loads, 4 no keys
 #endif
@@ -766,7 +762,7 @@ static_assert(kXwTileBits + kOpWideKeyBits <= 32, "packed sort key");
 
 // the sorted tile's length: the group's stream rounded up to a power of two
 __host__ __device__ inline int op_xi_tile(int T) {
-  const long n = (long)kOpXiSeqs * T;
+  const long n = (long)kOpWideSeqs * T;
   int L = 64;
   while (L < n && L < kXwTileMax) L <<= 1;
   return L;
@@ -788,12 +784,12 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned key[];   // [op_xi_tile(T)]
   __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP], Gm[kXwBatch][NP];
   __shared__ int kb[kXwBatch];
-  __shared__ double p0s[kOpXiSeqs][64];
+  __shared__ double p0s[kOpWideSeqs][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = a.K, KK = K * K, T = a.T;
   const int L = op_xi_tile(T);
-  const long b0 = (long)blockIdx.x * kOpXiSeqs;
-  const int nseq = (int)((a.B - b0) < kOpXiSeqs ? (a.B - b0) : kOpXiSeqs);
+  const long b0 = (long)blockIdx.x * kOpWideSeqs;
+  const int nseq = (int)((a.B - b0) < kOpWideSeqs ? (a.B - b0) : kOpWideSeqs);
   const int n = nseq * T;
   double* const out = a.slab + (size_t)blockIdx.x * a.xrow;
   // The sums on the matrix cores (v_mfma_f64_16x16x4, the steps as the inner
@@ -1087,7 +1083,7 @@ int xi_launch(const OpWideArgs& a, hipStream_t stream) {
   const size_t lds = (size_t)op_xi_tile(a.T) * sizeof(unsigned);
   static size_t set[kMaxDevices] = {};
   if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP>), lds, set)) return -1;
-  const dim3 g((unsigned)((a.B + kOpXiSeqs - 1) / kOpXiSeqs)), th(kXwThreads);
+  const dim3 g((unsigned)((a.B + kOpWideSeqs - 1) / kOpWideSeqs)), th(kXwThreads);
   hipLaunchKernelGGL((op_wide_xi_kernel<NP>), g, th, lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1096,7 +1092,7 @@ int op_wide_xi_launch(const OpWideArgs& a, hipStream_t stream) {
   if (a.B <= 0) return 0;
   if (a.K > 64 || a.K < 17 || a.oncomb > 65534 || !a.sc || !a.slab || a.Lbits < 0 ||
       ((long)(a.oncomb + 1) << a.Lbits) > (1L << kOpWideKeyBits) ||
-      a.xrow - a.K - (a.oncomb + 1) * a.K * a.K > kOpWideMaxH || (long)kOpXiSeqs * a.T >= (1L << 31))
+      a.xrow - a.K - (a.oncomb + 1) * a.K * a.K > kOpWideMaxH || (long)kOpWideSeqs * a.T >= (1L << 31))
     return -2;
   return op_wide_np(a.K) == 32 ? xi_launch<32>(a, stream) : xi_launch<64>(a, stream);
 }

@@ -634,11 +634,11 @@ int op_wide_estep(OpPlan* P, const int32_t* d_obs, int n_obs, int B, int T, doub
   if (const char* e = diag_env("NIPAMD_OP_WIDE_BYTES")) budget = (size_t)std::atoll(e);
   long chunk = 16;
   while (chunk < 65536 && (size_t)(chunk * 2) * per <= budget &&
-         (size_t)(chunk * 2 / kOpXiSeqs) * R * sizeof(double) <= ((size_t)8 << 30))
+         (size_t)(chunk * 2 / kOpWideSeqs) * R * sizeof(double) <= ((size_t)8 << 30))
     chunk *= 2;
   chunk = std::min<long>(chunk, std::max(16, B));
   const long nchunks = (B + chunk - 1) / chunk;
-  const long rows = (chunk + kOpXiSeqs - 1) / kOpXiSeqs;
+  const long rows = (chunk + kOpWideSeqs - 1) / kOpWideSeqs;
   const long lvl = (rows + 63) / 64;
   const size_t nsc = ((size_t)chunk * T * sizeof(int) + sizeof(double) - 1) / sizeof(double);
   const size_t nE = nsc + (size_t)(rows + 2 * lvl + nchunks + 2 * ((nchunks + 63) / 64) + 1) * R;
@@ -685,7 +685,7 @@ int op_wide_estep(OpPlan* P, const int32_t* d_obs, int n_obs, int B, int T, doub
       err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError());
       return NIPAMD_ERROR_DEVICE;
     }
-    const long nr = (nb + kOpXiSeqs - 1) / kOpXiSeqs;
+    const long nr = (nb + kOpWideSeqs - 1) / kOpWideSeqs;
     if (nipamd_tree_sum(slab, nr, (int)R, work, nchunks == 1 ? out : cres + (size_t)c * R, st)) {
       err = "tree launch failed";
       return NIPAMD_ERROR_DEVICE;

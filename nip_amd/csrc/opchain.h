@@ -149,6 +149,7 @@ struct OpWideArgs {
   int hoff[kOpMaxLeaf];
   int xrow;
 };
+constexpr int kOpWideSeqs = 8;         // op_wide_xi_kernel: sequences per block and slab row
 constexpr int kOpWideMaxH = 2048;      // doubles of leaf count rows (op_wide_xi_kernel's LDS)
 constexpr int kOpWideKeyBits = 18;     // (oncomb + 1) << Lbits <= 2^18
 inline int op_wide_np(int K) { return K <= 32 ? 32 : 64; }
