@@ -779,7 +779,7 @@ __device__ __forceinline__ int op_key(const OpWideArgs& a, const int32_t* o) {
   return k;
 }
 
-template <int NP>
+template <int NP, int TPW>
 __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned key[];   // [op_xi_tile(T)]
   __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP], Gm[kXwBatch][NP];
@@ -800,11 +800,11 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
   // the leaves' in leaf order.  An MFMA ignores EXEC, so steps outside a sum
   // enter as zero A operands, never by branching.
   constexpr int NT = NP / 16;
-  constexpr int TPW = NT == 2 ? 4 : 6;
   int tkind[TPW], tx[TPW], ty[TPW], tj[TPW];      // kind 0 none, 1 Xi' (x tile, y tile), 2 leaf (j, row tile, y tile)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);   // (so that every tile parameter is wave-uniform)
 #pragma unroll
   for (int i = 0; i < TPW; i++) {
-    int ti = wave + kXwWaves * i;
+    int ti = wv + kXwWaves * i;
     tkind[i] = 0; tx[i] = 0; ty[i] = 0; tj[i] = 0;
     if (ti < NT * NT) {
       tkind[i] = 1; tx[i] = ti / NT; ty[i] = ti % NT;
@@ -861,24 +861,33 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     cur = -1;
   };
   // the MFMAs of the batch's steps [k0, k1): Xi' tiles (xi) and / or leaf tiles (h)
-  constexpr int GU = NT == 2 ? 8 : 2;              // step groups unrolled (registers at 64 lanes)
+  constexpr int GU = (NT == 2 && TPW <= 2) ? 8 : 2;   // step groups unrolled (registers)
+  // Branch-free over the wave's tiles (every tile parameter is wave-uniform):
+  // a group's operands are read for all of them first, then their MFMAs issue
+  // back to back; a step outside [k0, k1) or a sum not asked for enters as a
+  // zero A operand.
   auto mfma_pass = [&](int k0, int k1, bool xi, bool h) __attribute__((always_inline)) {
 #pragma unroll GU
     for (int g = 0; g < kXwBatch / 4; g++) {
       const int k = 4 * g + lk;
       const bool in = k >= k0 && k < k1;
       const int kc = kb[k];
+      double av[TPW], bv[TPW];
 #pragma unroll
       for (int i = 0; i < TPW; i++) {
-        if (xi && tkind[i] == 1) {
-          const double av = Ab[k][16 * tx[i] + li], bv = Gb[k][16 * ty[i] + li];
-          D[i] = mfma(in ? av : 0.0, bv, D[i]);
-        } else if (h && tkind[i] == 2) {
-          const int r = (kc >> tsh[i]) & tmk[i];
-          const double bv = Gm[k][16 * ty[i] + li];
-          D[i] = mfma(in && r == 16 * tx[i] + li ? 1.0 : 0.0, bv, D[i]);
-        }
+        const bool isx = tkind[i] == 1;
+        const int col = 16 * ty[i] + li;
+        const int xcol = min(16 * tx[i] + li, NP - 1);
+        const double ax = Ab[k][xcol];
+        bv[i] = isx ? Gb[k][col] : Gm[k][col];
+        const int r = (kc >> tsh[i]) & tmk[i];
+        const bool hot = r == 16 * tx[i] + li;
+        av[i] = (in && tkind[i] != 0) ? (isx ? (xi ? ax : 0.0) : (h && hot ? 1.0 : 0.0)) : 0.0;
       }
+      // every slot's MFMA issues (an empty slot multiplies zeros): no branch
+      // around a matrix instruction
+#pragma unroll
+      for (int i = 0; i < TPW; i++) D[i] = mfma(av[i], bv[i], D[i]);
     }
   };
   constexpr int SPW = 64 / NP;
@@ -985,6 +994,12 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
         k0 = k1;
       }
     };
+    // a barrier that waits for LDS only: __syncthreads() also waits for every
+    // outstanding global load (s_waitcnt vmcnt(0)), which would drain the
+    // next batches' prefetches at every hand-over
+    auto lds_barrier = [] __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
     const std::integral_constant<int, 0> pa{};
     const std::integral_constant<int, 1> pb{};
     load_batch(0, pa);
@@ -992,17 +1007,17 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     if (kXwBatch < m) load_batch(kXwBatch, pa);
     for (int j0 = 0; j0 < m; j0 += 2 * kXwBatch) {
       // batch j0 in LDS, batch j0 + 32 in register set 0
-      __syncthreads();
+      lds_barrier();
       if (j0 + 2 * kXwBatch < m) load_batch(j0 + 2 * kXwBatch, pb);
       accumulate(j0);
-      __syncthreads();
+      lds_barrier();
       if (j0 + kXwBatch >= m) break;
       store_batch(pa);
       // batch j0 + 32 in LDS, batch j0 + 64 in register set 1
-      __syncthreads();
+      lds_barrier();
       if (j0 + 3 * kXwBatch < m) load_batch(j0 + 3 * kXwBatch, pa);
       accumulate(j0 + kXwBatch);
-      __syncthreads();
+      lds_barrier();
       if (j0 + 2 * kXwBatch < m) store_batch(pb);
     }
     flush(i0 == 0);
@@ -1073,19 +1088,29 @@ int op_wide_launch(const OpWideArgs& a, hipStream_t stream) {
   return op_wide_np(a.K) == 32 ? msgs_launch<32>(a, stream) : msgs_launch<64>(a, stream);
 }
 
-template <int NP>
-int xi_launch(const OpWideArgs& a, hipStream_t stream) {
-  // every MFMA tile needs an accumulator slot: NT^2 Xi' tiles + the leaves'
-  constexpr int NT = NP / 16, TPW = NT == 2 ? 4 : 6;
-  int tiles = NT * NT;
-  for (int j = 0; j < a.nleaf; j++) tiles += (a.lcard[j] + 2 + 15) / 16 * NT;
-  if (tiles > kXwWaves * TPW) return -2;
+template <int NP, int TPW>
+int xi_launch_t(const OpWideArgs& a, hipStream_t stream) {
   const size_t lds = (size_t)op_xi_tile(a.T) * sizeof(unsigned);
   static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP>), lds, set)) return -1;
+  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP, TPW>), lds, set)) return -1;
   const dim3 g((unsigned)((a.B + kOpWideSeqs - 1) / kOpWideSeqs)), th(kXwThreads);
-  hipLaunchKernelGGL((op_wide_xi_kernel<NP>), g, th, lds, stream, a);
+  hipLaunchKernelGGL((op_wide_xi_kernel<NP, TPW>), g, th, lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// accumulator slots per wave: the NT^2 Xi' tiles and the leaves' tiles over
+// the block's waves (an empty slot costs an MFMA on zeros)
+template <int NP>
+int xi_launch(const OpWideArgs& a, hipStream_t stream) {
+  constexpr int NT = NP / 16;
+  int tiles = NT * NT;
+  for (int j = 0; j < a.nleaf; j++) tiles += (a.lcard[j] + 2 + 15) / 16 * NT;
+  if (tiles <= 2 * kXwWaves) return xi_launch_t<NP, 2>(a, stream);
+  if (tiles <= 4 * kXwWaves) return xi_launch_t<NP, 4>(a, stream);
+  if constexpr (NP == 64) {
+    if (tiles <= 6 * kXwWaves) return xi_launch_t<NP, 6>(a, stream);
+  }
+  return -2;
 }
 
 int op_wide_xi_launch(const OpWideArgs& a, hipStream_t stream) {
