@@ -779,8 +779,23 @@ __device__ __forceinline__ int op_key(const OpWideArgs& a, const int32_t* o) {
   return k;
 }
 
+// Per instantiation: batches in flight (register sets), step groups unrolled
+// and the waves per SIMD the registers are held to.  At 16 states per tile
+// pair and two slots per wave (NP = 32, TPW = 2: the 17..32-state case) one batch in flight keeps
+// the kernel within 128 registers: two blocks, four waves per SIMD, which
+// beats two batches in flight at one block per CU (5.73 -> 4.97 ms,
+// profiles/r05/gpu/r05u_ab_estep_opchain_wide.txt)
 template <int NP, int TPW>
-__global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
+struct XiCfg {
+  static constexpr int pipe = 2, gu = 2, wpe = 1;
+};
+template <>
+struct XiCfg<32, 2> {
+  static constexpr int pipe = 1, gu = 2, wpe = 4;
+};
+
+template <int NP, int TPW>
+__global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCfg<NP, TPW>::wpe))) void op_wide_xi_kernel(OpWideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned key[];   // [op_xi_tile(T)]
   __shared__ double Ab[kXwBatch][NP], Gb[kXwBatch][NP], Gm[kXwBatch][NP];
   __shared__ int kb[kXwBatch];
@@ -861,7 +876,7 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     cur = -1;
   };
   // the MFMAs of the batch's steps [k0, k1): Xi' tiles (xi) and / or leaf tiles (h)
-  constexpr int GU = (NT == 2 && TPW <= 2) ? 8 : 2;   // step groups unrolled (registers)
+  constexpr int GU = XiCfg<NP, TPW>::gu;              // step groups unrolled
   // Branch-free over the wave's tiles (every tile parameter is wave-uniform):
   // a group's operands are read for all of them first, then their MFMAs issue
   // back to back; a step outside [k0, k1) or a sum not asked for enters as a
@@ -918,7 +933,8 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
       }
     // Staging, software-pipelined: the next batch's loads (messages, scale
     // exponent, leaf factors -- all addressed from the sorted key alone) are
-    // issued before this batch's sums and land in LDS after them.  Wave w
+    // issued before this batch's sums and land in LDS after them (XiCfg::pipe
+    // batches in flight).  Wave w
     // stages slots SL_w .. SL_w + SL - 1, 64 / NP per pass.
     constexpr int SL = kXwBatch / kXwWaves / SPW;
     // two batches in flight: the one in LDS is summed while the next one's
@@ -926,9 +942,9 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     // the other (the random-order message reads are latency-bound)
     // (register sets indexed by a compile-time buffer number: a struct passed
     // by reference would live in scratch)
-    double P_at[2][SL], P_bt[2][SL], P_ap[2][SL], P_e[2][SL];
-    int P_sc[2][SL], P_kc[2][SL];
-    bool P_ok[2][SL];
+    constexpr int NPB = XiCfg<NP, TPW>::pipe;
+    double P_at[NPB][SL], P_bt[NPB][SL], P_ap[NPB][SL], P_e[NPB][SL];
+    int P_sc[NPB][SL], P_kc[NPB][SL];              // P_kc: the key's code, -1 past the tile's end
     auto load_batch = [&](int j0, auto buf) __attribute__((always_inline)) {
       constexpr int u = decltype(buf)::value;
 #pragma unroll
@@ -947,8 +963,7 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
         P_ap[u][q] = on ? (t > 0 ? sa[-NP] : a.pi[y]) : 0.0;
         P_sc[u][q] = ok ? a.sc[(size_t)b * T + t] : 0;
         const int kc = (int)(v >> kXwTileBits);
-        P_kc[u][q] = kc;
-        P_ok[u][q] = ok;
+        P_kc[u][q] = ok ? kc : -1;
         // the leaf factors from the key's codes (no observation re-read), in
         // op_leaf_e's order
         double e = 1.0;
@@ -970,7 +985,7 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
         Ab[jj][y] = P_ap[u][q];
         Gb[jj][y] = P_bt[u][q] * P_e[u][q] * __builtin_ldexp(rz, P_sc[u][q]);
         Gm[jj][y] = pr * rz;
-        if (y == 0) kb[jj] = P_ok[u][q] ? P_kc[u][q] : -1;
+        if (y == 0) kb[jj] = P_kc[u][q];
       }
     };
     auto accumulate = [&](int j0) __attribute__((always_inline)) {
@@ -1002,23 +1017,35 @@ __global__ __launch_bounds__(kXwThreads) void op_wide_xi_kernel(OpWideArgs a) {
     };
     const std::integral_constant<int, 0> pa{};
     const std::integral_constant<int, 1> pb{};
-    load_batch(0, pa);
-    store_batch(pa);
-    if (kXwBatch < m) load_batch(kXwBatch, pa);
-    for (int j0 = 0; j0 < m; j0 += 2 * kXwBatch) {
-      // batch j0 in LDS, batch j0 + 32 in register set 0
-      lds_barrier();
-      if (j0 + 2 * kXwBatch < m) load_batch(j0 + 2 * kXwBatch, pb);
-      accumulate(j0);
-      lds_barrier();
-      if (j0 + kXwBatch >= m) break;
+    if constexpr (NPB == 1) {
+      // one batch in flight: its loads are issued before the batch in LDS is summed
+      load_batch(0, pa);
+      for (int j0 = 0; j0 < m; j0 += kXwBatch) {
+        store_batch(pa);
+        lds_barrier();
+        if (j0 + kXwBatch < m) load_batch(j0 + kXwBatch, pa);
+        accumulate(j0);
+        lds_barrier();
+      }
+    } else {
+      load_batch(0, pa);
       store_batch(pa);
-      // batch j0 + 32 in LDS, batch j0 + 64 in register set 1
-      lds_barrier();
-      if (j0 + 3 * kXwBatch < m) load_batch(j0 + 3 * kXwBatch, pa);
-      accumulate(j0 + kXwBatch);
-      lds_barrier();
-      if (j0 + 2 * kXwBatch < m) store_batch(pb);
+      if (kXwBatch < m) load_batch(kXwBatch, pa);
+      for (int j0 = 0; j0 < m; j0 += 2 * kXwBatch) {
+        // batch j0 in LDS, batch j0 + 32 in register set 0
+        lds_barrier();
+        if (j0 + 2 * kXwBatch < m) load_batch(j0 + 2 * kXwBatch, pb);
+        accumulate(j0);
+        lds_barrier();
+        if (j0 + kXwBatch >= m) break;
+        store_batch(pa);
+        // batch j0 + 32 in LDS, batch j0 + 64 in register set 1
+        lds_barrier();
+        if (j0 + 3 * kXwBatch < m) load_batch(j0 + 3 * kXwBatch, pa);
+        accumulate(j0 + kXwBatch);
+        lds_barrier();
+        if (j0 + 2 * kXwBatch < m) store_batch(pb);
+      }
     }
     flush(i0 == 0);
   }
