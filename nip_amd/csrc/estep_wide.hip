@@ -562,12 +562,39 @@ __device__ __forceinline__ double op_leaf_e(const OpWideArgs& a, const int32_t* 
 }
 
 typedef __attribute__((address_space(3))) double op_lds_d;
+typedef double op_d2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) op_d2 op_lds_d2;
+
+// op_wide_msgs_kernel's LDS row stride: K rounded up to 2 mod 4 entries
+__host__ __device__ inline int op_lds_row(int K) { return (K + 1) / 4 * 4 + 2; }
+// ... and its LDS copy's length: (oncomb + 1) operators of K rows, NP - K
+// zero rows, NP zeros (the last lane's reads run NP entries from its row)
+__host__ __device__ inline int op_lds_doubles(int oncomb, int K, int NP) {
+  return (oncomb * K + NP) * op_lds_row(K) + NP;
+}
+
+// op_wide_msgs_kernel per width: waves per block, steps of evidence prepared
+// a chunk ahead, and the waves per SIMD the registers are held to.  The
+// operators' LDS copy is staged once per block and at most two blocks fit a
+// CU, so at NP = 32 the block is wide (8 waves) and a 3-step chunk keeps it
+// within 128 registers: four waves per SIMD (estep_opchain_wide 3.95 ->
+// 3.46 ms, opchain_wide 2.46 -> 1.97 ms: profiles/r05/gpu/r05x_*).  At NP = 64
+// (64 coefficient registers more) the narrow block stays.
+template <int NP>
+struct MsgCfg {
+  static constexpr int waves = 4, chunk = 8, wpe = 1;
+};
+template <>
+struct MsgCfg<32> {
+  static constexpr int waves = 8, chunk = 3, wpe = 4;
+};
 
 template <int NP, bool TL>
-__global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs a) {
+__global__ __launch_bounds__(MsgCfg<NP>::waves * 64) __attribute__((amdgpu_waves_per_eu(MsgCfg<NP>::wpe))) void op_wide_msgs_kernel(OpWideArgs a) {
+  constexpr int kOpMsgWaves = MsgCfg<NP>::waves, kOpMsgChunk = MsgCfg<NP>::chunk;
   extern __shared__ __attribute__((aligned(16))) unsigned char op_smem[];
   constexpr int SPW = 64 / NP, NB = NP / 16;
-  constexpr int SPB = kMsgWaves * SPW;                      // sequences per block
+  constexpr int SPB = kOpMsgWaves * SPW;                      // sequences per block
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T, K = a.K, KK = K * K;
   // blocks [0, nbd) run forward filters, [nbd, 2 nbd) backward ones: each
@@ -578,9 +605,19 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
   const bool fwd = (int)blockIdx.x < nbd;
   const int blk = fwd ? (int)blockIdx.x : (int)blockIdx.x - nbd;
   const double* const src = fwd ? a.TtabT : a.Ttab;         // [(oncomb + 1)][K][K] + NP zeros
-  op_lds_d* const Tl = (op_lds_d*)(op_smem);                 // TL: the same in LDS
+  // TL: the same in LDS, rows padded to Kp = op_lds_row(K) entries (zeros),
+  // and NP - K zero rows after the last operator: every lane reads its own
+  // row (lanes y >= K too), so a lane's 16-byte reads fall on distinct bank
+  // slots across every 16-lane group of ds_read_b128 (the row stride is an
+  // odd number of slots)
+  op_lds_d* const Tl = (op_lds_d*)(op_smem);
+  const int Kp = TL ? op_lds_row(K) : K;
   if (TL) {
-    for (int i = tid; i < (a.oncomb + 1) * KK + NP; i += kMsgWaves * 64) Tl[i] = src[i];
+    const int rows = (a.oncomb + 1) * K;
+    for (int i = tid; i < op_lds_doubles(a.oncomb, K, NP); i += kOpMsgWaves * 64) {
+      const int r = i / Kp, x = i - r * Kp;
+      Tl[i] = (r < rows && x < K) ? src[r * K + x] : 0.0;
+    }
     __syncthreads();
   }
   const int s = lane / NP, y = lane % NP;
@@ -597,12 +634,12 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
   // a chunk's 8 steps at once (t = t0 + dir * (j + k)): each observed
   // column's 8 loads issue together, then the leaves' table loads -- two
   // waits per column and chunk, not a chain of dependent loads per step
-  auto prep = [&](int j, int (&code)[kMsgChunk], double (&e)[kMsgChunk]) {
-    int c[kMsgChunk];
-    bool ev[kMsgChunk], oor[kMsgChunk], in[kMsgChunk];
-    const int32_t* o[kMsgChunk];
+  auto prep = [&](int j, int (&code)[kOpMsgChunk], double (&e)[kOpMsgChunk]) {
+    int c[kOpMsgChunk];
+    bool ev[kOpMsgChunk], oor[kOpMsgChunk], in[kOpMsgChunk];
+    const int32_t* o[kOpMsgChunk];
 #pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) {
+    for (int k = 0; k < kOpMsgChunk; k++) {
       const int t = t0 + dir * (j + k);
       in[k] = obs && t >= 0 && t < T;
       o[k] = obs + (long)(in[k] ? t : 0) * a.obs_tstride;
@@ -610,11 +647,11 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
     }
     for (int q = 0; q < a.onobs; q++) {
       const int col = a.ocol[q], card = a.ocard[q], st = a.ocstride[q];
-      int v[kMsgChunk];
+      int v[kOpMsgChunk];
 #pragma unroll
-      for (int k = 0; k < kMsgChunk; k++) v[k] = in[k] ? o[k][col] : -1;
+      for (int k = 0; k < kOpMsgChunk; k++) v[k] = in[k] ? o[k][col] : -1;
 #pragma unroll
-      for (int k = 0; k < kMsgChunk; k++) {
+      for (int k = 0; k < kOpMsgChunk; k++) {
         oor[k] |= v[k] >= card;
         ev[k] |= v[k] >= 0;
         if (v[k] >= 0) c[k] += (v[k] + 1) * st;
@@ -623,31 +660,43 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
     for (int q = 0; q < a.nleaf; q++) {
       const int col = a.lcol[q], M = a.lcard[q];
       const double* lt = a.ltab + a.loff[q] + yc;
-      int v[kMsgChunk];
+      int v[kOpMsgChunk];
 #pragma unroll
-      for (int k = 0; k < kMsgChunk; k++) v[k] = in[k] ? o[k][col] : -1;
+      for (int k = 0; k < kOpMsgChunk; k++) v[k] = in[k] ? o[k][col] : -1;
 #pragma unroll
-      for (int k = 0; k < kMsgChunk; k++) {
+      for (int k = 0; k < kOpMsgChunk; k++) {
         ev[k] |= v[k] >= 0;
         const int r = v[k] < 0 ? M : (v[k] < M ? v[k] : M + 1);
         e[k] *= in[k] ? lt[r * K] : 1.0;
       }
     }
 #pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) code[k] = (oor[k] ? a.oncomb : c[k]) | (ev[k] ? kOpEv : 0);
+    for (int k = 0; k < kOpMsgChunk; k++) code[k] = (oor[k] ? a.oncomb : c[k]) | (ev[k] ? kOpEv : 0);
   };
   // this lane's column (forward) / row (backward) of T'_c, in 16-state
   // blocks: entries x >= K read the next row or the padding (finite), and
   // meet x = 0 in the mat-vec; lanes y >= K read row 0 and are zeroed after
   auto coef = [&](int code, double (&C)[NB][16]) {
-    const int base = (code & (kOpEv - 1)) * KK + yc * K;
+    const int base = (code & (kOpEv - 1)) * K * Kp + (TL ? y : yc) * Kp;
+    if (TL) {
+      const op_lds_d2* const p = (const op_lds_d2*)(Tl + base);   // 16-byte aligned: Kp even
 #pragma unroll
-    for (int k = 0; k < NB; k++)
+      for (int k = 0; k < NB; k++)
 #pragma unroll
-      for (int j = 0; j < 16; j++) C[k][j] = TL ? (double)Tl[base + 16 * k + j] : src[base + 16 * k + j];
+        for (int j = 0; j < 8; j++) {
+          const op_d2 v = p[8 * k + j];
+          C[k][2 * j] = v.x;
+          C[k][2 * j + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int j = 0; j < 16; j++) C[k][j] = src[base + 16 * k + j];
+    }
   };
-  int cc[kMsgChunk], cn[kMsgChunk];
-  double ec[kMsgChunk], en[kMsgChunk];
+  int cc[kOpMsgChunk], cn[kOpMsgChunk];
+  double ec[kOpMsgChunk], en[kOpMsgChunk];
   prep(0, cc, ec);
   double x;
   int sc = 0;
@@ -666,16 +715,16 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
   coef(cc[0], C);
   // forward: steps t = 0..T-1; backward: t = T-1..1 (each making beta_{t-1})
   const int n = fwd ? T : T - 1;
-  for (int j0 = 0; j0 < n; j0 += kMsgChunk) {
-    prep(j0 + kMsgChunk, cn, en);
+  for (int j0 = 0; j0 < n; j0 += kOpMsgChunk) {
+    prep(j0 + kOpMsgChunk, cn, en);
 #pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) {
+    for (int k = 0; k < kOpMsgChunk; k++) {
       const int j = j0 + k;
       if (j >= n) break;
       const int t = t0 + dir * j;
       const double m1v = fwd ? group_sum<NP>(x * wy) : 0.0;
       const double acc = matvec_dpp<NB>(fwd ? x : x * ec[k], C);
-      coef(k + 1 < kMsgChunk ? cc[k + 1] : cn[0], C);   // the next step's operator, under this step's work
+      coef(k + 1 < kOpMsgChunk ? cc[k + 1] : cn[0], C);   // the next step's operator, under this step's work
       double u = ys ? __builtin_ldexp(acc, sc) : 0.0;
       if (fwd) u *= ec[k];
       const double z = group_sum<NP>(u);
@@ -700,7 +749,7 @@ __global__ __launch_bounds__(kMsgWaves * 64) void op_wide_msgs_kernel(OpWideArgs
       x = u;
     }
 #pragma unroll
-    for (int k = 0; k < kMsgChunk; k++) {
+    for (int k = 0; k < kOpMsgChunk; k++) {
       cc[k] = cn[k];
       ec[k] = en[k];
     }
@@ -1084,16 +1133,15 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
 
 }  // namespace
 
-// the operators in LDS while two blocks per CU still fit (op_wide_msgs_kernel
-// runs two waves per SIMD)
-constexpr size_t kOpWideTl = 76 * 1024;
+// the operators in LDS (padded rows) while two blocks per CU still fit
+constexpr size_t kOpWideTl = 80 * 1024;
 
 template <int NP>
 int msgs_launch(const OpWideArgs& a, hipStream_t stream) {
-  const int spb = kMsgWaves * (64 / NP);
+  const int spb = MsgCfg<NP>::waves * (64 / NP);
   const int nbd = (int)((a.B + spb - 1) / spb);
-  const dim3 g((unsigned)(a.filter ? nbd : 2 * nbd)), th(kMsgWaves * 64);
-  const size_t tl = ((size_t)(a.oncomb + 1) * a.K * a.K + NP) * sizeof(double);
+  const dim3 g((unsigned)(a.filter ? nbd : 2 * nbd)), th(MsgCfg<NP>::waves * 64);
+  const size_t tl = (size_t)op_lds_doubles(a.oncomb, a.K, NP) * sizeof(double);
   if (tl <= kOpWideTl) {
     static size_t set[kMaxDevices] = {};
     if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_msgs_kernel<NP, true>), tl, set)) return -1;
