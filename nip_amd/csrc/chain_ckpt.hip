@@ -422,11 +422,13 @@ __device__ __forceinline__ void ck_partner(const ChainArgs& a, double* out, doub
 
 template <int PROJ>
 #ifndef NIPAMD_CK_PRIO
-// 3: the partners at s_setprio 1 and the filters at 2, above the posterior
-// wave sharing their SIMD: -3.6% (0.2476 vs 0.2569 ms) in 5 of 5 interleaved
-// pairs and 4 of 4 on a second box (profiles/r05/gpu/r05q_ab_fb.txt,
-// r05o_ab_fb_ckprio3.txt); 2: the partners only (round 4)
-#define NIPAMD_CK_PRIO 3
+// 5: the filters at s_setprio 2, the recompute waves at 1, the partners at 0:
+// -1.2% against 3 in 10 of 12 interleaved pairs (profiles/r05/gpu/r05af_ab_fb_prio.txt,
+// r05ag_ab_fb_prio.txt; phase B's binding wave is the beta recompute).
+// 3: the partners at 1 and the filters at 2: -3.6% against 2 in 5 of 5 pairs
+// and 4 of 4 on a second box (r05q_ab_fb.txt, r05o_ab_fb_ckprio3.txt);
+// 2: the partners only (round 4)
+#define NIPAMD_CK_PRIO 5
 #endif
 __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -478,9 +480,14 @@ __global__ __launch_bounds__(kCThreads, 1) void chain_fb_ckpt_kernel(ChainArgs a
     return;
   }
   // A/B builds: static wave priority for the recompute waves (1) or the partners (2)
+  // (4: filters 2, partners and recompute waves 1; 5: filters 2, recompute 1,
+  // partners 0; 6: filters and recompute waves 2, partners 1)
   if ((NIPAMD_CK_PRIO == 1 && wave >= 6) || ((NIPAMD_CK_PRIO == 2 || NIPAMD_CK_PRIO == 3) && role >= 2 && wave < 4))
     __builtin_amdgcn_s_setprio(1);
-  if (NIPAMD_CK_PRIO == 3 && wave < 2) __builtin_amdgcn_s_setprio(2);
+  if (NIPAMD_CK_PRIO >= 3 && wave < 2) __builtin_amdgcn_s_setprio(2);
+  if ((NIPAMD_CK_PRIO == 4 || NIPAMD_CK_PRIO == 6) && role >= 2 && wave < 4) __builtin_amdgcn_s_setprio(1);
+  if ((NIPAMD_CK_PRIO == 4 || NIPAMD_CK_PRIO == 5) && wave >= 6) __builtin_amdgcn_s_setprio(1);
+  if (NIPAMD_CK_PRIO == 6 && wave >= 6) __builtin_amdgcn_s_setprio(2);
   if (role >= 2 && wave < 4) {
     if (fwd) ck_partner<true, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
     else ck_partner<false, PROJ>(a, ring, rring, zr, Sblk, lane, b0, nchA, nchB, dg);
