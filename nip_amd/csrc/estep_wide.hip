@@ -833,14 +833,15 @@ __device__ __forceinline__ int op_key(const OpWideArgs& a, const int32_t* o) {
 // pair and two slots per wave (NP = 32, TPW = 2: the 17..32-state case) one batch in flight keeps
 // the kernel within 128 registers: two blocks, four waves per SIMD, which
 // beats two batches in flight at one block per CU (5.73 -> 4.97 ms,
-// profiles/r05/gpu/r05u_ab_estep_opchain_wide.txt)
+// profiles/r05/gpu/r05u_ab_estep_opchain_wide.txt); with the empty slots
+// skipped, one step group per iteration (3.50 -> 3.29 ms, r05ai_*)
 template <int NP, int TPW>
 struct XiCfg {
   static constexpr int pipe = 2, gu = 2, wpe = 1;
 };
 template <>
 struct XiCfg<32, 2> {
-  static constexpr int pipe = 1, gu = 2, wpe = 4;
+  static constexpr int pipe = 1, gu = 1, wpe = 4;
 };
 
 template <int NP, int TPW>
@@ -896,6 +897,9 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
   v4d D[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; i++) D[i] = v4d{0.0, 0.0, 0.0, 0.0};
+  int na = 0;                                      // slots with a tile (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < TPW; i++) na += tkind[i] != 0;
   const int li = lane & 15, lk = lane >> 4;
   // the row's Xi' part zeroed by the lanes that own its cells (each cell is
   // later written, or read and written, by the same lane only)
@@ -930,15 +934,18 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
   // a group's operands are read for all of them first, then their MFMAs issue
   // back to back; a step outside [k0, k1) or a sum not asked for enters as a
   // zero A operand.
-  auto mfma_pass = [&](int k0, int k1, bool xi, bool h) __attribute__((always_inline)) {
+  // NA: the wave's slots that hold a tile (a prefix of its TPW slots); the
+  // empty ones take no operands and no MFMAs
+  auto mfma_pass_n = [&](int k0, int k1, bool xi, bool h, auto na_c) __attribute__((always_inline)) {
+    constexpr int NA = decltype(na_c)::value;
 #pragma unroll GU
     for (int g = 0; g < kXwBatch / 4; g++) {
       const int k = 4 * g + lk;
       const bool in = k >= k0 && k < k1;
       const int kc = kb[k];
-      double av[TPW], bv[TPW];
+      double av[NA], bv[NA];
 #pragma unroll
-      for (int i = 0; i < TPW; i++) {
+      for (int i = 0; i < NA; i++) {
         const bool isx = tkind[i] == 1;
         const int col = 16 * ty[i] + li;
         const int xcol = min(16 * tx[i] + li, NP - 1);
@@ -946,14 +953,24 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
         bv[i] = isx ? Gb[k][col] : Gm[k][col];
         const int r = (kc >> tsh[i]) & tmk[i];
         const bool hot = r == 16 * tx[i] + li;
-        av[i] = (in && tkind[i] != 0) ? (isx ? (xi ? ax : 0.0) : (h && hot ? 1.0 : 0.0)) : 0.0;
+        av[i] = in ? (isx ? (xi ? ax : 0.0) : (h && hot ? 1.0 : 0.0)) : 0.0;
       }
-      // every slot's MFMA issues (an empty slot multiplies zeros): no branch
-      // around a matrix instruction
+      // every held slot's MFMA issues: no lane-varying branch around a
+      // matrix instruction
 #pragma unroll
-      for (int i = 0; i < TPW; i++) D[i] = mfma(av[i], bv[i], D[i]);
+      for (int i = 0; i < NA; i++) D[i] = mfma(av[i], bv[i], D[i]);
     }
   };
+#define NIPAMD_XI_NA(n)                                                        \
+  if constexpr (TPW >= n)                                                      \
+    if (na == n) {                                                             \
+      mfma_pass_n(k0, k1, xi, h, std::integral_constant<int, n>{});            \
+      return;                                                                  \
+    }
+  auto mfma_pass = [&](int k0, int k1, bool xi, bool h) __attribute__((always_inline)) {
+    NIPAMD_XI_NA(1) NIPAMD_XI_NA(2) NIPAMD_XI_NA(3) NIPAMD_XI_NA(4) NIPAMD_XI_NA(5) NIPAMD_XI_NA(6)
+  };
+#undef NIPAMD_XI_NA
   constexpr int SPW = 64 / NP;
   const int y = lane % NP;
   const bool ys = y < K;
