@@ -974,8 +974,13 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
   constexpr int SPW = 64 / NP;
   const int y = lane % NP;
   const bool ys = y < K;
+#ifndef NIPAMD_XI_STAMPS
+#define NIPAMD_XI_STAMPS 0   // timing builds: block 0 prints its phase cycles (keys, sort, sums)
+#endif
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0;
   for (int i0 = 0; i0 < n; i0 += L) {
     const int m = (n - i0) < L ? (n - i0) : L;
+    if (NIPAMD_XI_STAMPS) st0 = __builtin_readcyclecounter();
     for (int i = tid; i < L; i += kXwThreads) {
       unsigned v = 0xFFFFFFFFu;                       // padding sorts last
       if (i < m) {
@@ -986,6 +991,7 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
       key[i] = v;
     }
     __syncthreads();
+    if (NIPAMD_XI_STAMPS) st1 = __builtin_readcyclecounter();
     for (int k2 = 2; k2 <= (NIPAMD_XI_SKIP == 1 ? 1 : L); k2 <<= 1)
       for (int j = k2 >> 1; j > 0; j >>= 1) {
         for (int i = tid; i < L; i += kXwThreads) {
@@ -997,6 +1003,7 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
         }
         __syncthreads();
       }
+    if (NIPAMD_XI_STAMPS) st2 = __builtin_readcyclecounter();
     // Staging, software-pipelined: the next batch's loads (messages, scale
     // exponent, leaf factors -- all addressed from the sorted key alone) are
     // issued before this batch's sums and land in LDS after them (XiCfg::pipe
@@ -1086,13 +1093,31 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
     if constexpr (NPB == 1) {
       // one batch in flight: its loads are issued before the batch in LDS is summed
       load_batch(0, pa);
+      unsigned long long cs = 0, cb1 = 0, cl = 0, ca = 0, cb2 = 0, tq = 0;
+      auto lap = [&](unsigned long long& acc) __attribute__((always_inline)) {
+        if (NIPAMD_XI_STAMPS) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          const unsigned long long t = __builtin_readcyclecounter();
+          acc += t - tq;
+          tq = t;
+        }
+      };
+      if (NIPAMD_XI_STAMPS) tq = __builtin_readcyclecounter();
       for (int j0 = 0; j0 < m; j0 += kXwBatch) {
         store_batch(pa);
+        lap(cs);
         lds_barrier();
+        lap(cb1);
         if (j0 + kXwBatch < m) load_batch(j0 + kXwBatch, pa);
+        if (NIPAMD_XI_STAMPS == 2) lap(cl);
         accumulate(j0);
+        lap(ca);
         lds_barrier();
+        lap(cb2);
       }
+      if (NIPAMD_XI_STAMPS && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2) && lane == 0)
+        printf("[xi] block %d wave %d: store %llu bar1 %llu loads %llu accum %llu bar2 %llu\n", (int)blockIdx.x, wave,
+               cs, cb1, cl, ca, cb2);
     } else {
       load_batch(0, pa);
       store_batch(pa);
@@ -1114,6 +1139,12 @@ __global__ __launch_bounds__(kXwThreads) __attribute__((amdgpu_waves_per_eu(XiCf
       }
     }
     flush(i0 == 0);
+    if (NIPAMD_XI_STAMPS) {
+      st3 = __builtin_readcyclecounter();
+      if ((blockIdx.x == 0 || blockIdx.x == gridDim.x / 2) && tid == 0)
+        printf("[xi] block %d tile %d: keys %llu sort %llu sums %llu cycles (m %d)\n", (int)blockIdx.x, i0 / L,
+               st1 - st0, st2 - st1, st3 - st2, m);
+    }
   }
   // P0 per sequence: normalise(prior o T_{c_0} (e_0 o beta^_0)), as op_fb_kernel's
   // extra backward step; then summed over the group in sequence order
