@@ -588,7 +588,7 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         if ir:
             roof["issue"] = ir
     rec = {"metric": metric, "value": value, "unit": "sequence-timesteps/s", "n_gpus": world,
-           "steps": steps, "warmup": nw, "ms_per_step": elapsed / steps * 1e3,
+           "steps": steps, "warmup": nw, "warmup_requested": warmup, "ms_per_step": elapsed / steps * 1e3,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
            "data": "synthetic",
            "config": {"workload": workload, "B_per_gpu": B, "T": T, "hidden_states": N,
@@ -698,9 +698,12 @@ def main():
                          "clique smoothing; jtree: a factorial HMM on the general join-tree engine; "
                          "joint: the same slice as a joint-interface chain; generate: generate_data")
     ap.add_argument("--no-secondary", action="store_true", help="the headline workload only")
-    ap.add_argument("--min-warm", type=float, default=0.0,
-                    help="headline: add warmup steps until this many seconds of warmup ran (the secondary "
-                         "lines use 0.5; kernel traces of a secondary workload run it as the headline)")
+    ap.add_argument("--min-warm", type=float, default=0.5,
+                    help="after the W warmup steps, add untimed steps (at most 64) until this many seconds "
+                         "of warmup ran, as the secondary lines do: the f64 kernels run their first "
+                         "launches at a lower clock (config 2: 0.278-0.288 ms per step after 3 warmup "
+                         "steps, 0.243-0.252 after 0.5 s, profiles/r05/gpu/r05av_warm.txt); 0 = exactly W. "
+                         "The line's 'warmup' is the count that ran, 'warmup_requested' W")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline")
     ap.add_argument("--no-check", action="store_true", help="skip the output sanity check (ablation builds)")
