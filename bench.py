@@ -493,8 +493,10 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
     elif name == "em":
         kname += " + tree64 + finalize"
         workload = ("config4: em_learn iterations of HMM-shaped DBN, %d hidden x %d observed, "
-                    "B=%d seq/GPU x T=%d, %d GPU(s), one packed RCCL all-gather per iteration" % (
-                        N, M, B, T, world))
+                    "B=%d seq/GPU x T=%d, %d GPU(s), %s" % (
+                        N, M, B, T, world,
+                        "one packed RCCL all-gather per iteration" if world > 1 else
+                        "no collective at world 1 (the packed RCCL all-gather runs at N > 1)"))
         metric = "sequence-timesteps/s em_learn (E-step + exchange + M-step per iteration), 16-state DBN"
         P = model.partial_size()
         extra["em"] = {"iterations_timed": steps, "ll_per_iteration": em_state["ll"][-steps:],
@@ -557,7 +559,9 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         metric = "sequence-timesteps/s fwd-bwd smoothing, demo1 @ 32 states"
     else:
         workload = "config5: wide clique {X0,Y1,Z1,X1} 64^4 entries, O1 16 states observed, X1 posterior, " \
-                   "B=%d seq/GPU x T=%d" % (B, T)
+                   "B=%d seq/GPU x T=%d; the 16.7M-entry in-clique is marginalised once per model version on " \
+                   "the GPU (fold_lane_kernel, the line's fold field) and the timed step is the folded " \
+                   "64-state chain" % (B, T)
         metric = "sequence-timesteps/s fwd-bwd smoothing, wide-clique DBN (64^4 in-clique)"
     achieved = bpu * B * T / (kern_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

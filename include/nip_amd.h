@@ -261,7 +261,11 @@ int nipamd_estep_partial(nipamd_model* m, const int32_t* d_obs, int n_obs,
  * operator chain's e_step (whose partial is larger): such requests run on the
  * general engine there.  With capacity >= nipamd_estep_partial_size_req the
  * operator chain takes them; capacity < nipamd_estep_partial_size fails with
- * NIP_ERROR_INVALID_ARGUMENT. */
+ * NIP_ERROR_INVALID_ARGUMENT.  The two forms therefore route such a request
+ * differently -- nipamd_estep_partial to the general engine (slower; route tag
+ * (0, 1, 0), nipamd_last_kernel says so), nipamd_estep_partial_ex to the
+ * operator chain (tag (-1, -1, -1)) -- and their partials do not combine:
+ * every rank of a data-parallel e_step uses the same entry point. */
 int nipamd_estep_partial_ex(nipamd_model* m, const int32_t* d_obs, int n_obs,
                             const int* obs_vars, int B, int T, double* d_partial,
                             long capacity, double* d_ll, uint32_t* d_status,

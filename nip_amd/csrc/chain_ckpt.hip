@@ -545,21 +545,21 @@ int chain_fb_ckpt_launch(const ChainArgs& a, hipStream_t stream) {
     for (int jv = 0; jv < a.nproj; jv++) cmax = a.proj_card[jv] > cmax ? a.proj_card[jv] : cmax;
     if (cmax <= 4) {
       static size_t s4[kMaxDevices] = {};
-      if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<4>), lds, s4)) return -1;
+      if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<4>), lds, s4)) return rc;
       hipLaunchKernelGGL(chain_fb_ckpt_kernel<4>, dim3(blocks), dim3(kCThreads), lds, stream, a);
     } else if (cmax <= 8) {
       static size_t s8[kMaxDevices] = {};
-      if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<8>), lds, s8)) return -1;
+      if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<8>), lds, s8)) return rc;
       hipLaunchKernelGGL(chain_fb_ckpt_kernel<8>, dim3(blocks), dim3(kCThreads), lds, stream, a);
     } else {
       static size_t s16[kMaxDevices] = {};
-      if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<16>), lds, s16)) return -1;
+      if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<16>), lds, s16)) return rc;
       hipLaunchKernelGGL(chain_fb_ckpt_kernel<16>, dim3(blocks), dim3(kCThreads), lds, stream, a);
     }
     g_last_kernel = "chain_fb_ckpt_kernel<proj>";
   } else {
     static size_t lds_set[kMaxDevices] = {};
-    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<0>), lds, lds_set)) return -1;
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_ckpt_kernel<0>), lds, lds_set)) return rc;
     hipLaunchKernelGGL(chain_fb_ckpt_kernel<0>, dim3(blocks), dim3(kCThreads), lds, stream, a);
     g_last_kernel = "chain_fb_ckpt_kernel";
   }

@@ -3,14 +3,30 @@
 
 #include <hip/hip_runtime.h>
 #include <cstddef>
+#include <cstdlib>
+
+#include "diag.h"
 
 namespace nipamd {
 
+// Launchers return 0, kLaunchRefused when the host refuses the request before
+// anything is queued (a shape or an LDS budget the kernel does not take), or
+// -1 when a HIP call fails.  The engine reports a refusal as
+// NIPAMD_ERROR_UNSUPPORTED with the kernel's name and a HIP failure as
+// NIPAMD_ERROR_DEVICE (engine.cpp launch_fail).
+constexpr int kLaunchRefused = -2;
+constexpr size_t kLdsPerCU = 160 * 1024;
+
 // The dynamic-LDS limit of a kernel is a per-device attribute: raise it on
 // the current device when a launch needs more than the default 64 KB,
-// remembering (per kernel, per device) the largest value already set.
+// remembering (per kernel, per device) the largest value already set.  More
+// than a CU holds is a refusal.  Diagnostics builds: NIPAMD_LDS_CAP (bytes)
+// lowers that bound, so that tests can force a refusal through the C ABI.
 constexpr int kMaxDevices = 64;
 inline int ensure_dyn_lds(const void* kernel, size_t lds, size_t (&set)[kMaxDevices]) {
+  size_t cap = kLdsPerCU;
+  if (const char* e = diag_env("NIPAMD_LDS_CAP")) cap = (size_t)std::strtoull(e, nullptr, 10);
+  if (lds > cap) return kLaunchRefused;
   if (lds <= 65536) return 0;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
@@ -330,6 +346,12 @@ size_t chain_estep16_lds_bytes(int M, int T, int ne);
 // sequences per slab row of chain_estep16_kernel (one row per block: 16, or 8 / 24)
 int chain_estep16_seqs_per_row(int M, int T, int ne);
 size_t chain_estep16_scratch_bytes(long B, int T);
+// checkpoint + recompute e_step (estep_ck.hip, round 6): 16-state interface
+// chains with one observed child; a wave per 16 sequences, one slab row each
+// (chain_estep_slab); kLaunchRefused when the request does not fit it
+size_t chain_estep_ck_lds_bytes(int M);
+size_t chain_estep_ck_scratch_bytes(long B, int T);
+int chain_estep_ck_launch(const ChainArgs& a, hipStream_t stream);
 int tree_reduce_launch(const double* in, long n, int S, double* out, hipStream_t stream);
 int estep_finalize_launch(const double* R, const ChainFinalize& f, double* counts, hipStream_t stream);
 // the e_step partial's route tag: tag[0] = a, tag[1] = b, tag[2] = c

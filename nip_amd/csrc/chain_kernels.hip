@@ -942,7 +942,7 @@ size_t chain_estep16_scratch_bytes(long B, int T) {
 template <int NSEQ, int KC, int NE, int PR>
 static int estep16_launch_pr(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC, NE, PR>), lds, lds_set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep16_kernel<NSEQ, KC, NE, PR>), lds, lds_set)) return rc;
   const int blocks = (int)((a.B + NSEQ - 1) / NSEQ);
   hipLaunchKernelGGL((chain_estep16_kernel<NSEQ, KC, NE, PR>), dim3(blocks), dim3(NSEQ * 32), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1131,7 +1131,7 @@ __global__ void estep_prefix_flag_kernel(const int32_t* obs, long bstride, int n
   for (int t = 0; t <= first_bad; t++)
     for (int c = 0; c < n_obs; c++) {
       const int32_t v = o[(long)t * n_obs + c];
-      if (v >= 0 && !(v == 0 && ((trivial >> c) & 1u))) return;
+      if (v >= 0 && !(v == 0 && c < 32 && ((trivial >> c) & 1u))) return;   // the mask covers columns 0..31
     }
   status[b] |= 2u;                                   // NIPAMD_STATUS_BAD_LUCK
 }

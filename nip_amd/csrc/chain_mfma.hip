@@ -693,7 +693,7 @@ namespace {
 template <bool DMA, bool ES>
 int launch_mfma(const ChainArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA, ES>), lds, lds_set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_fb_mfma_kernel<DMA, ES>), lds, lds_set)) return rc;
   const int blocks = (int)((a.B + kMSeq - 1) / kMSeq);
   hipLaunchKernelGGL((chain_fb_mfma_kernel<DMA, ES>), dim3(blocks), dim3(kMThreads), lds, stream, a);
   g_last_kernel = ES ? "chain_fb_mfma_kernel<estep>" : "chain_fb_mfma_kernel";

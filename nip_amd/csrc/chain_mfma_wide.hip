@@ -830,7 +830,7 @@ namespace {
 template <int NT, bool FILT, int NC>
 int launch_wide_nc(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
   static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT, NC>), lds, set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_mfma_wide_kernel<NT, FILT, NC>), lds, set)) return rc;
   const int blocks = (int)((a.B + kWGroups * kWSeq - 1) / (kWGroups * kWSeq));
   hipLaunchKernelGGL((chain_mfma_wide_kernel<NT, FILT, NC>), dim3(blocks), dim3(FILT ? kWThreads / 2 : kWThreads),
                      lds, stream, a);
@@ -850,7 +850,7 @@ int launch_wide(const WideMfmaArgs& a, size_t lds, hipStream_t stream) {
 
 int chain_mfma_wide_launch(const WideMfmaArgs& a, int NT, bool filter_only, hipStream_t stream) {
   const size_t lds = (chain_mfma_wide_lds_bytes(NT, a.tab_rows, a.ncol, a.T) + 15) & ~(size_t)15;
-  if (lds > 160 * 1024 || (filter_only && a.H != a.T)) return -1;
+  if (lds > 160 * 1024 || (filter_only && a.H != a.T)) return kLaunchRefused;
   if (NT == 1) return filter_only ? launch_wide<1, true>(a, lds, stream) : launch_wide<1, false>(a, lds, stream);
   return filter_only ? launch_wide<2, true>(a, lds, stream) : launch_wide<2, false>(a, lds, stream);
 }

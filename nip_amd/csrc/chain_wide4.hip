@@ -727,7 +727,7 @@ namespace {
 template <int NC>
 int launch_r64(const WideArgs& a, size_t lds, hipStream_t stream) {
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<true, NC>), lds, lds_set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<true, NC>), lds, lds_set)) return rc;
   hipLaunchKernelGGL((chain_wide4_kernel<true, NC>), dim3((unsigned)a.B), dim3(kR64Threads), lds, stream, a);
   return 0;
 }
@@ -738,16 +738,16 @@ int chain_wide4_launch(const WideArgs& a, hipStream_t stream) {
   if (lds > 160 * 1024) return -2;
   if (NIPAMD_R64) {
     switch (a.ncol) {
-      case 0: if (launch_r64<0>(a, lds, stream)) return -1; break;
-      case 1: if (launch_r64<1>(a, lds, stream)) return -1; break;
-      case 2: if (launch_r64<2>(a, lds, stream)) return -1; break;
-      case 3: if (launch_r64<3>(a, lds, stream)) return -1; break;
-      default: if (launch_r64<4>(a, lds, stream)) return -1; break;
+      case 0: if (int rc = launch_r64<0>(a, lds, stream)) return rc; break;
+      case 1: if (int rc = launch_r64<1>(a, lds, stream)) return rc; break;
+      case 2: if (int rc = launch_r64<2>(a, lds, stream)) return rc; break;
+      case 3: if (int rc = launch_r64<3>(a, lds, stream)) return rc; break;
+      default: if (int rc = launch_r64<4>(a, lds, stream)) return rc; break;
     }
     g_last_kernel = "chain_row64_kernel";
   } else {
     static size_t lds_set[kMaxDevices] = {};
-    if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<false, 0>), lds, lds_set)) return -1;
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_wide4_kernel<false, 0>), lds, lds_set)) return rc;
     hipLaunchKernelGGL((chain_wide4_kernel<false, 0>), dim3((unsigned)a.B), dim3(kW4Threads), lds, stream, a);
     g_last_kernel = "chain_wide4_kernel";
   }

@@ -34,6 +34,16 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// A launcher's nonzero return (chain_kernels.h): kLaunchRefused -- the host
+// refused the request before queueing anything (a shape or LDS budget the
+// kernel does not take) -- is NIPAMD_ERROR_UNSUPPORTED; anything else is a
+// failed HIP call, NIPAMD_ERROR_DEVICE with HIP's last error.
+int launch_fail(int rc, const char* what) {
+  if (rc == nipamd::kLaunchRefused)
+    return fail(NIPAMD_ERROR_UNSUPPORTED, std::string(what) + ": the request does not fit the kernel (refused on the host)");
+  return fail(NIPAMD_ERROR_DEVICE, std::string(what) + ": kernel launch failed: " + hipGetErrorString(hipGetLastError()));
+}
+
 #define HIP_OK(expr)                                                         \
   do {                                                                       \
     hipError_t e_ = (expr);                                                  \
@@ -407,6 +417,9 @@ int ensure_work(nipamd_model* mm, size_t bytes) {
 #define NIPAMD_ESTEP_SEQS 16384
 #endif
 constexpr long kEstepChunk = NIPAMD_ESTEP_SEQS;
+// chain_estep_ck_kernel's launches: its scratch holds one checkpoint per four
+// steps (~4.4 GB at 131072 x 1024), so a whole config-4 shard is one launch
+constexpr long kEstepCkChunk = 131072;
 
 // rows [n][S] -> out [S] by repeated radix-64 tree levels (ping-pong tA/tB)
 int reduce_rows(const double* in, long n, int S, double* tA, double* tB, double* out, hipStream_t st) {
@@ -830,8 +843,8 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
       HIP_OK(hipMemsetAsync(w.diag, 0, (size_t)nblk * 16 * sizeof(unsigned long long), (hipStream_t)stream));
     }
 #endif
-    if (nipamd::chain_mfma_wide_launch(w, NT, filt, (hipStream_t)stream))
-      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (int rc = nipamd::chain_mfma_wide_launch(w, NT, filt, (hipStream_t)stream))
+      return launch_fail(rc, "chain_mfma_wide_kernel");
 #ifdef NIPAMD_DIAGNOSTICS
     if (w.diag) {
       std::vector<unsigned long long> h((size_t)nblk * 16);
@@ -877,8 +890,8 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
       HIP_OK(hipMemsetAsync(w.diag, 0, (size_t)B * 16 * sizeof(unsigned long long), (hipStream_t)stream));
     }
 #endif
-    if (nipamd::chain_wide_launch(w, (hipStream_t)stream))
-      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (int rc = nipamd::chain_wide_launch(w, (hipStream_t)stream))
+      return launch_fail(rc, "wide chain kernel");
 #ifdef NIPAMD_DIAGNOSTICS
     if (w.diag) {
       std::vector<unsigned long long> h((size_t)B * 16);
@@ -950,8 +963,7 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
     }
   }
 #endif
-  if (rc)
-    return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (rc) return launch_fail(rc, kind == kNarrowMfma ? "chain_fb_mfma_kernel" : "chain_kernel");
   return 0;
 }
 
@@ -997,8 +1009,8 @@ static int launch_joint_marginals(nipamd_model* mm, const Route& r, ReqTables* r
   a.ll = d_ll;
   a.status = d_status;
   const int rc = nipamd::chain_fb_ckpt_launch(a, (hipStream_t)stream);
-  if (rc == -2) return 0;
-  if (rc) return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (rc == -2) return 0;                            // not taken: the next kernel serves it
+  if (rc) return launch_fail(rc, "chain_fb_ckpt_kernel");
   *taken = true;
   return 0;
 }
@@ -1069,8 +1081,8 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
         for (size_t j = 0; j < out.size() && out[j] != query[i]; j++) g.prev_stride *= mm->m.vars[out[j]].card;
         g.prev_card = mm->m.vars[query[i]].card;
         g.child_col = -1;
-        if (nipamd::derive_launch(g, (hipStream_t)stream))
-          return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+        if (int rc = nipamd::derive_launch(g, (hipStream_t)stream))
+          return launch_fail(rc, "derive_kernel");
         off += g.prev_card;
       }
       return 0;
@@ -1177,8 +1189,8 @@ static int fb_impl(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int*
       g.hid_card = mm->m.vars[P.hidden[j]].card;
       g.G = d->G[j];
     }
-    if (nipamd::derive_launch(g, (hipStream_t)stream))
-      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (int rc = nipamd::derive_launch(g, (hipStream_t)stream))
+      return launch_fail(rc, "derive_kernel");
   }
   return 0;
 }
@@ -1327,6 +1339,7 @@ int nipamd_estep_partial_size_req(nipamd_model* mm, int n_obs, const int* obs_va
 // waves; NIPAMD_ESTEP_KERNEL=dpp8 in diagnostics builds, or when the 16-seq
 // block's LDS does not fit), 1 = the matrix-core kernel (NIPAMD_ESTEP_KERNEL=mfma).
 // Measured on config 4.
+static bool estep16_sparse_ok(const nipamd::ChainPlan& P, int ne);
 static int chain_estep_kernel(const nipamd_model* mm, int T) {
   const auto& P = mm->m.chain;
   if (estep_general_plan(P))                       // only chain_estep16_kernel takes several children
@@ -1334,6 +1347,13 @@ static int chain_estep_kernel(const nipamd_model* mm, int T) {
   const int M = P.emits[0].M;
   const char* ek = nipamd::diag_env("NIPAMD_ESTEP_KERNEL");
   const std::string want = ek ? ek : "";
+  // 4 = chain_estep_ck_kernel (checkpoints + recomputation, round 6): the
+  // default where both recursions may rescale every 4th step (the host's
+  // underflow bound) and its count tables fit; NIPAMD_ESTEP_KERNEL=e16 in
+  // diagnostics builds runs chain_estep16_kernel instead
+  if (want != "mfma" && want != "dpp8" && want != "e16" && P.N <= 16 && P.hmm &&
+      nipamd::chain_estep_ck_lds_bytes(M) <= 160 * 1024 && estep16_sparse_ok(P, 1))
+    return 4;
   if (want == "mfma" && P.N <= 16 && M <= 16 && nipamd::chain_estep_mfma_lds_bytes(M, T) <= 160 * 1024) return 1;
   if (want != "dpp8" && P.N <= 16 && nipamd::chain_estep16_lds_bytes(M, T, 1) <= 160 * 1024) return 3;
   if (nipamd::chain_lds_bytes(M, T, true) <= 96 * 1024) return 2;
@@ -1613,8 +1633,7 @@ static int estep_mw_partial(nipamd_model* mm, const Route& r, const int32_t* d_o
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     const int lrc = nipamd::estep_mw_launch(a, st);
-    if (lrc == -2) return fail(NIPAMD_ERROR_UNSUPPORTED, "matrix-core e_step: the request does not fit the kernel");
-    if (lrc) return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (lrc) return launch_fail(lrc, "chain_estep_mw_kernel");
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
     if (reduce_rows(slab, (nb + 15) / 16, S, tA, tB, out, st))
       return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
@@ -1698,8 +1717,7 @@ static int estep_wide_partial(nipamd_model* mm, const Route& r, const int32_t* d
       row += P.emits[k].M + 2;
     }
     const int lrc = nipamd::estep_wide_launch(a, st);
-    if (lrc == -2) return fail(NIPAMD_ERROR_UNSUPPORTED, "wide chain e_step: the count tables do not fit the kernel");
-    if (lrc) return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (lrc) return launch_fail(lrc, "wide chain e_step (chain_msgs_kernel + chain_stats_kernel)");
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
     if (reduce_rows(slab, (nb + 15) / 16, S, tA, tB, out, st))
       return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");
@@ -1737,6 +1755,10 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     if (!nipamd::jt_supported(mm, n_obs, obs_vars, 0, nullptr, why)) return fail(NIPAMD_ERROR_UNSUPPORTED, why);
     if (int rc = nipamd::jt_estep_partial(mm, d_obs, n_obs, obs_vars, B, T, d_partial, d_ll, d_status, stream))
       return rc;
+    // an operator-chain request on a partial too small for its section (the
+    // capacity-free nipamd_estep_partial): say so in nipamd_last_kernel
+    if (capacity >= 0 && op_estep_route(mm, n_obs, obs_vars, T, -1))
+      nipamd::g_last_kernel = "general engine (operator-chain request on a partial without room for its section)";
     if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 1.0, 0.0, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
     return zero_tail(mm, d_partial, nipamd::param_size(mm->m), (hipStream_t)stream);
@@ -1750,7 +1772,9 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   const bool mfma = ek == 1;
   // sequences per slab row: the matrix-core kernel's and chain_estep16_kernel's
   // blocks (one row each), the round-2 DPP kernel's sequences
-  const int per_row = mfma ? 16 : ek == 3 ? nipamd::chain_estep16_seqs_per_row(Mo, T, general ? (int)P.emits.size() : 1) : 1;
+  const bool ck = ek == 4;
+  const int per_row = (mfma || ck) ? 16 : ek == 3 ? nipamd::chain_estep16_seqs_per_row(Mo, T, general ? (int)P.emits.size() : 1) : 1;
+  const long echunk = ck ? kEstepCkChunk : kEstepChunk;
   hipStream_t st = (hipStream_t)stream;
   if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 1.0, 0.0, 0.0, st))
     return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
@@ -1763,13 +1787,14 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   if (int rc = ensure_req_tables(mm, rh, &rt)) return rc;
   if (general)
     if (int rc = ensure_etab_all(mm)) return rc;
-  const long chunk = B < kEstepChunk ? B : kEstepChunk;
-  const long nchunks = (B + kEstepChunk - 1) / kEstepChunk;
+  const long chunk = B < echunk ? B : echunk;
+  const long nchunks = (B + echunk - 1) / echunk;
   const long rows = (chunk + per_row - 1) / per_row;
   const long lvl = (rows + 63) / 64;
   const size_t work = ((size_t)rows + 2 * lvl + nchunks + 64) * S * sizeof(double);
-  if (int rc = ensure_scratch(mm, ek == 3 ? nipamd::chain_estep16_scratch_bytes(chunk, T)
-                                          : nipamd::chain_scratch_bytes((int)chunk, T))) return rc;
+  if (int rc = ensure_scratch(mm, ck ? nipamd::chain_estep_ck_scratch_bytes(chunk, T)
+                                  : ek == 3 ? nipamd::chain_estep16_scratch_bytes(chunk, T)
+                                            : nipamd::chain_scratch_bytes((int)chunk, T))) return rc;
   if (int rc = ensure_work(mm, work)) return rc;
   DevState* d = dev_of(mm);
   double* slab = d->W;
@@ -1778,8 +1803,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
   double* cres = tB + (size_t)lvl * S;
   const long ocols = n_obs > 0 ? n_obs : 1;
   for (long c = 0; c < nchunks; c++) {
-    const long b0 = c * kEstepChunk;
-    const int nb = (int)((B - b0) < kEstepChunk ? (B - b0) : kEstepChunk);
+    const long b0 = c * echunk;
+    const int nb = (int)((B - b0) < echunk ? (B - b0) : echunk);
     nipamd::ChainArgs a{};
     a.obs = (general ? r.ncol > 0 : col >= 0) ? d_obs + b0 * T * ocols : nullptr;
     a.obs_bstride = (long)T * ocols;
@@ -1802,7 +1827,8 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
     a.counts = slab;
-    a.proper = ek == 3 && chain_proper(P) ? (estep16_sparse_ok(P, a.ne) ? 2 : 1) : 0;
+    a.proper = ck ? (chain_proper(P) ? 1 : 0)
+                  : ek == 3 && chain_proper(P) ? (estep16_sparse_ok(P, a.ne) ? 2 : 1) : 0;
 #ifdef NIPAMD_DIAGNOSTICS
     static const bool times = std::getenv("NIPAMD_PHASE_TIMES") != nullptr;
     const int nblk = (nb + 15) / 16;
@@ -1818,10 +1844,12 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       a.diag = e16d;
     }
 #endif
-    const int lrc = mfma ? nipamd::chain_estep_mfma_launch(a, st)
+    const int lrc = ck ? nipamd::chain_estep_ck_launch(a, st)
+                    : mfma ? nipamd::chain_estep_mfma_launch(a, st)
                     : ek == 3 ? nipamd::chain_estep16_launch(a, st) : nipamd::chain_estep_launch(a, st);
     if (lrc)
-      return fail(NIPAMD_ERROR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+      return launch_fail(lrc, ck ? "chain_estep_ck_kernel" : mfma ? "chain_fb_mfma_kernel (e_step)"
+                              : ek == 3 ? "chain_estep16_kernel" : "chain_kernel<true>");
 #ifdef NIPAMD_DIAGNOSTICS
     if (e16d) {
       std::vector<unsigned long long> h((size_t)nblk8 * 64);

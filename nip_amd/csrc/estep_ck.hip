@@ -1,0 +1,439 @@
+// estep_ck.hip -- e_step of 16-state interface chains with one observed child
+// (the HMM-shaped DBN of SURVEY 8(d) config 4) on the matrix cores, with
+// checkpoints and recomputation instead of the interface-message round trip
+// (round 6).
+//
+// What the reference computes per sequence (src/nip.c:1708-2007; families
+// :1925-1967) follows from three sums over the sequence:
+//   K(x, y)  = sum_t alpha_{t-1}(x) e_t(y) beta_t(y) / Z      (alpha_{-1} = prior)
+//   H[m][y]  = sum_t [m = code of o_t] gamma_t(y)             (M1 counts, rows M + 2)
+//   P0(x)    = gamma_{-1}(x) = prior(x) beta_{-1}(x) / Z      (OLD_OUTGOING at t = 0)
+// with the transition factor A(x, y) applied to K and the missing row split
+// by the finalize (estep_finalize_kernel), and ll the forward filter's.
+//
+// chain_estep16_kernel stores every interface message to HBM and reads it
+// back: 256 of its 260 B per sequence-step.  Here a WAVE owns 16 sequences
+// and does everything itself, with no barrier and no other wave:
+//   forward pass   t = 0..T-1: alpha^_t = e_t o (A^T alpha^_{t-1}), four
+//                  v_mfma_f64_16x16x4 per step (the fb kernels' register
+//                  algebra, chain_mfma_core.h); every 4th message (t = 4k+3,
+//                  rescaled to sum ~1) and its exponent go to HBM: 32 B per
+//                  sequence-step written, the same read back;
+//   backward pass  t = T-1..0 in chunks of four steps: beta^ by the same
+//                  matrix-core recursion with A; the chunk's three other
+//                  alpha^ recomputed from the checkpoint below it (one chunk
+//                  ahead, so the recomputation overlaps the steps); per step
+//                  alpha^_{t-1}, the xi weight w_t and gamma_t go through a
+//                  wave-private LDS transpose into sequence-major lanes, xi
+//                  is four v_mfma_f64_16x16x4 (K = the wave's 16 sequences)
+//                  and the M1 counts are read-add-writes into four LDS count
+//                  tables (lane quarter k owns table k, so no two lanes of an
+//                  instruction touch one cell: deterministic, no atomics).
+// HBM per sequence-step: the observation (4 B, read by both passes) and the
+// checkpoints (2 x 8 B amortised: 128 B per 4 steps written, read once): 72 B
+// against chain_estep16_kernel's 260.
+//
+// Normalisation: both recursions rescale by exact powers of two every 4th step
+// (only where the host's bound rules out underflow between rescales,
+// engine.cpp estep16_sparse_ok) and carry the exponents (Ef, Eb), so
+// c_t = sum_y alpha^_t beta^_t = Z 2^(Ef_t + Eb_t) for every t: one exact sum
+// per chunk (c*, E*) normalises the chunk's four steps,
+//   gamma_t = alpha^_t o beta^_t 2^(E* - Ef_t - Eb_t) / c*
+//   w_t     = e_t o beta^_t 2^(E* - Ef_{t-1} - Eb_t) / c*   (paired with alpha^_{t-1})
+// -- the drift of chain_estep16_kernel's per-phase c* cannot build up here.
+// P0 is normalised exactly.  Sums in a fixed order throughout; one slab row per
+// wave (chain_estep_slab layout: Kf = K, Kb = 0, Hf = H, Hb = 0, P0), reduced
+// by tree64_kernel and applied by estep_finalize_kernel like every 16-state
+// e_step slab, so partials of whole 16-sequence groups combine bit-identically.
+//
+// ll (nip.c:1458-1474): proper models (rows of A and of the child sum to 1:
+// the per-step masses telescope) log of the final forward mass minus its
+// exponent; otherwise m2_t = sum(alpha_t), m1_t = sum(u_t o s) per step (u_t =
+// A^T alpha^_{t-1}; a missing step has e = s, so both are the same bits and
+// the step adds exactly 0), as mantissa / exponent products.
+#include "chain_mfma_core.h"
+#include "store_pol.h"
+
+#include <type_traits>
+
+namespace nipamd {
+
+namespace {
+
+constexpr int kCkWaves = 4;                  // waves per block, one per SIMD; a wave owns 16 sequences
+constexpr int kCkThreads = 64 * kCkWaves;
+constexpr int kCkEt = 18;                    // evidence row stride (doubles): rows 144 B apart (chain_ckpt.hip)
+constexpr int kCkXD = 256;                   // one transpose buffer: [16 sequences][16 states]
+#ifndef NIPAMD_CK_SCR_NT
+#define NIPAMD_CK_SCR_NT 0                   // A/B builds: checkpoints stored / loaded nontemporal
+#endif
+
+// per-wave LDS (doubles): four count tables [4][R][16], three transpose
+// buffers (alpha^_{t-1}, w_t, gamma_t), the chunk's packed codes [16] words
+__host__ __device__ inline int ck_wave_doubles(int R) { return 4 * R * 16 + 3 * kCkXD + 8; }
+__host__ __device__ inline int ck_et_doubles(int R) { return (R * kCkEt + 1) & ~1; }
+// checkpoints per group: alpha^_{4k+3} for k < nck, [nck][16][16] doubles, then [nck][16] int exponents
+__host__ __device__ inline int ck_count(int T) { return (T + 3) >> 2; }
+__host__ __device__ inline long ck_group_doubles(int T) { return (long)ck_count(T) * (256 + 8); }
+
+// transpose buffer [row][16]: the 16-byte piece p of row r at (p ^ (r & 7)):
+// the filter-layout writes (lane (g, j): pieces g and g + 4 of row j) and the
+// sequence-major reads (a row's 16 doubles per 16 lanes) are conflict-free
+__device__ __forceinline__ int tp_off(int row, int piece) { return row * 16 + ((piece ^ (row & 7)) << 1); }
+
+// filter layout (lane (g, j): states 2g, 2g+1, 2g+8, 2g+9 of sequence j) -> row j
+__device__ __forceinline__ void tp_write(double* buf, int j, int g, const v4d& v) {
+  *reinterpret_cast<v2d*>(buf + tp_off(j, g)) = v2d{v.x, v.y};
+  *reinterpret_cast<v2d*>(buf + tp_off(j, g + 4)) = v2d{v.z, v.w};
+}
+
+// sequence-major: lane l gets state l & 15 of sequences 4q + (l >> 4), q = 0..3 --
+// exactly the A (i = state, k = sequence) and B (k = sequence, j = state)
+// operands of v_mfma_f64_16x16x4 q
+__device__ __forceinline__ v4d tp_read(const double* buf, int lane) {
+  const int y = lane & 15, k = lane >> 4;
+  const int p = y >> 1, e = y & 1;
+  v4d r;
+  r.x = buf[tp_off(k, p) + e];
+  r.y = buf[tp_off(4 + k, p) + e];
+  r.z = buf[tp_off(8 + k, p) + e];
+  r.w = buf[tp_off(12 + k, p) + e];
+  return r;
+}
+
+__device__ __forceinline__ v4d mfma4(const v4d& a, const v4d& b, v4d d) {
+  d = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.x, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b.y, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f64_16x16x4f64(a.z, b.z, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f64_16x16x4f64(a.w, b.w, d, 0, 0, 0);
+  return d;
+}
+
+__device__ __forceinline__ unsigned byte_of(unsigned w, int k) { return (w >> (8 * k)) & 0xFFu; }
+
+// mantissa / exponent running product
+struct MProd {
+  double m = 1.0;
+  int e = 0;
+  __device__ __forceinline__ void mul(double x) { m *= x; }
+  __device__ __forceinline__ void renorm() {
+    const int k = __builtin_amdgcn_frexp_exp(m);
+    m = __builtin_ldexp(m, -k);
+    e += k;
+  }
+};
+
+template <int PR>
+__global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = a.M, R = M + 2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* Et = reinterpret_cast<double*>(smem);                                // [R][kCkEt]
+  double* wl = Et + ck_et_doubles(R) + (size_t)wave * ck_wave_doubles(R);
+  double* H = wl;                                                             // [4][R][16]
+  double* XA = H + 4 * R * 16;                                                // alpha^_{t-1}
+  double* XW = XA + kCkXD;                                                    // w_t
+  double* XG = XW + kCkXD;                                                    // gamma_t
+  unsigned* CW = reinterpret_cast<unsigned*>(XG + kCkXD);                     // [16] packed codes
+
+  for (int i = tid; i < R * 16; i += kCkThreads) Et[(i >> 4) * kCkEt + (i & 15)] = a.Etab[i];
+  for (int i = lane; i < 4 * R * 16; i += 64) H[i] = 0.0;
+  __syncthreads();                                                            // the block's only barrier
+
+  const long grp = (long)blockIdx.x * kCkWaves + wave;
+  const long b0 = grp * 16;
+  if (b0 >= a.B) return;
+  const int j = lane & 15, g = lane >> 4;
+  const int sj = state_of(j & 3, j >> 2);
+  const bool active = b0 + j < a.B;
+  const int* orow = a.obs ? a.obs + (active ? (b0 + j) * a.obs_bstride : 0) + a.obs_col : nullptr;
+  const bool vec = a.obs && a.obs_tstride == 1 && (a.obs_bstride & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) && a.obs_col == 0;
+  const int nck = ck_count(T);
+  double* Sg = a.S + (size_t)grp * ck_group_doubles(T);                      // [nck][16][16]
+  int* Xg = reinterpret_cast<int*>(Sg + (size_t)nck * 256);                   // [nck][16]
+
+  // the four codes of chunk c (steps 4c..4c+3) of this lane's sequence, one
+  // byte each: the state, M missing, M + 1 out of range; steps past T and
+  // sequences past B read as missing
+  auto codes_of = [&](int c) -> unsigned {
+    int o[4];
+    const int t0 = 4 * c;
+    if (vec && active && t0 >= 0 && t0 + 3 < T) {
+      const int4 v = *reinterpret_cast<const int4*>(orow + t0);
+      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        o[k] = (orow && active && t0 + k >= 0 && t0 + k < T) ? orow[(long)(t0 + k) * a.obs_tstride] : -1;
+    }
+    unsigned w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int cd = o[k] < 0 ? M : (o[k] < M ? o[k] : M + 1);
+      w |= (unsigned)cd << (8 * k);
+    }
+    return w;
+  };
+  const double* Etg = Et + 2 * g;
+  auto evid = [&](unsigned w, int k) { return load4(Etg + byte_of(w, k) * kCkEt); };
+
+  // the matrix-core operands: forward u(y) = sum_x A[x][y] X(x), backward u(x) = sum_y A[x][y] X(y)
+  double Af[4], Ab[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    Af[r] = a.A[state_of(g, r) * 16 + sj];
+    Ab[r] = a.A[sj * 16 + state_of(g, r)];
+  }
+  const v4d zero = {0.0, 0.0, 0.0, 0.0};
+  const v4d prior = active ? load4(a.pi + 2 * g) : zero;
+  const v4d srow = load4(Etg + M * kCkEt);                                    // s: the missing row
+
+  // ---------------------------------------------------------------- forward
+  v4d X = prior;                 // alpha^_{t-1}
+  int Ef = 0;
+  MProd m2, m1;
+  bool dead = false;
+  {
+    unsigned wa = codes_of(0), wb = codes_of(1);
+    const int nfull = T >> 2;
+    for (int c = 0; c < nfull; c++) {
+      const unsigned w = wa;
+      wa = wb;
+      wb = codes_of(c + 2);
+      v4d e[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) e[k] = evid(w, k);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const v4d u = matvec(Af, X);
+        v4d p = u * e[k];
+        double z = 0.0;
+        if (!PR) {
+          z = chain_sum(p);
+          m2.mul(z);
+          m1.mul(chain_sum(u * srow));
+          m2.renorm();
+          m1.renorm();
+          dead |= z == 0.0;
+        }
+        if (k == 3) {
+          if (PR) z = chain_sum(p);
+          const int sc = -__builtin_amdgcn_frexp_exp(z);     // frexp exponent of 0 is 0
+          p = ldexp4(p, sc);
+          Ef += sc;
+          double* q = Sg + (size_t)c * 256 + j * 16 + 2 * g;
+          store_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<v2d*>(q), v2d{p.x, p.y});
+          store_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<v2d*>(q + 8), v2d{p.z, p.w});
+          if (g == 0) Xg[c * 16 + j] = Ef;
+        }
+        X = p;
+      }
+    }
+    // the last, partial chunk (T % 4 steps): no checkpoint
+    for (int t = nfull * 4; t < T; t++) {
+      const v4d u = matvec(Af, X);
+      const v4d p = u * evid(wa, t & 3);
+      if (!PR) {
+        const double z = chain_sum(p);
+        m2.mul(z);
+        m1.mul(chain_sum(u * srow));
+        m2.renorm();
+        m1.renorm();
+        dead |= z == 0.0;
+      }
+      X = p;
+    }
+  }
+  // ll and status (nip.c:1458-1474; e_step's BAD_LUCK on a zero mass, nip.c:1827-1854)
+  if (PR) {
+    const double zT = chain_sum(X);
+    dead = zT == 0.0;
+    if (active && g == 0) {
+      const double ll = dead ? -DBL_MAX : log(zT) - (double)Ef * 0.69314718055994530942;
+      if (a.ll) a.ll[b0 + j] = ll;
+      if (a.status) a.status[b0 + j] = dead ? 3u : 0u;
+    }
+  } else {
+    if (active && g == 0) {
+      double ll = log(m2.m) - log(m1.m) + (double)(m2.e - m1.e) * 0.69314718055994530942;
+      if (dead || m2.m == 0.0) ll = -DBL_MAX;
+      if (a.ll) a.ll[b0 + j] = ll;
+      if (a.status) a.status[b0 + j] = (dead || m2.m == 0.0) ? 3u : 0u;
+    }
+  }
+  // the checkpoints back from HBM by this wave: its own stores first
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+
+  // --------------------------------------------------------------- backward
+  // checkpoint k = alpha^_{4k+3} (exponent in Xg); k = -1: the prior, exponent 0
+  auto ck_load = [&](int k, int& e) -> v4d {
+    if (k < 0) { e = 0; return prior; }
+    const double* q = Sg + (size_t)k * 256 + j * 16 + 2 * g;
+    const v2d u = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q));
+    const v2d w = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q + 8));
+    e = Xg[k * 16 + j];
+    return v4d{u.x, u.y, w.x, w.y};
+  };
+  const int ctop = (T - 1) >> 2;
+  v4d Bt;                                       // beta^_t
+  Bt.x = (active && state_of(g, 0) < a.N) ? 1.0 : 0.0;
+  Bt.y = (active && state_of(g, 1) < a.N) ? 1.0 : 0.0;
+  Bt.z = (active && state_of(g, 2) < a.N) ? 1.0 : 0.0;
+  Bt.w = (active && state_of(g, 3) < a.N) ? 1.0 : 0.0;
+  int Eb = 0;
+  v4d Kd = zero;                                // xi sums (D[i][y]: lane (i % 4) * 16 + y, register i / 4)
+  const int tk = lane >> 4, ty = lane & 15;     // sequence-major lane: table tk, state ty
+  double* Hk = H + tk * R * 16 + ty;
+
+  // chunk c's alpha^: V[0..2] recomputed from checkpoint c - 1 (exponent Es),
+  // V3 = checkpoint c (exponent E3; the top chunk's is the forward pass's X
+  // when T % 4 == 0, and unused otherwise)
+  v4d V[3], Vn[3];
+  int Es, E3;
+  v4d S3;
+  unsigned wc, wn;                              // codes of chunk c, c - 1
+  v4d ec[4], en[4];                             // evidence of chunk c, c - 1
+  auto recompute = [&](const v4d& start, const v4d (&e)[4], v4d (&out)[3]) {
+    v4d x = start;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      x = matvec(Af, x) * e[k];
+      out[k] = x;
+    }
+  };
+  // prologue: chunk ctop's codes, evidence, checkpoints and recomputation
+  wc = codes_of(ctop);
+  wn = codes_of(ctop - 1);
+#pragma unroll
+  for (int k = 0; k < 4; k++) ec[k] = evid(wc, k);
+  v4d Sb = ck_load(ctop - 1, Es);               // checkpoint below chunk ctop
+  S3 = ((T & 3) == 0) ? X : zero;
+  E3 = Ef;
+  recompute(Sb, ec, V);
+
+  // one chunk: its steps t = 4c + k, k = kmax..0 (kmax = 3 but in a short top
+  // chunk), with chunk c - 1's recomputation issued one step per step
+  auto chunk = [&](int c, auto full) {
+    constexpr bool FULL = decltype(full)::value;
+    if (g == 0) CW[j] = wc;                      // this chunk's packed codes, for the sequence-major lanes
+    // chunk c - 1: its evidence, the checkpoint below it (c - 2; c - 1 itself is Sb)
+    v4d Sbn = prior;
+    int Esn = 0;
+    if (c > 0) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) en[k] = evid(wn, k);
+      Sbn = ck_load(c - 2, Esn);
+    }
+    const unsigned wnn = c > 1 ? codes_of(c - 2) : 0u;
+    const unsigned cq0 = CW[tk], cq1 = CW[4 + tk], cq2 = CW[8 + tk], cq3 = CW[12 + tk];
+    const int kmax = FULL ? 3 : ((T - 1) & 3);
+    double rc = 0.0;
+    int Estar = 0;
+    v4d x = Sbn;                                 // chunk c - 1's recomputation chain
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+      if (c > 0 && k < 3) {                      // one recomputed step per step: Vn[0], Vn[1], Vn[2]
+        x = matvec(Af, x) * en[2 - k];
+        Vn[2 - k] = x;
+      }
+      if (!FULL && k > kmax) continue;           // the top chunk's steps past T - 1
+      const v4d cur = k == 3 ? S3 : V[k];        // alpha^_t
+      const v4d prv = k == 0 ? Sb : V[k - 1];    // alpha^_{t-1}
+      const int efc = k == 3 ? E3 : Es, efp = Es;
+      const v4d Xb = ec[k] * Bt;                 // e_t o beta^_t: the xi weight and the backward input
+      const v4d pr = cur * Bt;
+      if (FULL ? k == 3 : k == kmax) {           // the chunk's exact mass: c* = c_t, E*
+        rc = recip(chain_sum(pr));
+        Estar = efc + Eb;
+      }
+      const double f = __builtin_ldexp(rc, Estar - efp - Eb);
+      const double gg = __builtin_ldexp(rc, Estar - efc - Eb);
+      tp_write(XA, j, g, prv);
+      tp_write(XW, j, g, Xb * f);
+      tp_write(XG, j, g, pr * gg);
+      Bt = matvec(Ab, Xb);                       // beta^_{t-1}, exponent Eb until the chunk's rescale
+      const v4d aT = tp_read(XA, lane), wT = tp_read(XW, lane), gT = tp_read(XG, lane);
+      Kd = mfma4(aT, wT, Kd);
+      // M1 counts: lane (tk, ty) adds gamma_t(ty) of sequences 4q + tk to table tk, row = its code
+      Hk[byte_of(cq0, k) * 16] += gT.x;
+      Hk[byte_of(cq1, k) * 16] += gT.y;
+      Hk[byte_of(cq2, k) * 16] += gT.z;
+      Hk[byte_of(cq3, k) * 16] += gT.w;
+    }
+    // beta^ rescaled once per chunk (exact powers of two; the exponent carries the scale)
+    {
+      const int sb = -__builtin_amdgcn_frexp_exp(chain_sum(Bt));
+      Bt = ldexp4(Bt, sb);
+      Eb += sb;
+    }
+    // rotate: chunk c - 1 becomes current
+    S3 = Sb;
+    E3 = Es;
+    Sb = Sbn;
+    Es = Esn;
+#pragma unroll
+    for (int k = 0; k < 3; k++) V[k] = Vn[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) ec[k] = en[k];
+    wc = wn;
+    wn = wnn;
+  };
+  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{});
+  else chunk(ctop, std::false_type{});
+  for (int c = ctop - 1; c >= 0; c--) chunk(c, std::true_type{});
+
+  // P0 = gamma_{-1}: prior o beta^_{-1}, normalised exactly; summed over the
+  // wave's sequences in a fixed order (transpose, in-lane, then lane quarters)
+  const v4d p0 = prior * Bt;
+  const v4d q0 = p0 * recip(chain_sum(p0));
+  tp_write(XG, j, g, q0);
+  const v4d q0T = tp_read(XG, lane);
+  const double p0s = sum_lanes16(sum_lanes32((q0T.x + q0T.y) + (q0T.z + q0T.w)));
+
+  // the slab row (chain_estep_slab layout)
+  double* slab = a.counts + (size_t)grp * chain_estep_slab(M);
+#pragma unroll
+  for (int r = 0; r < 4; r++) slab[kSlabKf + (4 * r + tk) * 16 + ty] = Kd[r];
+  for (int i = lane; i < 256; i += 64) slab[kSlabKb + i] = 0.0;
+  for (int i = lane; i < R * 16; i += 64) {
+    const int row = i >> 4, y = i & 15;
+    const double v = ((H[row * 16 + y] + H[R * 16 + row * 16 + y]) + H[2 * R * 16 + row * 16 + y]) +
+                     H[3 * R * 16 + row * 16 + y];
+    slab[kSlabH + i] = v;
+    slab[kSlabH + R * 16 + i] = 0.0;
+  }
+  if (lane < 16) slab[chain_slab_p0(M) + lane] = p0s;
+}
+
+}  // namespace
+
+size_t chain_estep_ck_lds_bytes(int M) {
+  const int R = M + 2;
+  return ((size_t)ck_et_doubles(R) + (size_t)kCkWaves * ck_wave_doubles(R)) * sizeof(double);
+}
+
+size_t chain_estep_ck_scratch_bytes(long B, int T) {
+  return (size_t)((B + 15) / 16) * (size_t)ck_group_doubles(T) * sizeof(double);
+}
+
+int chain_estep_ck_launch(const ChainArgs& a, hipStream_t stream) {
+  const size_t lds = (chain_estep_ck_lds_bytes(a.M) + 15) & ~(size_t)15;
+  if (a.N > 16 || a.ne != 1 || !a.counts || a.T < 1 || lds > 160 * 1024) return kLaunchRefused;
+  const long groups = (a.B + 15) / 16;
+  const int blocks = (int)((groups + kCkWaves - 1) / kCkWaves);
+  if (a.proper) {
+    static size_t set[kMaxDevices] = {};
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_ck_kernel<1>), lds, set)) return rc;
+    hipLaunchKernelGGL(chain_estep_ck_kernel<1>, dim3(blocks), dim3(kCkThreads), lds, stream, a);
+  } else {
+    static size_t set[kMaxDevices] = {};
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_ck_kernel<0>), lds, set)) return rc;
+    hipLaunchKernelGGL(chain_estep_ck_kernel<0>, dim3(blocks), dim3(kCkThreads), lds, stream, a);
+  }
+  g_last_kernel = "chain_estep_ck_kernel";
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace nipamd

@@ -735,7 +735,7 @@ __global__ __launch_bounds__(kThreads, 1) void chain_estep_mw_kernel(EMwArgs a) 
 template <int NC>
 int launch_nc(const EMwArgs& a, size_t lds, hipStream_t stream) {
   static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_mw_kernel<NC>), lds, set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_mw_kernel<NC>), lds, set)) return rc;
   const int blocks = (int)((a.B + kGroups * kSeq - 1) / (kGroups * kSeq));
   hipLaunchKernelGGL((chain_estep_mw_kernel<NC>), dim3(blocks), dim3(kThreads), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -517,7 +517,7 @@ int stats_launch(const EWideArgs& a, hipStream_t stream) {
   static size_t set[2][kMaxDevices] = {};
   const void* k = tl ? reinterpret_cast<const void*>(&chain_stats_kernel<NT, HR, true>)
                      : reinterpret_cast<const void*>(&chain_stats_kernel<NT, HR, false>);
-  if (ensure_dyn_lds(k, lds, set[tl])) return -1;
+  if (int rc = ensure_dyn_lds(k, lds, set[tl])) return rc;
   const int blocks = (int)((a.B + kStatSeqs - 1) / kStatSeqs);
   if (tl) hipLaunchKernelGGL((chain_stats_kernel<NT, HR, true>), dim3(blocks), dim3(kStatWaves * 64), lds, stream, a);
   else hipLaunchKernelGGL((chain_stats_kernel<NT, HR, false>), dim3(blocks), dim3(kStatWaves * 64), lds, stream, a);
@@ -1192,7 +1192,7 @@ int msgs_launch(const OpWideArgs& a, hipStream_t stream) {
   const size_t tl = (size_t)op_lds_doubles(a.oncomb, a.K, NP) * sizeof(double);
   if (tl <= kOpWideTl) {
     static size_t set[kMaxDevices] = {};
-    if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_msgs_kernel<NP, true>), tl, set)) return -1;
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_msgs_kernel<NP, true>), tl, set)) return rc;
     hipLaunchKernelGGL((op_wide_msgs_kernel<NP, true>), g, th, tl, stream, a);
   } else {
     hipLaunchKernelGGL((op_wide_msgs_kernel<NP, false>), g, th, 0, stream, a);
@@ -1215,7 +1215,7 @@ template <int NP, int TPW>
 int xi_launch_t(const OpWideArgs& a, hipStream_t stream) {
   const size_t lds = (size_t)op_xi_tile(a.T) * sizeof(unsigned);
   static size_t set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP, TPW>), lds, set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&op_wide_xi_kernel<NP, TPW>), lds, set)) return rc;
   const dim3 g((unsigned)((a.B + kOpWideSeqs - 1) / kOpWideSeqs)), th(kXwThreads);
   hipLaunchKernelGGL((op_wide_xi_kernel<NP, TPW>), g, th, lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

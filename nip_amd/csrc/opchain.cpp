@@ -31,11 +31,22 @@
 #include <vector>
 
 namespace nipamd {
+
+// a launcher's nonzero return: kLaunchRefused (the host refused the request)
+// -> NIPAMD_ERROR_UNSUPPORTED, anything else -> NIPAMD_ERROR_DEVICE
+static int op_launch_fail(int rc, const char* what, std::string& err) {
+  if (rc == kLaunchRefused) {
+    err = std::string(what) + ": the request does not fit the kernel (refused on the host)";
+    return NIPAMD_ERROR_UNSUPPORTED;
+  }
+  err = std::string(what) + ": kernel launch failed: " + hipGetErrorString(hipGetLastError());
+  return NIPAMD_ERROR_DEVICE;
+}
 namespace {
 
 constexpr long kOpMaxWork = 1L << 26;     // assignments x consistent combinations
 constexpr size_t kOpMaxTableBytes = 64L << 20;   // operators in HBM (LDS when <= 96 KB)
-constexpr size_t kOpMaxWideRow = 32L << 20;      // 17..64 states: an e_step slab row (16 sequences)
+constexpr size_t kOpMaxWideRow = 32L << 20;      // 17..64 states: an e_step slab row (kOpWideSeqs = 8 sequences)
 
 struct OpPlan {
   std::vector<int> ov;
@@ -400,10 +411,7 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
       w.post_bstride = jbs; w.post_tstride = jts; w.post_off = joff;
       w.ll = d_ll ? d_ll + b0 : nullptr;
       w.status = d_status ? d_status + b0 : nullptr;
-      if (op_wide_launch(w, (hipStream_t)stream)) {
-        err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError());
-        return NIPAMD_ERROR_DEVICE;
-      }
+      if (int rc = op_wide_launch(w, (hipStream_t)stream)) return op_launch_fail(rc, "op_wide_msgs_kernel", err);
     }
     if (K_out) *K_out = P->K;
     return 0;
@@ -434,8 +442,7 @@ int op_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
   a.ll = d_ll; a.status = d_status;
   if (K_out) *K_out = P->K;
   const int rc = op_fb_launch(a, (hipStream_t)stream);
-  if (rc == -2) { err = "operators do not fit the kernel's LDS"; return NIPAMD_ERROR_UNSUPPORTED; }
-  if (rc) { err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()); return NIPAMD_ERROR_DEVICE; }
+  if (rc) return op_launch_fail(rc, "op_fb_kernel", err);
   return 0;
 }
 
@@ -619,7 +626,7 @@ long op_estep_chunk(int K, int T) {
 
 // 17..64 states: op_wide_msgs_kernel in e_step mode stores every message and
 // scale exponent, op_wide_xi_kernel sums the xi weights per combination into
-// one slab row per 16 sequences, and the fixed-order tree reduces the rows --
+// one slab row per kOpWideSeqs = 8 sequences, and the fixed-order tree reduces the rows --
 // per launch a power-of-two chunk of sequences whose messages stay within
 // ~4 GB and slab rows within ~8 GB (a row holds (ncomb + 1) K^2 + K doubles:
 // 29.6 MB at 20 states and 9261 combinations, so 256 rows fill the chip).
@@ -681,10 +688,8 @@ int op_wide_estep(OpPlan* P, const int32_t* d_obs, int n_obs, int B, int T, doub
     w.estep = 1;
     w.sc = sc;
     w.slab = slab;
-    if (op_wide_launch(w, st) || op_wide_xi_launch(w, st)) {
-      err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError());
-      return NIPAMD_ERROR_DEVICE;
-    }
+    if (int rc = op_wide_launch(w, st)) return op_launch_fail(rc, "op_wide_msgs_kernel (e_step)", err);
+    if (int rc = op_wide_xi_launch(w, st)) return op_launch_fail(rc, "op_wide_xi_kernel", err);
     const long nr = (nb + kOpWideSeqs - 1) / kOpWideSeqs;
     if (nipamd_tree_sum(slab, nr, (int)R, work, nchunks == 1 ? out : cres + (size_t)c * R, st)) {
       err = "tree launch failed";
@@ -705,7 +710,9 @@ bool op_estep_supported(nipamd_model* mm, int n_obs, const int* obs_vars, int T,
   OpPlan* P = plan_for(mm, n_obs, obs_vars);
   if (!P->ok) { why = P->why; return false; }
   if (P->K > 16) {
-    // op_wide_msgs_kernel + op_wide_xi_kernel: one slab row per 16 sequences
+    // op_wide_msgs_kernel + op_wide_xi_kernel: one slab row per 8 sequences (kOpWideSeqs); every
+    // block zeroes and writes its row's whole (ncomb + 1) K^2 section, so the slab traffic per
+    // sequence is R / 8 doubles whatever the sequence touches (a cost, not a bound)
     if ((size_t)P->xrow * sizeof(double) > kOpMaxWideRow) {
       why = "too many evidence combinations for the wide e_step's slab rows";
       return false;
@@ -819,14 +826,13 @@ int op_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     a.P0 = P0;
     a.C = Cc;
     const int rc = op_fb_launch(a, st);
-    if (rc == -2) { err = "operators do not fit the kernel's LDS"; return NIPAMD_ERROR_UNSUPPORTED; }
-    if (rc) { err = std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()); return NIPAMD_ERROR_DEVICE; }
+    if (rc) return op_launch_fail(rc, "op_fb_kernel (e_step)", err);
     OpXiArgs x{};
     x.obs = a.obs; x.obs_bstride = a.obs_bstride; x.obs_tstride = a.obs_tstride; x.nobs = n_obs;
     for (int i = 0; i < n_obs; i++) { x.col[i] = i; x.card[i] = P->card[i]; x.cstride[i] = P->stride[i]; }
     x.B = nb; x.T = T; x.K = K; x.ncomb = P->ncomb;
     x.W = W; x.P0 = P0; x.C = Cc; x.slab = slab;
-    if (op_xi_launch(x, st)) { err = "xi launch failed"; return NIPAMD_ERROR_DEVICE; }
+    if (int rc = op_xi_launch(x, st)) return op_launch_fail(rc, "op_xi_kernel", err);
     const long nr = (nb + kOpXiSeqs - 1) / kOpXiSeqs;
     if (nipamd_tree_sum(slab, nr, R, work, nchunks == 1 ? out : cres + (size_t)c * R, stream)) {
       err = "tree launch failed";

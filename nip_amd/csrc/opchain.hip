@@ -473,7 +473,7 @@ int op_xi_launch(const OpXiArgs& a, hipStream_t stream) {
   const size_t slds = (op_xi_sort_lds(a.ncomb, a.T) + 15) & ~(size_t)15;
   if (slds <= 160 * 1024) {
     static size_t sort_set[kMaxDevices] = {};
-    if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_sort_kernel), slds, sort_set)) return -1;
+    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_sort_kernel), slds, sort_set)) return rc;
     const int blocks = (int)((a.B + kOpXiSeqs - 1) / kOpXiSeqs);
     hipLaunchKernelGGL(op_xi_sort_kernel, dim3(blocks), dim3(256), slds, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -481,7 +481,7 @@ int op_xi_launch(const OpXiArgs& a, hipStream_t stream) {
   if (!op_xi_fits(a.K, a.ncomb)) return -2;
   const size_t lds = ((size_t)op_xi_row(a.K, a.ncomb) * sizeof(double) + 15) & ~(size_t)15;
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_kernel), lds, lds_set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&op_xi_kernel), lds, lds_set)) return rc;
   const int blocks = (int)((a.B + kOpXiSeqs - 1) / kOpXiSeqs);
   hipLaunchKernelGGL(op_xi_kernel, dim3(blocks), dim3(256), lds, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -503,7 +503,7 @@ int op_fb_launch(const OpArgs& a, hipStream_t stream) {
   const size_t lds = (op_lds_bytes(a.K, a.ncomb, a.T, b.tlds != 0) + 15) & ~(size_t)15;
   if (lds > 160 * 1024 || a.K > 16 || a.ncomb > 65534) return -2;
   static size_t lds_set[kMaxDevices] = {};
-  if (ensure_dyn_lds(reinterpret_cast<const void*>(&op_fb_kernel), lds, lds_set)) return -1;
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&op_fb_kernel), lds, lds_set)) return rc;
   const int blocks = (int)((a.B + kOpSeqs - 1) / kOpSeqs);
   hipLaunchKernelGGL(op_fb_kernel, dim3(blocks), dim3(kOpThreads), lds, stream, b);
   g_last_kernel = "op_fb_kernel";

@@ -98,9 +98,11 @@ class GpuEStep:
         two scalars on the GPU): no pack kernels, no host round trip before the
         collective.  Returns (packed, partial size)."""
         import torch
-        from . import _ints, _obs3, estep_partial, estep_tail, lib
+        from . import NIPAMD_ERROR_UNSUPPORTED, NipError, _ints, _obs3, estep_partial, estep_tail, lib
         o = _obs3(obs, obs_vars)
         S = lib().nipamd_estep_partial_size_req(model._h, int(o.shape[2]), _ints(obs_vars), int(o.shape[1]))
+        if S < 0:                                 # no GPU e_step plan for this model / request
+            raise NipError(NIPAMD_ERROR_UNSUPPORTED, "model has no GPU e_step plan")
         buf = torch.empty((S + 2,), dtype=torch.float64, device=obs.device)
         _, ll, status = estep_partial(model, o, obs_vars, partial=buf[:S])
         estep_tail(ll, status, out=buf[S:])

@@ -131,7 +131,7 @@ def test_wide_op_estep_zero_mass_sequences():
 
 
 def test_wide_op_partial_shard_invariant():
-    """One slab row per 16 sequences, power-of-two chunks: four 64-sequence
+    """One slab row per 8 sequences (kOpWideSeqs), power-of-two chunks: four 64-sequence
     shards combine into the 256-sequence partial bit for bit."""
     m, ov, obs = demo1_20(24, 256, seed=2)
     o = torch.from_numpy(obs).cuda().contiguous()

@@ -171,6 +171,34 @@ def test_config3_full_size_properties_and_parity():
         assert abs(ll[b].item() - rl) <= 1e-11 * abs(rl)
 
 
+@pytest.mark.parametrize("T", [4096, 8192])
+def test_config3_long_sequences_analytic_normalisation(T):
+    """chain_mfma_wide_kernel<2>'s phase B normalises every
+    posterior with one mass c* taken at the partner's first phase-B step
+    (NIPAMD_MW_ANALYTIC); the rounding drift grows with |t - t*|.  At T = 4096
+    and 8192 (16x / 32x config 3's length) every row still sums to 1 within
+    1e-12 and every posterior and ll matches the textbook smoother (1e-12 /
+    1e-11), missing runs included."""
+    from textbook_util import chain_tables, smoother
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(32))
+    ov = [m.variable("A1"), m.variable("B1")]
+    q = [m.variable("C1")]
+    B = 48
+    obs_np = synth.observations(B, T, 32, seed=T + 1, n_obs=2)
+    obs_np[3, 500:900, :] = -1
+    obs_np[7, :, 1] = -1
+    obs = torch.from_numpy(obs_np).cuda()
+    post, ll, st = nip_amd.forward_backward_inference(m, obs, ov, q)
+    torch.cuda.synchronize()
+    assert not st.any().item()
+    s = post.sum(dim=2)
+    assert float((s - 1.0).abs().max()) <= 1e-12
+    A, pi, Es = chain_tables(m, m.variable("C0"), q[0], ov)
+    tp, tf, tl = smoother(A, pi, Es, [obs_np[:, :, 0], obs_np[:, :, 1]])
+    assert np.abs(post.cpu().numpy() - tp).max() <= 1e-12
+    assert np.all(np.abs(ll.cpu().numpy() - tl) <= 1e-11 * np.abs(tl))
+
+
 # 33..64 states: chain_row64_kernel (one filter wave per direction; chain_wide4_kernel, four per direction, one
 # barrier per step, sparse rescaling, partner waves for scratch/posterior/ll)
 @pytest.mark.parametrize("card,B,T", [(48, 3, 21), (40, 2, 2), (64, 2, 9), (33, 3, 1)])
