@@ -84,6 +84,13 @@ def kernel_bytes(kname: str, N: int, n_obs: int, posterior: bool):
         return (4 * n_obs + 2 * ck + 8 * N,
                 "obs %d + every 4th interface message as a checkpoint (%d written + %d read) + posterior %d"
                 % (4 * n_obs, ck, ck, 8 * N))
+    if kname.startswith("chain_estep_ck_kernel"):
+        # round 6: every 4th forward message (16 states) and its exponent to HBM, read back once
+        ck = (8 * 16 + 4) // 4
+        return (2 * 4 * n_obs + 2 * ck,
+                "obs %d (read by the forward and the backward pass) + every 4th forward message and its "
+                "exponent as a checkpoint (%d written + %d read); the recomputed messages and the counts "
+                "stay on chip" % (2 * 4 * n_obs, ck, ck))
     post = 8 * N if posterior else 0
     if kname.startswith("chain_mfma_wide_kernel") and posterior:
         # both filters read the observation codes from HBM (no LDS staging)

@@ -1836,6 +1836,13 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       HIP_OK(hipMalloc(&a.diag, (size_t)nblk * 24 * sizeof(unsigned long long)));
       HIP_OK(hipMemsetAsync(a.diag, 0, (size_t)nblk * 24 * sizeof(unsigned long long), st));
     }
+    unsigned long long* ckd = nullptr;               // chain_estep_ck_kernel's per-group stamps [group][5]
+    const long ngrp = (nb + 15) / 16;
+    if (ck && times && c == 0) {
+      HIP_OK(hipMalloc(&ckd, (size_t)ngrp * 5 * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(ckd, 0, (size_t)ngrp * 5 * sizeof(unsigned long long), st));
+      a.diag = ckd;
+    }
     unsigned long long* e16d = nullptr;              // chain_estep16_kernel's per-wave stamps [block][16][4]
     const int nblk8 = (nb + 7) / 8;                  // blocks of 8 or 16 sequences: room for either
     if (ek == 3 && times && c == 0) {
@@ -1851,6 +1858,26 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
       return launch_fail(lrc, ck ? "chain_estep_ck_kernel" : mfma ? "chain_fb_mfma_kernel (e_step)"
                               : ek == 3 ? "chain_estep16_kernel" : "chain_kernel<true>");
 #ifdef NIPAMD_DIAGNOSTICS
+    if (ckd) {
+      std::vector<unsigned long long> h((size_t)ngrp * 5);
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(h.data(), ckd, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      (void)hipFree(ckd);
+      a.diag = nullptr;
+      unsigned long long t0 = ~0ull, t1 = 0;
+      double fw = 0, bw = 0, wall = 0;
+      for (long k = 0; k < ngrp; k++) {
+        const unsigned long long* r = h.data() + k * 5;
+        t0 = std::min(t0, r[0]);
+        t1 = std::max(t1, r[1]);
+        fw += (double)r[2];
+        bw += (double)r[3];
+        wall += (double)(r[1] - r[0]);
+      }
+      std::fprintf(stderr, "[nipamd] estep_ck groups %ld, launch span %.1f us; per group: forward %.0f cycles, "
+                   "backward %.0f cycles, wall %.1f us\n", ngrp, (t1 - t0) / 100.0, fw / ngrp, bw / ngrp,
+                   wall / ngrp / 100.0);
+    }
     if (e16d) {
       std::vector<unsigned long long> h((size_t)nblk8 * 64);
       HIP_OK(hipStreamSynchronize(st));

@@ -67,13 +67,19 @@ constexpr int kCkXD = 256;                   // one transpose buffer: [16 sequen
 #ifndef NIPAMD_CK_SCR_NT
 #define NIPAMD_CK_SCR_NT 0                   // A/B builds: checkpoints stored / loaded nontemporal
 #endif
+#ifndef NIPAMD_CK_NCK
+#define NIPAMD_CK_NCK 1                      // checkpoints per four steps: 1 (t = 4c+3) or 2 (also t = 4c+1)
+#endif
+constexpr int NCK = NIPAMD_CK_NCK;
+static_assert(NCK == 1 || NCK == 2, "checkpoints per chunk");
 
 // per-wave LDS (doubles): four count tables [4][R][16], three transpose
 // buffers (alpha^_{t-1}, w_t, gamma_t), the chunk's packed codes [16] words
 __host__ __device__ inline int ck_wave_doubles(int R) { return 4 * R * 16 + 3 * kCkXD + 8; }
 __host__ __device__ inline int ck_et_doubles(int R) { return (R * kCkEt + 1) & ~1; }
-// checkpoints per group: alpha^_{4k+3} for k < nck, [nck][16][16] doubles, then [nck][16] int exponents
-__host__ __device__ inline int ck_count(int T) { return (T + 3) >> 2; }
+// checkpoint slots per group: chunk c's alpha^_{4c+1} (NCK = 2) and alpha^_{4c+3} at
+// c NCK + (0 | NCK - 1): [nck][16][16] doubles, then [nck][16] int exponents
+__host__ __device__ inline int ck_count(int T) { return NCK * ((T + 3) >> 2); }
 __host__ __device__ inline long ck_group_doubles(int T) { return (long)ck_count(T) * (256 + 8); }
 
 // transpose buffer [row][16]: the 16-byte piece p of row r at (p ^ (r & 7)):
@@ -111,6 +117,17 @@ __device__ __forceinline__ v4d mfma4(const v4d& a, const v4d& b, v4d d) {
 
 __device__ __forceinline__ unsigned byte_of(unsigned w, int k) { return (w >> (8 * k)) & 0xFFu; }
 
+#ifndef NIPAMD_CK_LDS_ADD
+#define NIPAMD_CK_LDS_ADD 1                  // A/B builds: 0 = read-add-write
+#endif
+__device__ __forceinline__ void count_add(double* cell, double v) {
+#if NIPAMD_CK_LDS_ADD
+  (void)__hip_atomic_fetch_add(cell, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+  *cell += v;
+#endif
+}
+
 // mantissa / exponent running product
 struct MProd {
   double m = 1.0;
@@ -123,7 +140,7 @@ struct MProd {
   }
 };
 
-template <int PR>
+template <int PR, bool VEC>
 __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int M = a.M, R = M + 2, T = a.T;
@@ -143,12 +160,16 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   const long grp = (long)blockIdx.x * kCkWaves + wave;
   const long b0 = grp * 16;
   if (b0 >= a.B) return;
+  // diagnostics builds (a.diag): per group the wall clock at entry and exit
+  // (s_memrealtime, 100 MHz), the forward and backward passes' shader cycles
+  // and the SIMD
+  const unsigned long long r_in = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+  const unsigned long long c_in = a.diag ? __builtin_readcyclecounter() : 0;
+  unsigned long long c_mid = 0;
   const int j = lane & 15, g = lane >> 4;
   const int sj = state_of(j & 3, j >> 2);
   const bool active = b0 + j < a.B;
   const int* orow = a.obs ? a.obs + (active ? (b0 + j) * a.obs_bstride : 0) + a.obs_col : nullptr;
-  const bool vec = a.obs && a.obs_tstride == 1 && (a.obs_bstride & 3) == 0 &&
-                   ((reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) && a.obs_col == 0;
   const int nck = ck_count(T);
   double* Sg = a.S + (size_t)grp * ck_group_doubles(T);                      // [nck][16][16]
   int* Xg = reinterpret_cast<int*>(Sg + (size_t)nck * 256);                   // [nck][16]
@@ -156,12 +177,16 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   // the four codes of chunk c (steps 4c..4c+3) of this lane's sequence, one
   // byte each: the state, M missing, M + 1 out of range; steps past T and
   // sequences past B read as missing
+  // (VEC: [B][T] int32 rows, T % 4 == 0, 16-byte aligned: one int4 load at a
+  // clamped step, the lanes past the batch or the steps past T select -1)
   auto codes_of = [&](int c) -> unsigned {
     int o[4];
     const int t0 = 4 * c;
-    if (vec && active && t0 >= 0 && t0 + 3 < T) {
-      const int4 v = *reinterpret_cast<const int4*>(orow + t0);
-      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    if (VEC) {
+      const int tc = t0 < 0 ? 0 : (t0 > T - 4 ? T - 4 : t0);
+      const int4 v = *reinterpret_cast<const int4*>(orow + tc);
+      const bool in = active && t0 >= 0 && t0 < T;
+      o[0] = in ? v.x : -1; o[1] = in ? v.y : -1; o[2] = in ? v.z : -1; o[3] = in ? v.w : -1;
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++)
@@ -188,6 +213,13 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   const v4d zero = {0.0, 0.0, 0.0, 0.0};
   const v4d prior = active ? load4(a.pi + 2 * g) : zero;
   const v4d srow = load4(Etg + M * kCkEt);                                    // s: the missing row
+
+  auto ck_store = [&](int slot, const v4d& p, int e) {
+    double* q = Sg + (size_t)slot * 256 + j * 16 + 2 * g;
+    store_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<v2d*>(q), v2d{p.x, p.y});
+    store_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<v2d*>(q + 8), v2d{p.z, p.w});
+    if (g == 0) Xg[slot * 16 + j] = e;
+  };
 
   // ---------------------------------------------------------------- forward
   v4d X = prior;                 // alpha^_{t-1}
@@ -222,18 +254,18 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
           const int sc = -__builtin_amdgcn_frexp_exp(z);     // frexp exponent of 0 is 0
           p = ldexp4(p, sc);
           Ef += sc;
-          double* q = Sg + (size_t)c * 256 + j * 16 + 2 * g;
-          store_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<v2d*>(q), v2d{p.x, p.y});
-          store_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<v2d*>(q + 8), v2d{p.z, p.w});
-          if (g == 0) Xg[c * 16 + j] = Ef;
+          ck_store(c * NCK + NCK - 1, p, Ef);
+        } else if (NCK == 2 && k == 1) {
+          ck_store(c * NCK, p, Ef);                         // at the chunk's exponent
         }
         X = p;
       }
     }
-    // the last, partial chunk (T % 4 steps): no checkpoint
+    // the last, partial chunk (T % 4 steps): its middle checkpoint only (NCK = 2)
     for (int t = nfull * 4; t < T; t++) {
       const v4d u = matvec(Af, X);
       const v4d p = u * evid(wa, t & 3);
+      if (NCK == 2 && (t & 3) == 1) ck_store(nfull * NCK, p, Ef);
       if (!PR) {
         const double z = chain_sum(p);
         m2.mul(z);
@@ -265,17 +297,21 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   // the checkpoints back from HBM by this wave: its own stores first
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (a.diag) c_mid = __builtin_readcyclecounter();
 
   // --------------------------------------------------------------- backward
-  // checkpoint k = alpha^_{4k+3} (exponent in Xg); k = -1: the prior, exponent 0
+  // checkpoint slot k (exponent in Xg); k < 0: the prior, exponent 0
+  // (branch-free: k < 0 loads slot 0 and selects the prior)
   auto ck_load = [&](int k, int& e) -> v4d {
-    if (k < 0) { e = 0; return prior; }
-    const double* q = Sg + (size_t)k * 256 + j * 16 + 2 * g;
+    const int kc = k < 0 ? 0 : k;
+    const double* q = Sg + (size_t)kc * 256 + j * 16 + 2 * g;
     const v2d u = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q));
     const v2d w = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q + 8));
-    e = Xg[k * 16 + j];
-    return v4d{u.x, u.y, w.x, w.y};
+    const int ex = Xg[kc * 16 + j];
+    e = k < 0 ? 0 : ex;
+    return k < 0 ? prior : v4d{u.x, u.y, w.x, w.y};
   };
+  auto below = [](int c) { return c * NCK - 1; };   // slot of alpha^_{4c-1}
   const int ctop = (T - 1) >> 2;
   v4d Bt;                                       // beta^_t
   Bt.x = (active && state_of(g, 0) < a.N) ? 1.0 : 0.0;
@@ -287,62 +323,66 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   const int tk = lane >> 4, ty = lane & 15;     // sequence-major lane: table tk, state ty
   double* Hk = H + tk * R * 16 + ty;
 
-  // chunk c's alpha^: V[0..2] recomputed from checkpoint c - 1 (exponent Es),
-  // V3 = checkpoint c (exponent E3; the top chunk's is the forward pass's X
-  // when T % 4 == 0, and unused otherwise)
+  // chunk c's alpha^: V[0..2] (recomputed from the checkpoint below it, or
+  // V[1] the middle checkpoint when NCK = 2; all at the exponent Es of the
+  // checkpoint below), V3 = alpha^_{4c+3} (exponent E3; the top chunk's is the
+  // forward pass's X when T % 4 == 0, unused otherwise).  The chunk's
+  // evidence is read from LDS where a step needs it; chunk c - 1's (for its
+  // recomputation, during chunk c) one chunk ahead.
   v4d V[3], Vn[3];
   int Es, E3;
   v4d S3;
-  unsigned wc, wn;                              // codes of chunk c, c - 1
-  v4d ec[4], en[4];                             // evidence of chunk c, c - 1
-  auto recompute = [&](const v4d& start, const v4d (&e)[4], v4d (&out)[3]) {
-    v4d x = start;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      x = matvec(Af, x) * e[k];
-      out[k] = x;
-    }
-  };
-  // prologue: chunk ctop's codes, evidence, checkpoints and recomputation
-  wc = codes_of(ctop);
-  wn = codes_of(ctop - 1);
-#pragma unroll
-  for (int k = 0; k < 4; k++) ec[k] = evid(wc, k);
-  v4d Sb = ck_load(ctop - 1, Es);               // checkpoint below chunk ctop
+  unsigned wc = codes_of(ctop), wn = codes_of(ctop - 1);   // codes of chunk c, c - 1
+  v4d Sb = ck_load(below(ctop), Es);            // alpha^_{4 ctop - 1}
+  int Esn = 0, Esx = 0;
+  v4d Sbn = ck_load(below(ctop - 1), Esn);      // the one below chunk ctop - 1
+  v4d Mbn = zero;                               // chunk ctop - 1's middle checkpoint (NCK = 2)
   S3 = ((T & 3) == 0) ? X : zero;
   E3 = Ef;
-  recompute(Sb, ec, V);
+  if (NCK == 1) {
+    v4d x = Sb;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { x = matvec(Af, x) * evid(wc, k); V[k] = x; }
+  } else {
+    const v4d mid = ck_load(ctop * NCK, Esx);
+    V[0] = matvec(Af, Sb) * evid(wc, 0);
+    V[1] = mid;
+    V[2] = matvec(Af, mid) * evid(wc, 2);
+    Mbn = ck_load((ctop - 1) * NCK, Esx);
+  }
 
   // one chunk: its steps t = 4c + k, k = kmax..0 (kmax = 3 but in a short top
-  // chunk), with chunk c - 1's recomputation issued one step per step
+  // chunk), with chunk c - 1's recomputation issued along the steps
   auto chunk = [&](int c, auto full) {
     constexpr bool FULL = decltype(full)::value;
     if (g == 0) CW[j] = wc;                      // this chunk's packed codes, for the sequence-major lanes
-    // chunk c - 1: its evidence, the checkpoint below it (c - 2; c - 1 itself is Sb)
-    v4d Sbn = prior;
-    int Esn = 0;
-    if (c > 0) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) en[k] = evid(wn, k);
-      Sbn = ck_load(c - 2, Esn);
-    }
-    const unsigned wnn = c > 1 ? codes_of(c - 2) : 0u;
+    // chunk c - 1's evidence (its recomputation runs during this chunk from
+    // Sbn / Mbn, loaded one chunk ago); the checkpoints chunk c - 2 needs are
+    // loaded now, a whole chunk before their use.  Branch-free: at c = 0 the
+    // recomputation of chunk -1 runs on missing codes and is never used.
+    v4d en0 = evid(wn, 0), en1 = NCK == 1 ? evid(wn, 1) : zero, en2 = evid(wn, 2);
+    int Esf = 0;
+    const v4d Sf = ck_load(below(c - 2), Esf);
+    const v4d Mf = NCK == 2 ? ck_load((c - 2) * NCK, Esx) : zero;
+    const unsigned wnn = codes_of(c - 2);
     const unsigned cq0 = CW[tk], cq1 = CW[4 + tk], cq2 = CW[8 + tk], cq3 = CW[12 + tk];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
     double rc = 0.0;
     int Estar = 0;
-    v4d x = Sbn;                                 // chunk c - 1's recomputation chain
+    v4d x = Sbn;                                 // chunk c - 1's recomputation chain (NCK = 1)
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
-      if (c > 0 && k < 3) {                      // one recomputed step per step: Vn[0], Vn[1], Vn[2]
-        x = matvec(Af, x) * en[2 - k];
+      if (NCK == 1 && k < 3) {                   // one recomputed step per step: Vn[0], Vn[1], Vn[2]
+        x = matvec(Af, x) * (k == 2 ? en0 : k == 1 ? en1 : en2);
         Vn[2 - k] = x;
       }
+      if (NCK == 2 && k == 2) Vn[0] = matvec(Af, Sbn) * en0;
+      if (NCK == 2 && k == 1) { Vn[2] = matvec(Af, Mbn) * en2; Vn[1] = Mbn; }
       if (!FULL && k > kmax) continue;           // the top chunk's steps past T - 1
       const v4d cur = k == 3 ? S3 : V[k];        // alpha^_t
       const v4d prv = k == 0 ? Sb : V[k - 1];    // alpha^_{t-1}
       const int efc = k == 3 ? E3 : Es, efp = Es;
-      const v4d Xb = ec[k] * Bt;                 // e_t o beta^_t: the xi weight and the backward input
+      const v4d Xb = evid(wc, k) * Bt;           // e_t o beta^_t: the xi weight and the backward input
       const v4d pr = cur * Bt;
       if (FULL ? k == 3 : k == kmax) {           // the chunk's exact mass: c* = c_t, E*
         rc = recip(chain_sum(pr));
@@ -356,11 +396,15 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
       Bt = matvec(Ab, Xb);                       // beta^_{t-1}, exponent Eb until the chunk's rescale
       const v4d aT = tp_read(XA, lane), wT = tp_read(XW, lane), gT = tp_read(XG, lane);
       Kd = mfma4(aT, wT, Kd);
-      // M1 counts: lane (tk, ty) adds gamma_t(ty) of sequences 4q + tk to table tk, row = its code
-      Hk[byte_of(cq0, k) * 16] += gT.x;
-      Hk[byte_of(cq1, k) * 16] += gT.y;
-      Hk[byte_of(cq2, k) * 16] += gT.z;
-      Hk[byte_of(cq3, k) * 16] += gT.w;
+      // M1 counts: lane (tk, ty) adds gamma_t(ty) of sequences 4q + tk to
+      // table tk, row = its code.  LDS adds without return (ds_add_f64): no
+      // two lanes of one instruction share a cell, and a wave's LDS operations
+      // execute in program order, so every cell sums its terms in a fixed
+      // order -- deterministic -- without the read-add-write chain's waits
+      count_add(Hk + byte_of(cq0, k) * 16, gT.x);
+      count_add(Hk + byte_of(cq1, k) * 16, gT.y);
+      count_add(Hk + byte_of(cq2, k) * 16, gT.z);
+      count_add(Hk + byte_of(cq3, k) * 16, gT.w);
     }
     // beta^ rescaled once per chunk (exact powers of two; the exponent carries the scale)
     {
@@ -373,10 +417,11 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
     E3 = Es;
     Sb = Sbn;
     Es = Esn;
+    Sbn = Sf;
+    Esn = Esf;
+    Mbn = Mf;
 #pragma unroll
     for (int k = 0; k < 3; k++) V[k] = Vn[k];
-#pragma unroll
-    for (int k = 0; k < 4; k++) ec[k] = en[k];
     wc = wn;
     wn = wnn;
   };
@@ -405,9 +450,25 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
     slab[kSlabH + R * 16 + i] = 0.0;
   }
   if (lane < 16) slab[chain_slab_p0(M) + lane] = p0s;
+  if (a.diag && lane == 0) {
+    unsigned long long* d = a.diag + (size_t)grp * 5;
+    d[0] = r_in;
+    d[1] = __builtin_amdgcn_s_memrealtime();
+    d[2] = c_mid - c_in;
+    d[3] = __builtin_readcyclecounter() - c_mid;
+    d[4] = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3;   // hwreg(HW_REG_HW_ID): SIMD
+  }
 }
 
 }  // namespace
+
+template <int PR, bool VEC>
+static int ck_launch(const ChainArgs& a, size_t lds, int blocks, hipStream_t stream) {
+  static size_t set[kMaxDevices] = {};
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_ck_kernel<PR, VEC>), lds, set)) return rc;
+  hipLaunchKernelGGL((chain_estep_ck_kernel<PR, VEC>), dim3(blocks), dim3(kCkThreads), lds, stream, a);
+  return 0;
+}
 
 size_t chain_estep_ck_lds_bytes(int M) {
   const int R = M + 2;
@@ -423,15 +484,12 @@ int chain_estep_ck_launch(const ChainArgs& a, hipStream_t stream) {
   if (a.N > 16 || a.ne != 1 || !a.counts || a.T < 1 || lds > 160 * 1024) return kLaunchRefused;
   const long groups = (a.B + 15) / 16;
   const int blocks = (int)((groups + kCkWaves - 1) / kCkWaves);
-  if (a.proper) {
-    static size_t set[kMaxDevices] = {};
-    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_ck_kernel<1>), lds, set)) return rc;
-    hipLaunchKernelGGL(chain_estep_ck_kernel<1>, dim3(blocks), dim3(kCkThreads), lds, stream, a);
-  } else {
-    static size_t set[kMaxDevices] = {};
-    if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_ck_kernel<0>), lds, set)) return rc;
-    hipLaunchKernelGGL(chain_estep_ck_kernel<0>, dim3(blocks), dim3(kCkThreads), lds, stream, a);
-  }
+  const bool vec = a.obs && a.obs_tstride == 1 && (a.obs_bstride & 3) == 0 && (a.T & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) && a.obs_col == 0;
+  int rc = 0;
+  if (a.proper) rc = vec ? ck_launch<1, true>(a, lds, blocks, stream) : ck_launch<1, false>(a, lds, blocks, stream);
+  else rc = vec ? ck_launch<0, true>(a, lds, blocks, stream) : ck_launch<0, false>(a, lds, blocks, stream);
+  if (rc) return rc;
   g_last_kernel = "chain_estep_ck_kernel";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

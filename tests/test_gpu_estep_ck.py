@@ -126,7 +126,8 @@ def test_ck_partials_are_shard_invariant():
         parts.append(p.clone())
     comb = tree_sum(torch.stack(parts))
     torch.cuda.synchronize()
-    assert torch.equal(comb, whole)
+    assert torch.equal(comb[:-3], whole[:-3])             # the body, bit for bit
+    assert comb[-3:].tolist() == [4.0, 0.0, 0.0] and whole[-3:].tolist() == [1.0, 0.0, 0.0]   # route tag counts
 
 
 def test_ck_batch_over_two_launches_matches_tree():
