@@ -313,12 +313,19 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   };
   auto below = [](int c) { return c * NCK - 1; };   // slot of alpha^_{4c-1}
   const int ctop = (T - 1) >> 2;
-  v4d Bt;                                       // beta^_t
-  Bt.x = (active && state_of(g, 0) < a.N) ? 1.0 : 0.0;
-  Bt.y = (active && state_of(g, 1) < a.N) ? 1.0 : 0.0;
-  Bt.z = (active && state_of(g, 2) < a.N) ? 1.0 : 0.0;
-  Bt.w = (active && state_of(g, 3) < a.N) ? 1.0 : 0.0;
-  int Eb = 0;
+  // beta~_t = beta_t 2^-Ef_t / Z: the backward message normalised against
+  // the forward one, sum_y alpha^_t beta~_t = 1 for every t -- gamma_t =
+  // alpha^_t o beta~_t and the xi weight w_t = e_t o beta~_t 2^(Ef_t - Ef_{t-1})
+  // need no per-step or per-chunk normaliser, and beta~_{t-1} = A w_t is the
+  // recursion itself (no rescaling: its size follows alpha^'s).  Start:
+  // beta~_{T-1} = 1 / z_T on the real states, z_T = sum_y alpha^_{T-1}
+  // (0 for a dead or absent sequence: everything it adds is then 0).
+  const double rz = recip(chain_sum(X));
+  v4d Bt;                                       // beta~_t
+  Bt.x = state_of(g, 0) < a.N ? rz : 0.0;
+  Bt.y = state_of(g, 1) < a.N ? rz : 0.0;
+  Bt.z = state_of(g, 2) < a.N ? rz : 0.0;
+  Bt.w = state_of(g, 3) < a.N ? rz : 0.0;
   v4d Kd = zero;                                // xi sums (D[i][y]: lane (i % 4) * 16 + y, register i / 4)
   const int tk = lane >> 4, ty = lane & 15;     // sequence-major lane: table tk, state ty
   double* Hk = H + tk * R * 16 + ty;
@@ -367,8 +374,6 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
     const unsigned wnn = codes_of(c - 2);
     const unsigned cq0 = CW[tk], cq1 = CW[4 + tk], cq2 = CW[8 + tk], cq3 = CW[12 + tk];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
-    double rc = 0.0;
-    int Estar = 0;
     v4d x = Sbn;                                 // chunk c - 1's recomputation chain (NCK = 1)
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
@@ -381,19 +386,14 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
       if (!FULL && k > kmax) continue;           // the top chunk's steps past T - 1
       const v4d cur = k == 3 ? S3 : V[k];        // alpha^_t
       const v4d prv = k == 0 ? Sb : V[k - 1];    // alpha^_{t-1}
-      const int efc = k == 3 ? E3 : Es, efp = Es;
-      const v4d Xb = evid(wc, k) * Bt;           // e_t o beta^_t: the xi weight and the backward input
-      const v4d pr = cur * Bt;
-      if (FULL ? k == 3 : k == kmax) {           // the chunk's exact mass: c* = c_t, E*
-        rc = recip(chain_sum(pr));
-        Estar = efc + Eb;
-      }
-      const double f = __builtin_ldexp(rc, Estar - efp - Eb);
-      const double gg = __builtin_ldexp(rc, Estar - efc - Eb);
+      // w_t = e_t o beta~_t, times 2^(Ef_t - Ef_{t-1}) at the chunk's top step
+      // (alpha^_{4c+3} carries the forward pass's rescale, the others Es)
+      v4d Xb = evid(wc, k) * Bt;
+      if (k == 3) Xb = ldexp4(Xb, E3 - Es);
       tp_write(XA, j, g, prv);
-      tp_write(XW, j, g, Xb * f);
-      tp_write(XG, j, g, pr * gg);
-      Bt = matvec(Ab, Xb);                       // beta^_{t-1}, exponent Eb until the chunk's rescale
+      tp_write(XW, j, g, Xb);
+      tp_write(XG, j, g, cur * Bt);              // gamma_t
+      Bt = matvec(Ab, Xb);                       // beta~_{t-1} = A w_t
       const v4d aT = tp_read(XA, lane), wT = tp_read(XW, lane), gT = tp_read(XG, lane);
       Kd = mfma4(aT, wT, Kd);
       // M1 counts: lane (tk, ty) adds gamma_t(ty) of sequences 4q + tk to
@@ -405,12 +405,6 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
       count_add(Hk + byte_of(cq1, k) * 16, gT.y);
       count_add(Hk + byte_of(cq2, k) * 16, gT.z);
       count_add(Hk + byte_of(cq3, k) * 16, gT.w);
-    }
-    // beta^ rescaled once per chunk (exact powers of two; the exponent carries the scale)
-    {
-      const int sb = -__builtin_amdgcn_frexp_exp(chain_sum(Bt));
-      Bt = ldexp4(Bt, sb);
-      Eb += sb;
     }
     // rotate: chunk c - 1 becomes current
     S3 = Sb;
