@@ -509,10 +509,10 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         extra["em"] = {"iterations_timed": steps, "ll_per_iteration": em_state["ll"][-steps:],
                        "exchange_ms_median": float(np.median(em_state["exchange_ms"][-steps:])),
                        "exchange_bytes_per_rank": 8 * (P + 2),
-                       "note": "kernel_ms is the whole iteration on the launch stream (e_step kernels over "
-                               "8 launches of 16384 sequences, exchange, finalize, host m_step); the "
-                               "exchange packs the e_step partial (%d doubles incl. its 3-slot route tag), "
-                               "the ll tree sum and the failure count" % P}
+                       "note": ("kernel_ms is the whole iteration on the launch stream (the e_step kernel "
+                                "(%s), the slab trees, exchange, finalize, host m_step); the exchange packs "
+                                "the e_step partial (%d doubles incl. its 3-slot route tag), the ll tree sum "
+                                "and the failure count" % (kname.split(" + ")[0], P))}
     elif name == "generate":
         bpu, bnote = 4 * model.num_vars, "the int32 draws written; the tables stay in cache"
         workload = "generate_data: HMM-shaped DBN, %d hidden x %d observed states, B=%d series/GPU x T=%d" % (

@@ -67,19 +67,13 @@ constexpr int kCkXD = 256;                   // one transpose buffer: [16 sequen
 #ifndef NIPAMD_CK_SCR_NT
 #define NIPAMD_CK_SCR_NT 0                   // A/B builds: checkpoints stored / loaded nontemporal
 #endif
-#ifndef NIPAMD_CK_NCK
-#define NIPAMD_CK_NCK 1                      // checkpoints per four steps: 1 (t = 4c+3) or 2 (also t = 4c+1)
-#endif
-constexpr int NCK = NIPAMD_CK_NCK;
-static_assert(NCK == 1 || NCK == 2, "checkpoints per chunk");
 
 // per-wave LDS (doubles): four count tables [4][R][16], three transpose
 // buffers (alpha^_{t-1}, w_t, gamma_t), the chunk's packed codes [16] words
 __host__ __device__ inline int ck_wave_doubles(int R) { return 4 * R * 16 + 3 * kCkXD + 8; }
 __host__ __device__ inline int ck_et_doubles(int R) { return (R * kCkEt + 1) & ~1; }
-// checkpoint slots per group: chunk c's alpha^_{4c+1} (NCK = 2) and alpha^_{4c+3} at
-// c NCK + (0 | NCK - 1): [nck][16][16] doubles, then [nck][16] int exponents
-__host__ __device__ inline int ck_count(int T) { return NCK * ((T + 3) >> 2); }
+// checkpoint slot c per group: alpha^_{4c+3}; [nck][16][16] doubles, then [nck][16] int exponents
+__host__ __device__ inline int ck_count(int T) { return (T + 3) >> 2; }
 __host__ __device__ inline long ck_group_doubles(int T) { return (long)ck_count(T) * (256 + 8); }
 
 // transpose buffer [row][16]: the 16-byte piece p of row r at (p ^ (r & 7)):
@@ -176,26 +170,34 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
 
   // the four codes of chunk c (steps 4c..4c+3) of this lane's sequence, one
   // byte each: the state, M missing, M + 1 out of range; steps past T and
-  // sequences past B read as missing
+  // sequences past B read as missing.  Loaded raw (codes_raw) and packed
+  // where they are used (codes_pack), a chunk later: nothing consumes a load
+  // in the chunk that issues it, so no wait for it lands there.
   // (VEC: [B][T] int32 rows, T % 4 == 0, 16-byte aligned: one int4 load at a
-  // clamped step, the lanes past the batch or the steps past T select -1)
-  auto codes_of = [&](int c) -> unsigned {
-    int o[4];
+  // clamped step)
+  auto codes_raw = [&](int c) -> int4 {
     const int t0 = 4 * c;
     if (VEC) {
       const int tc = t0 < 0 ? 0 : (t0 > T - 4 ? T - 4 : t0);
-      const int4 v = *reinterpret_cast<const int4*>(orow + tc);
-      const bool in = active && t0 >= 0 && t0 < T;
-      o[0] = in ? v.x : -1; o[1] = in ? v.y : -1; o[2] = in ? v.z : -1; o[3] = in ? v.w : -1;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        o[k] = (orow && active && t0 + k >= 0 && t0 + k < T) ? orow[(long)(t0 + k) * a.obs_tstride] : -1;
+      return *reinterpret_cast<const int4*>(orow + tc);
     }
+    int o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int t = t0 + k < 0 ? 0 : (t0 + k > T - 1 ? T - 1 : t0 + k);
+      o[k] = orow ? orow[(long)t * a.obs_tstride] : -1;
+    }
+    return int4{o[0], o[1], o[2], o[3]};
+  };
+  auto codes_pack = [&](const int4& v, int c) -> unsigned {
+    const int t0 = 4 * c;
+    const int o[4] = {v.x, v.y, v.z, v.w};
     unsigned w = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const int cd = o[k] < 0 ? M : (o[k] < M ? o[k] : M + 1);
+      const bool in = active && t0 + k >= 0 && t0 + k < T;
+      const int ok = in ? o[k] : -1;
+      const int cd = ok < 0 ? M : (ok < M ? ok : M + 1);
       w |= (unsigned)cd << (8 * k);
     }
     return w;
@@ -227,15 +229,17 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   MProd m2, m1;
   bool dead = false;
   {
-    unsigned wa = codes_of(0), wb = codes_of(1);
-    const int nfull = T >> 2;
-    for (int c = 0; c < nfull; c++) {
-      const unsigned w = wa;
-      wa = wb;
-      wb = codes_of(c + 2);
+    // one full chunk of four steps from the codes w (loaded two chunks ago);
+    // w is reloaded with chunk c + 2's.  Two chunks per loop iteration with
+    // fixed registers (wA, wB): a loaded register is never copied, so no wait
+    // on a load still in flight lands in the loop (a copy at the back edge
+    // would wait for the load issued in the same iteration)
+    auto fchunk = [&](int c, int4& wr) {
+      const unsigned w = codes_pack(wr, c);
       v4d e[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) e[k] = evid(w, k);
+      wr = codes_raw(c + 2);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const v4d u = matvec(Af, X);
@@ -254,18 +258,25 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
           const int sc = -__builtin_amdgcn_frexp_exp(z);     // frexp exponent of 0 is 0
           p = ldexp4(p, sc);
           Ef += sc;
-          ck_store(c * NCK + NCK - 1, p, Ef);
-        } else if (NCK == 2 && k == 1) {
-          ck_store(c * NCK, p, Ef);                         // at the chunk's exponent
+          ck_store(c, p, Ef);
         }
         X = p;
       }
+    };
+    int4 wA = codes_raw(0), wB = codes_raw(1);
+    const int nfull = T >> 2;
+    int c = 0;
+    for (; c + 2 <= nfull; c += 2) {
+      fchunk(c, wA);
+      fchunk(c + 1, wB);
     }
-    // the last, partial chunk (T % 4 steps): its middle checkpoint only (NCK = 2)
+    if (c < nfull) fchunk(c++, wA);
+    // the last, partial chunk (T % 4 steps): no checkpoint; its codes are in
+    // wA when nfull is even, wB when odd
+    const unsigned wl = codes_pack((nfull & 1) ? wB : wA, nfull);
     for (int t = nfull * 4; t < T; t++) {
       const v4d u = matvec(Af, X);
-      const v4d p = u * evid(wa, t & 3);
-      if (NCK == 2 && (t & 3) == 1) ck_store(nfull * NCK, p, Ef);
+      const v4d p = u * evid(wl, t & 3);
       if (!PR) {
         const double z = chain_sum(p);
         m2.mul(z);
@@ -300,18 +311,25 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   if (a.diag) c_mid = __builtin_readcyclecounter();
 
   // --------------------------------------------------------------- backward
-  // checkpoint slot k (exponent in Xg); k < 0: the prior, exponent 0
-  // (branch-free: k < 0 loads slot 0 and selects the prior)
-  auto ck_load = [&](int k, int& e) -> v4d {
+  // checkpoint slot k (exponent in Xg); k < 0: the prior, exponent 0.
+  // Loaded raw (slot 0 for k < 0) and selected where used, a chunk later.
+  struct CkRaw {
+    v2d lo, hi;
+    int e;
+  };
+  auto ck_raw = [&](int k) -> CkRaw {
     const int kc = k < 0 ? 0 : k;
     const double* q = Sg + (size_t)kc * 256 + j * 16 + 2 * g;
-    const v2d u = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q));
-    const v2d w = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q + 8));
-    const int ex = Xg[kc * 16 + j];
-    e = k < 0 ? 0 : ex;
-    return k < 0 ? prior : v4d{u.x, u.y, w.x, w.y};
+    CkRaw r;
+    r.lo = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q));
+    r.hi = load_pol<NIPAMD_CK_SCR_NT>(reinterpret_cast<const v2d*>(q + 8));
+    r.e = Xg[kc * 16 + j];
+    return r;
   };
-  auto below = [](int c) { return c * NCK - 1; };   // slot of alpha^_{4c-1}
+  auto ck_val = [&](const CkRaw& r, int k) -> v4d {
+    return k < 0 ? prior : v4d{r.lo.x, r.lo.y, r.hi.x, r.hi.y};
+  };
+  auto ck_exp = [&](const CkRaw& r, int k) -> int { return k < 0 ? 0 : r.e; };
   const int ctop = (T - 1) >> 2;
   // beta~_t = beta_t 2^-Ef_t / Z: the backward message normalised against
   // the forward one, sum_y alpha^_t beta~_t = 1 for every t -- gamma_t =
@@ -330,62 +348,66 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
   const int tk = lane >> 4, ty = lane & 15;     // sequence-major lane: table tk, state ty
   double* Hk = H + tk * R * 16 + ty;
 
-  // chunk c's alpha^: V[0..2] (recomputed from the checkpoint below it, or
-  // V[1] the middle checkpoint when NCK = 2; all at the exponent Es of the
-  // checkpoint below), V3 = alpha^_{4c+3} (exponent E3; the top chunk's is the
-  // forward pass's X when T % 4 == 0, unused otherwise).  The chunk's
-  // evidence is read from LDS where a step needs it; chunk c - 1's (for its
-  // recomputation, during chunk c) one chunk ahead.
-  v4d V[3], Vn[3];
-  int Es, E3;
-  v4d S3;
-  unsigned wc = codes_of(ctop), wn = codes_of(ctop - 1);   // codes of chunk c, c - 1
-  v4d Sb = ck_load(below(ctop), Es);            // alpha^_{4 ctop - 1}
-  int Esn = 0, Esx = 0;
-  v4d Sbn = ck_load(below(ctop - 1), Esn);      // the one below chunk ctop - 1
-  v4d Mbn = zero;                               // chunk ctop - 1's middle checkpoint (NCK = 2)
-  S3 = ((T & 3) == 0) ? X : zero;
-  E3 = Ef;
-  if (NCK == 1) {
-    v4d x = Sb;
+  // What chunk c needs, all at hand when it starts (loaded or recomputed
+  // during chunk c + 1): V[0..2] = alpha^_{4c..4c+2} (recomputed from the
+  // checkpoint below, exponent Es), S3 = alpha^_{4c+3} (checkpoint c, E3;
+  // the top chunk's is the forward pass's X when T % 4 == 0, unused
+  // otherwise), Sb = alpha^_{4c-1} (checkpoint c - 1 or the prior, Es), Sr =
+  // checkpoint c - 2 (chunk c - 1's recomputation starts from it), the codes
+  // of chunk c (wc) and of chunk c - 1 (wn).  Every load is consumed by the
+  // next chunk, and two states alternate (two chunks per loop iteration):
+  // no loaded register is ever copied, so no wait on an in-flight load lands
+  // in the loop.  Checkpoints c - 1 and c - 2 are read again from L2 rather
+  // than carried in registers across chunks.
+  struct CkState {
+    v4d V[3];
+    CkRaw S3, Sb, Sr;
+    int4 wc, wn;
+  };
+  auto load_state = [&](CkState& n, int c) {   // the loads chunk c consumes (issued during chunk c + 1)
+    n.S3 = ck_raw(c);
+    n.Sb = ck_raw(c - 1);
+    n.Sr = ck_raw(c - 2);
+    n.wc = codes_raw(c);
+    n.wn = codes_raw(c - 1);
+  };
+  CkState A, B;
+  load_state(A, ctop);
+  v4d topX = X;                                 // the top chunk's alpha^_{4 ctop + 3} when T % 4 == 0
+  {
+    const unsigned w = codes_pack(A.wc, ctop);
+    v4d x = ck_val(A.Sb, ctop - 1);
 #pragma unroll
-    for (int k = 0; k < 3; k++) { x = matvec(Af, x) * evid(wc, k); V[k] = x; }
-  } else {
-    const v4d mid = ck_load(ctop * NCK, Esx);
-    V[0] = matvec(Af, Sb) * evid(wc, 0);
-    V[1] = mid;
-    V[2] = matvec(Af, mid) * evid(wc, 2);
-    Mbn = ck_load((ctop - 1) * NCK, Esx);
+    for (int k = 0; k < 3; k++) { x = matvec(Af, x) * evid(w, k); A.V[k] = x; }
   }
 
   // one chunk: its steps t = 4c + k, k = kmax..0 (kmax = 3 but in a short top
-  // chunk), with chunk c - 1's recomputation issued along the steps
-  auto chunk = [&](int c, auto full) {
+  // chunk), chunk c - 1's recomputation issued one step per step, its loads
+  // into the other state
+  auto chunk = [&](int c, auto full, CkState& cs, CkState& ns) {
     constexpr bool FULL = decltype(full)::value;
+    // the values this chunk consumes, from the loads of chunk c + 1
+    const unsigned wc = codes_pack(cs.wc, c), wn = codes_pack(cs.wn, c - 1);
+    const bool top = c == ctop && (T & 3) == 0;
+    const v4d S3 = top ? topX : ck_val(cs.S3, c), Sb = ck_val(cs.Sb, c - 1), Sr = ck_val(cs.Sr, c - 2);
+    const int E3 = top ? Ef : ck_exp(cs.S3, c), Es = ck_exp(cs.Sb, c - 1);
     if (g == 0) CW[j] = wc;                      // this chunk's packed codes, for the sequence-major lanes
-    // chunk c - 1's evidence (its recomputation runs during this chunk from
-    // Sbn / Mbn, loaded one chunk ago); the checkpoints chunk c - 2 needs are
-    // loaded now, a whole chunk before their use.  Branch-free: at c = 0 the
-    // recomputation of chunk -1 runs on missing codes and is never used.
-    v4d en0 = evid(wn, 0), en1 = NCK == 1 ? evid(wn, 1) : zero, en2 = evid(wn, 2);
-    int Esf = 0;
-    const v4d Sf = ck_load(below(c - 2), Esf);
-    const v4d Mf = NCK == 2 ? ck_load((c - 2) * NCK, Esx) : zero;
-    const unsigned wnn = codes_of(c - 2);
+    // chunk c - 1's evidence (its recomputation); branch-free: at c = 0 the
+    // recomputation of chunk -1 runs on missing codes and is never used
+    const v4d en0 = evid(wn, 0), en1 = evid(wn, 1), en2 = evid(wn, 2);
+    load_state(ns, c - 1);
     const unsigned cq0 = CW[tk], cq1 = CW[4 + tk], cq2 = CW[8 + tk], cq3 = CW[12 + tk];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
-    v4d x = Sbn;                                 // chunk c - 1's recomputation chain (NCK = 1)
+    v4d x = Sr;                                  // chunk c - 1's recomputation chain
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
-      if (NCK == 1 && k < 3) {                   // one recomputed step per step: Vn[0], Vn[1], Vn[2]
+      if (k < 3) {                               // one recomputed step per step: ns.V[0], V[1], V[2]
         x = matvec(Af, x) * (k == 2 ? en0 : k == 1 ? en1 : en2);
-        Vn[2 - k] = x;
+        ns.V[2 - k] = x;
       }
-      if (NCK == 2 && k == 2) Vn[0] = matvec(Af, Sbn) * en0;
-      if (NCK == 2 && k == 1) { Vn[2] = matvec(Af, Mbn) * en2; Vn[1] = Mbn; }
       if (!FULL && k > kmax) continue;           // the top chunk's steps past T - 1
-      const v4d cur = k == 3 ? S3 : V[k];        // alpha^_t
-      const v4d prv = k == 0 ? Sb : V[k - 1];    // alpha^_{t-1}
+      const v4d cur = k == 3 ? S3 : cs.V[k];     // alpha^_t
+      const v4d prv = k == 0 ? Sb : cs.V[k - 1];      // alpha^_{t-1}
       // w_t = e_t o beta~_t, times 2^(Ef_t - Ef_{t-1}) at the chunk's top step
       // (alpha^_{4c+3} carries the forward pass's rescale, the others Es)
       v4d Xb = evid(wc, k) * Bt;
@@ -406,22 +428,18 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
       count_add(Hk + byte_of(cq2, k) * 16, gT.z);
       count_add(Hk + byte_of(cq3, k) * 16, gT.w);
     }
-    // rotate: chunk c - 1 becomes current
-    S3 = Sb;
-    E3 = Es;
-    Sb = Sbn;
-    Es = Esn;
-    Sbn = Sf;
-    Esn = Esf;
-    Mbn = Mf;
-#pragma unroll
-    for (int k = 0; k < 3; k++) V[k] = Vn[k];
-    wc = wn;
-    wn = wnn;
+    // keep the next chunk's unpacking of these loads out of this chunk: the
+    // scheduler would hoist it here and wait for loads issued a moment ago
+    __builtin_amdgcn_sched_barrier(0);
   };
-  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{});
-  else chunk(ctop, std::false_type{});
-  for (int c = ctop - 1; c >= 0; c--) chunk(c, std::true_type{});
+  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{}, A, B);
+  else chunk(ctop, std::false_type{}, A, B);
+  int c = ctop - 1;
+  for (; c >= 1; c -= 2) {
+    chunk(c, std::true_type{}, B, A);
+    chunk(c - 1, std::true_type{}, A, B);
+  }
+  if (c == 0) chunk(0, std::true_type{}, B, A);
 
   // P0 = gamma_{-1}: prior o beta^_{-1}, normalised exactly; summed over the
   // wave's sequences in a fixed order (transpose, in-lane, then lane quarters)

@@ -224,11 +224,12 @@ def test_partials_of_different_routes_are_refused():
     sequence; beyond it the wide chain e_step runs) and on the engine setting
     (the general engine): partials of the layouts have the same size, and
     combining them must fail in the finalize, not sum mismatched layouts
-    (ADVICE r02).  A peaked transition (1e-50 off the diagonal) keeps the
-    model off chain_estep_ck_kernel, whose LDS does not depend on T."""
+    (ADVICE r02).  Peaked tables (1e-50 / 1e-60 off the diagonal) fail the
+    host's rescaling bound and keep the model off chain_estep_ck_kernel, whose
+    LDS does not depend on T."""
     N = 4
     nodes = [("P0", N, "P1"), ("P1", N, None), ("M1", N, None)]
-    pots = [("M1", ["P1"], synth.cpt(5, N, N)), ("P1", ["P0"], _near_identity(N, 1e-50)),
+    pots = [("M1", ["P1"], _near_identity(N, 1e-60)), ("P1", ["P0"], _near_identity(N, 1e-50)),
             ("P0", [], np.full(N, 1.0 / N))]
     m = nip_amd.Model.from_spec(nodes, pots)
     ov = [m.variable("M1")]

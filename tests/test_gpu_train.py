@@ -56,6 +56,12 @@ def test_em_learn_ragged_series_vs_oracle():
     ov = [m.variable("M1")]
     rng = np.random.default_rng(3)
     series = [rng.integers(-1, 5, size=(T, 1)).astype(np.int32) for T in (5, 1, 17, 5, 33, 2, 9, 17)]
+    # every series observes its first step: a leading missing run meets the
+    # reference's BAD_LUCK verdict (prefix.cpp), which after an m_step flips
+    # with ulp-level differences of the learned tables (the
+    # em_util.check_em_curve tests cover it) -- not what this test is about
+    for s in series:
+        s[0, 0] = abs(int(s[0, 0]))
     init = rng.random(m.param_size())
     rc, curve = nip_amd.em_learn_series(m, series, ov, 1e-6, init=init, max_iterations=2)
     assert rc == 0 and len(curve) == 2
