@@ -442,7 +442,15 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         metric = "sequence-timesteps/s batched e_step (EM expected counts), 16-state DBN"
         kname += " + tree64 + finalize"
     elif name == "estep_config3":
-        if kname.startswith("chain_estep_mw_kernel"):
+        if kname.startswith("chain_estep_ckw_kernel"):
+            # round 6: every 4th forward message (32 states) and its exponent to HBM, read back once
+            ck = (8 * 32 + 4) // 4
+            bpu = 2 * 4 * len(ov) + 2 * ck
+            bnote = ("obs %d (read by the forward and the backward pass) + every 4th forward message and its "
+                     "exponent as a checkpoint (%d written + %d read); the recomputed messages and the three "
+                     "sums stay on chip" % (2 * 4 * len(ov), ck, ck))
+            kname += " + tree64 + map finalize"
+        elif kname.startswith("chain_estep_mw_kernel"):
             NP = 32
             bpu = 2 * 4 * len(ov) + 2 * 8 * NP + 8
             bnote = ("obs %d (read by both filters) + half of each direction's messages written to the scratch and "

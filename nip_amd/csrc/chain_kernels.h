@@ -323,6 +323,14 @@ int estep_mw_max_cols();
 size_t estep_mw_scratch_bytes(long B, int T);
 // -2: the request does not fit the kernel (N > 32, more than 64 count rows, LDS)
 int estep_mw_launch(const EMwArgs& a, hipStream_t stream);
+// checkpoint + recompute e_step at 17..32 states (estep_ckw.hip, round 6):
+// one or two observed columns, the same wide slab row per 16 sequences;
+// count_rows = sum over the observed columns of M_k + 2.  Needs the host's
+// underflow bound for rescaling every 4th step (engine.cpp ckw_sparse_ok);
+// proper: ll from the final forward mass.  kLaunchRefused when it does not fit.
+size_t chain_estep_ckw_lds_bytes(int tab_rows, int count_rows);
+size_t chain_estep_ckw_scratch_bytes(long B, int T);
+int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream);
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);

@@ -1547,6 +1547,34 @@ static int zero_tail(nipamd_model* mm, double* d_partial, int written, hipStream
   return 0;
 }
 
+// chain_estep_ckw_kernel rescales each recursion every 4th step: allowed when
+// no step can shrink a vector's largest entry by more than 1e-30 (the bound of
+// estep16_sparse_ok at several columns).  For every previous state x: the
+// largest over y of A[x][y] times the smallest evidence any code combination
+// gives y (per column the smallest of its rows, missing included; column 0
+// carries the unobserved children's row sums).
+static bool ckw_sparse_ok(const nipamd::ChainPlan& P, const Route& r, const bool (&seen)[4]) {
+  if (P.N > 64) return false;
+  std::vector<double> ev(P.N, 1.0);
+  for (int k = 0; k < (int)P.emits.size() && k < 4; k++)
+    if (!seen[k])
+      for (int y = 0; y < P.N; y++) ev[y] *= P.emits[k].s[y];
+  for (int i = 0; i < r.ncol; i++) {
+    const auto& E = P.emit(r.emit[i]);
+    for (int y = 0; y < P.N; y++) {
+      double lo = E.s[y];
+      for (int o = 0; o < E.M; o++) lo = std::min(lo, E.E[(size_t)o * 64 + y]);
+      ev[y] *= lo;
+    }
+  }
+  for (int x = 0; x < P.N; x++) {
+    double best = 0.0;
+    for (int y = 0; y < P.N; y++) best = std::max(best, P.A64[x * 64 + y] * ev[y]);
+    if (!(best >= 1e-30)) return false;
+  }
+  return true;
+}
+
 // The wide chain e_step (estep_wide.hip): the filters store every message of
 // a chunk of sequences, the statistics kernel writes one slab row per 16
 // sequences, and the fixed-order tree sums the rows (per chunk, then over
@@ -1582,9 +1610,19 @@ static int estep_mw_partial(nipamd_model* mm, const Route& r, const int32_t* d_o
     return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
   if (int rc = zero_tail(mm, d_partial, S, st)) return rc;
   if (B == 0) { HIP_OK(hipMemsetAsync(d_partial, 0, (size_t)S * sizeof(double), st)); return 0; }
+  // chain_estep_ckw_kernel (checkpoints + recomputation, round 6): the
+  // default where every step may rescale every 4th step (ckw_sparse_ok) and
+  // its LDS fits; NIPAMD_ESTEP_WIDE_KERNEL=mw in diagnostics builds runs
+  // chain_estep_mw_kernel instead
+  int crows = 0;
+  for (int i = 0; i < r.ncol; i++) crows += P.emit(r.emit[i]).M + 2;
+  const char* wk = nipamd::diag_env("NIPAMD_ESTEP_WIDE_KERNEL");
+  const bool ck = !(wk && std::string(wk) == "mw") && r.ncol >= 1 && r.ncol <= 2 &&
+                  nipamd::chain_estep_ckw_lds_bytes(rt->mtab_rows, crows) <= 160 * 1024 && ckw_sparse_ok(P, r, seen);
   // sequences per launch: a power of two (the chunk trees are subtrees of the
   // batch's tree), scratch within ~8 GB: config 3's 65,536 x 256 in one launch
-  const size_t per_seq = nipamd::estep_mw_scratch_bytes(32, T) / 32 + 1;
+  const size_t per_seq = ck ? nipamd::chain_estep_ckw_scratch_bytes(16, T) / 16 + 1
+                            : nipamd::estep_mw_scratch_bytes(32, T) / 32 + 1;
   const size_t cap = std::min<size_t>(65536, std::max<size_t>(32, ((size_t)8 << 30) / per_seq));
   long chunk = 32;
   while ((size_t)chunk * 2 <= cap) chunk *= 2;
@@ -1593,7 +1631,8 @@ static int estep_mw_partial(nipamd_model* mm, const Route& r, const int32_t* d_o
   const long srows = (chunk + 15) / 16;
   const long lvl = (srows + 63) / 64;
   const size_t work = ((size_t)srows + 2 * lvl + nchunks + 64) * S * sizeof(double);
-  if (int rc = ensure_scratch(mm, nipamd::estep_mw_scratch_bytes(chunk, T))) return rc;
+  if (int rc = ensure_scratch(mm, ck ? nipamd::chain_estep_ckw_scratch_bytes(chunk, T)
+                                     : nipamd::estep_mw_scratch_bytes(chunk, T))) return rc;
   if (int rc = ensure_work(mm, work)) return rc;
   DevState* d = dev_of(mm);
   double* slab = d->W;
@@ -1632,8 +1671,8 @@ static int estep_mw_partial(nipamd_model* mm, const Route& r, const int32_t* d_o
     a.B = nb;
     a.ll = d_ll ? d_ll + b0 : nullptr;
     a.status = d_status ? d_status + b0 : nullptr;
-    const int lrc = nipamd::estep_mw_launch(a, st);
-    if (lrc) return launch_fail(lrc, "chain_estep_mw_kernel");
+    const int lrc = ck ? nipamd::chain_estep_ckw_launch(a, chain_proper(P), st) : nipamd::estep_mw_launch(a, st);
+    if (lrc) return launch_fail(lrc, ck ? "chain_estep_ckw_kernel" : "chain_estep_mw_kernel");
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
     if (reduce_rows(slab, (nb + 15) / 16, S, tA, tB, out, st))
       return fail(NIPAMD_ERROR_DEVICE, "reduction launch failed");

@@ -27,13 +27,18 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CNT_RTOL = 1e-11
 LL_RTOL = 1e-12
 WIDE = "chain_msgs_kernel + chain_stats_kernel"
-FUSED = "chain_estep_mw_kernel"         # estep_mw.hip: 17..32 states, up to two observed children
+# 17..32 states, one or two observed children: estep_ckw.hip where the host's
+# rescaling bound holds (round 6), estep_mw.hip otherwise (and with none)
+FUSED = ("chain_estep_ckw_kernel", "chain_estep_mw_kernel")
 
 
 def expected_kernel(m, ov, N):
-    """The route the engine takes: the fused matrix-core e_step for 17..32
-    states with at most two observed children, the two-kernel one otherwise."""
-    return FUSED if 16 < N <= 32 and len(ov) <= 2 else WIDE
+    """The routes the engine may take: the fused matrix-core e_steps for
+    17..32 states with at most two observed children, the two-kernel one
+    otherwise."""
+    if not (16 < N <= 32 and len(ov) <= 2):
+        return (WIDE,)
+    return FUSED if ov else FUSED[1:]
 
 
 def close(a, b, rtol):
@@ -72,7 +77,7 @@ def test_wide_estep_vs_oracle_and_general_engine(name, spec, osyms, iface, B, T)
     else:
         obs = np.zeros((B, T, 0), np.int32)
     cnt, ll, st = gpu_estep(m, obs, ov)
-    assert nip_amd.last_kernel() == expected_kernel(m, ov, m.card(m.variable(iface))), nip_amd.last_kernel()
+    assert nip_amd.last_kernel() in expected_kernel(m, ov, m.card(m.variable(iface))), nip_amd.last_kernel()
     orc = PortOracle(m.desc())
     rc, rl, rb = orc.estep(obs, ov, np.ones(m.param_size()))
     assert np.array_equal(st != 0, rb != 0)
@@ -114,7 +119,7 @@ def test_wide_partial_is_shard_invariant_and_reproducible():
                                           axis=2)).cuda().contiguous()
     whole, _, _ = nip_amd.estep_partial(m, obs, ov)
     whole = whole.clone()
-    assert nip_amd.last_kernel() == FUSED
+    assert nip_amd.last_kernel() in FUSED
     again, _, _ = nip_amd.estep_partial(m, obs, ov)
     assert torch.equal(whole, again)
     parts = []
@@ -177,7 +182,7 @@ def test_em_learn_demo1_32_on_chain_kernels_matches_general_engine():
         rc = em_learn(m, torch.from_numpy(obs_np).cuda(), ov, 1e-6, curve,
                       init=synth.uniform01(5, m.param_size()) + 0.05, max_iterations=5)
         if engine == nip_amd.ENGINE_AUTO:
-            assert nip_amd.last_kernel() == FUSED
+            assert nip_amd.last_kernel() in FUSED
         curves.append((rc, curve))
     assert curves[0][0] == curves[1][0]
     assert len(curves[0][1]) == len(curves[1][1])
@@ -217,7 +222,7 @@ def test_config3_estep_full_size_sums_vs_textbook():
     obs = torch.from_numpy(obs_np).cuda()
     partial, ll, st = nip_amd.estep_partial(m, obs, ov)
     torch.cuda.synchronize()
-    assert nip_amd.last_kernel() == FUSED
+    assert nip_amd.last_kernel() in FUSED
     assert not bool(st.any())
     # the slab's children in the chain plan's order: by their {C1, child} clique
     c1 = m.variable("C1")
