@@ -47,8 +47,9 @@ constexpr int kMaxCol = 2;
 
 // per-wave LDS (doubles): the count table [rows][NP] (observed columns' rows,
 // then one dummy row for the unused half of a single-column add), three
-// transposes (alpha^_{t-1}, w_t, gamma_t), packed codes [2][16] words
-__host__ __device__ inline int ckw_wave_doubles(int rows) { return (rows + 1) * NP + 3 * kXD + 16; }
+// transposes (alpha^_{t-1}, w_t, gamma_t), the chunk's count-row offsets
+// [4 steps][2 halves][16 sequences] ints
+__host__ __device__ inline int ckw_wave_doubles(int rows) { return (rows + 1) * NP + 3 * kXD + 64; }
 __host__ __device__ inline int ckw_tab_doubles(int tab_rows) { return (tab_rows * NPS + 1) & ~1; }
 __host__ __device__ inline int ckw_count(int T) { return (T + 3) >> 2; }
 // checkpoints per group: [nck][16][32] doubles, then [nck][16] int exponents
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   double* XA = Hl + (crows + 1) * NP;
   double* XW = XA + kXD;
   double* XG = XW + kXD;
-  unsigned* CW = reinterpret_cast<unsigned*>(XG + kXD);                      // [NC][16]
+  int* AD = reinterpret_cast<int*>(XG + kXD);                                // [4][2][16]
 
   for (int i = tid; i < a.tab_rows * NP; i += kWThreads) tab[(i / NP) * NPS + i % NP] = a.tab[i];
   for (int i = lane; i < (crows + 1) * NP; i += 64) Hl[i] = 0.0;
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   const int j = lane & 15, g = lane >> 4;
   const int sj = state_of(j & 3, j >> 2);
   const bool active = b0 + j < a.B;
-  const int* orow = (a.obs && a.ncol > 0) ? a.obs + (active ? (b0 + j) * a.obs_bstride : 0) : nullptr;
+  const int* orow = a.obs + (active ? (b0 + j) * a.obs_bstride : 0);      // the launcher requires obs
   const int nck = ckw_count(T);
   double* Sg = a.S + (size_t)grp * ckw_group_doubles(T);                     // [nck][16][32]
   int* Xg = reinterpret_cast<int*>(Sg + (size_t)nck * 16 * NP);              // [nck][16]
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     for (int k = 0; k < 4; k++) {
       const int t = t0 + k < 0 ? 0 : (t0 + k > T - 1 ? T - 1 : t0 + k);
 #pragma unroll
-      for (int q = 0; q < NC; q++) r.v[q][k] = orow ? orow[(long)t * a.obs_tstride + a.col[q]] : -1;
+      for (int q = 0; q < NC; q++) r.v[q][k] = orow[(long)t * a.obs_tstride + a.col[q]];
     }
     return r;
   };
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
       unsigned x = 0;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const bool in = orow && active && t0 + k >= 0 && t0 + k < T;
+        const bool in = active && t0 + k >= 0 && t0 + k < T;
         const int o = in ? r.v[q][k] : -1;
         const int cd = o < 0 ? M : (o < M ? o : M + 1);
         x |= (unsigned)cd << (8 * k);
@@ -359,7 +360,6 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   // count adds: lane half h = lane >> 5 takes column h's row (a dummy row
   // past the table when the request has one column), state lane & 31
   const int ch = lane >> 5, cy = lane & 31;
-  const int hbase = (ch < NC ? cro[ch] : crows) * NP + cy;
   auto recomp = [&](v4d (&x)[NT], const v4d (&e)[NT]) {
     v4d u[NT];
     matvec2(Af, x, u);
@@ -399,10 +399,11 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     constexpr bool FULL = decltype(full)::value;
     const CkRaw L = ck_raw(c - 3);
     const Raw Lc = codes_raw(c - 2);
-    if (g == 0) {
+    // the count rows of step g, both halves, for sequence j (element offsets
+    // into the table; half 1 of a one-column request: the dummy row)
 #pragma unroll
-      for (int q = 0; q < NC; q++) CW[q * 16 + j] = wc[q];
-    }
+    for (int h = 0; h < 2; h++)
+      AD[(g * 2 + h) * 16 + j] = (h < NC ? cro[h] + (int)byte_of4(wc[h < NC ? h : 0], g) : crows) * NP;
     v4d x[NT] = {Cr[0], Cr[1]};                  // chunk c - 1's recomputation chain
     v4d nV[3][NT];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
@@ -439,13 +440,20 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
         for (int xt = 0; xt < NT; xt++)
 #pragma unroll
           for (int yt = 0; yt < NT; yt++) Kd[xt][yt] = mfma1(aT[xt][q], wT[yt][q], Kd[xt][yt]);
-      // count rows: one add per sequence (lanes 0-31 column 0's row, 32-63 column 1's)
+      // count rows: one add per sequence (lanes 0-31 column 0's row, 32-63
+      // column 1's); every operand read before the first add, so the adds
+      // (which the compiler must order against later LDS reads) cost one wait
+      {
+        const int4* ad = reinterpret_cast<const int4*>(AD + (k * 2 + ch) * 16);
+        const int4 o4[4] = {ad[0], ad[1], ad[2], ad[3]};
+        double gv[16];
 #pragma unroll
-      for (int s = 0; s < 16; s++) {
-        const double gv = XG[s * NPS + cy];
-        const unsigned wq = CW[(ch < NC ? ch : 0) * 16 + s];
-        const int row = ch < NC ? (int)byte_of4(wq, k) : 0;
-        (void)__hip_atomic_fetch_add(Hl + hbase + row * NP, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int s = 0; s < 16; s++) gv[s] = XG[s * NPS + cy];
+        const int off[16] = {o4[0].x, o4[0].y, o4[0].z, o4[0].w, o4[1].x, o4[1].y, o4[1].z, o4[1].w,
+                             o4[2].x, o4[2].y, o4[2].z, o4[2].w, o4[3].x, o4[3].y, o4[3].z, o4[3].w};
+#pragma unroll
+        for (int s = 0; s < 16; s++)
+          (void)__hip_atomic_fetch_add(Hl + cy + off[s], gv[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -539,7 +547,8 @@ size_t chain_estep_ckw_scratch_bytes(long B, int T) {
 }
 
 int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream) {
-  if (a.N < 1 || a.N > NP || a.ncol < 1 || a.ncol > kMaxCol || a.T < 1 || a.n_unobs > 4) return kLaunchRefused;
+  if (!a.obs || a.N < 1 || a.N > NP || a.ncol < 1 || a.ncol > kMaxCol || a.T < 1 || a.n_unobs > 4)
+    return kLaunchRefused;
   int crows = 0;
   for (int c = 0; c < a.ncol; c++) {
     if (a.M[c] < 1 || a.M[c] + 2 > 255 || a.tab_off[c] % NP != 0) return kLaunchRefused;
