@@ -61,12 +61,13 @@ N_CU = 256
 # kernel -> (cycles per filter step, sequences per block, blocks resident per CU)
 LATENCY_STEP = {
     # 4 chained v_mfma_f64_16x16x4 and the step's evidence multiply on the
-    # VALU between them (V4: the recursion's own dependency chain; the MFMAs
-    # alone, V2, take 328)
-    "chain_fb_ckpt_kernel": (464.0, 16, 1),
-    "chain_fb_ckpt_kernel<proj>": (464.0, 16, 1),
-    "chain_fb_mfma_kernel": (464.0, 16, 1),
-    "chain_mfma_wide_kernel<1>": (464.0, 32, 1),       # two groups of 16 per block, concurrently
+    # VALU between them (V4: the recursion's own dependency chain, 424 cycles
+    # in round 6's profiles/r06/gpu/r06a_mb_lat6.txt, 464 in round 3's build;
+    # the MFMAs alone, V2, take 328)
+    "chain_fb_ckpt_kernel": (424.0, 16, 1),
+    "chain_fb_ckpt_kernel<proj>": (424.0, 16, 1),
+    "chain_fb_mfma_kernel": (424.0, 16, 1),
+    "chain_mfma_wide_kernel<1>": (424.0, 32, 1),       # two groups of 16 per block, concurrently
     "chain_mfma_wide_kernel<2>": (1136.1, 32, 1),      # 2 x 8 chained MFMAs, interleaved (V3); two groups of 16
 }
 CLOCK_GHZ = 2.39                 # in-kernel clock under the chain loop (s_memtime / s_memrealtime, r03_mb_lat.txt)
@@ -92,6 +93,13 @@ def kernel_bytes(kname: str, N: int, n_obs: int, posterior: bool):
                 "exponent as a checkpoint (%d written + %d read); the recomputed messages and the counts "
                 "stay on chip" % (2 * 4 * n_obs, ck, ck))
     post = 8 * N if posterior else 0
+    if kname.startswith("chain_fb_ckw_kernel"):
+        # round 6: every 4th forward message (32 states) and its exponent to HBM, read back once
+        ck = (8 * 32 + 4) // 4
+        return (2 * 4 * n_obs + 2 * ck + post,
+                "obs %d (read by the forward and the backward pass) + every 4th forward message and its "
+                "exponent as a checkpoint (%d written + %d read) + posterior %d"
+                % (2 * 4 * n_obs, ck, ck, post))
     if kname.startswith("chain_mfma_wide_kernel") and posterior:
         # both filters read the observation codes from HBM (no LDS staging)
         return (8 * n_obs + 16 * N + post,
@@ -598,7 +606,15 @@ def run_workload(name, args, world, rank, dev, steps, warmup, min_warm_s=0.0):
         roof["latency"] = {"bound": "filter dependency chain", "cycles_per_step": cyc, "steps": T,
                            "block_rounds": rounds, "clock_ghz": CLOCK_GHZ, "floor_ms": floor_ms,
                            "frac": floor_ms / kern_ms,
-                           "source": "profiles/r03/r03x_mb_lat.txt (mb_lat.hip: V4 for the 16-state step, V3 for the 32-state step)"}
+                           "source": "profiles/r06/gpu/r06a_mb_lat6.txt (V4, the 16-state step) and "
+                                     "profiles/r03/r03x_mb_lat.txt (V3, the 32-state step)"}
+        if spb == 16:
+            # round 6: the other forms of the 16-state step
+            roof["latency"]["step_forms"] = {
+                "V4 chained (the kernels)": 424, "V5 4 K-slices + add tree": 468,
+                "V6 2 x 2-MFMA chains + add": 444, "V7 4 K-slices, evidence in the tree": 416,
+                "note": "no form is more than 2% shorter than the chained step, so the chained step's "
+                        "424 cycles set the ceiling (DESIGN.md 5)"}
     pr = pipe_roof(workload, kern_ms)
     if pr:
         roof["pipe"] = pr

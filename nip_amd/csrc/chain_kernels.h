@@ -317,6 +317,10 @@ struct EMwArgs {
   int n_unobs;
   int urow[4], uM[4];
   unsigned long long* diag;   // stamps builds: per group [4 waves][4] cycles, else null
+  // chain_fb_ckw_launch only: the interface posteriors [B][T] rows
+  double* post;
+  long post_bstride;
+  int post_tstride, post_off;
 };
 size_t estep_mw_lds_bytes(int tab_rows);
 int estep_mw_max_cols();
@@ -331,6 +335,10 @@ int estep_mw_launch(const EMwArgs& a, hipStream_t stream);
 size_t chain_estep_ckw_lds_bytes(int tab_rows, int count_rows);
 size_t chain_estep_ckw_scratch_bytes(long B, int T);
 int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream);
+// the same kernel's forward_backward_inference form (chain_fb_ckw_kernel):
+// the interface posteriors to post (normalised per step), ll, status (1 for
+// zero mass); scratch chain_estep_ckw_scratch_bytes; no slab
+int chain_fb_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream);
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);

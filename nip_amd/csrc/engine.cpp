@@ -807,6 +807,9 @@ static void phase_report(const unsigned long long* h, int nblk) {
 }
 #endif
 
+static bool chain_proper(const nipamd::ChainPlan& P);
+static bool ckw_sparse_ok(const nipamd::ChainPlan& P, const Route& r, const bool (&seen)[4]);
+
 // One launch of the chain kernel `kind` for route r: the interface
 // variable's marginals (smoothed, or filtered) into dst rows (dbs / dts /
 // doff), or only ll / status when dst is null.
@@ -819,6 +822,39 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
   if (kind == kMfmaWide) {
     // matrix-core interface chain: N <= 32, up to four observed children
     const int NT = P.N <= 16 ? 1 : 2;
+    // chain_fb_ckw_kernel (round 6): smoothing at 17..32 states with one or
+    // two observed columns where every recursion may rescale every 4th step
+    // (ckw_sparse_ok): checkpoints + recomputation, no message round trip;
+    // NIPAMD_FB_WIDE_KERNEL=mw in diagnostics builds keeps chain_mfma_wide_kernel
+    if (NT == 2 && !filt && dst && r.ncol >= 1 && r.ncol <= 2 && P.emits.size() <= 4) {
+      bool seen[4] = {false, false, false, false}, ok = true;
+      int crows = 0;
+      for (int i = 0; i < r.ncol; i++) {
+        const int k = r.emit[i];
+        if (k < 0 || k >= (int)P.emits.size() || seen[k]) ok = false;
+        else seen[k] = true;
+        if (ok) crows += P.emits[k].M + 2;
+      }
+      const char* wk = nipamd::diag_env("NIPAMD_FB_WIDE_KERNEL");
+      if (ok && !(wk && std::string(wk) == "mw") && ckw_sparse_ok(P, r, seen)) {
+        if (int rc = ensure_scratch(mm, nipamd::chain_estep_ckw_scratch_bytes(B, T))) return rc;
+        nipamd::EMwArgs a{};
+        a.obs = d_obs; a.obs_bstride = (long)T * ocols; a.obs_tstride = (int)ocols;
+        a.ncol = r.ncol;
+        for (int i = 0; i < 4; i++) {
+          a.col[i] = i < r.ncol ? r.col[i] : 0;
+          a.M[i] = i < r.ncol ? P.emit(r.emit[i]).M : 0;
+          a.tab_off[i] = rt->mtab_off[i];
+        }
+        a.tab_rows = rt->mtab_rows; a.tab = rt->mtab;
+        a.B = B; a.T = T; a.H = T / 2; a.N = P.N;
+        a.A = d->A64; a.pi = d->pi64; a.w = rt->wv; a.S = d->S;
+        a.ll = d_ll; a.status = d_status;
+        a.post = dst; a.post_bstride = dbs; a.post_tstride = dts; a.post_off = doff;
+        const int lrc = nipamd::chain_fb_ckw_launch(a, chain_proper(P), (hipStream_t)stream);
+        if (lrc != nipamd::kLaunchRefused) return lrc ? launch_fail(lrc, "chain_fb_ckw_kernel") : 0;
+      }
+    }
     if (int rc = ensure_scratch(mm, filt ? 64 * sizeof(double) : nipamd::chain_mfma_wide_scratch_bytes(NT, B, T)))
       return rc;
     nipamd::WideMfmaArgs w{};

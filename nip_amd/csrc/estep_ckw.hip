@@ -104,7 +104,10 @@ __device__ __forceinline__ void tp_read2(const double* buf, int lane, double (&r
     for (int q = 0; q < 4; q++) r[xt][q] = buf[(4 * q + k) * NPS + 16 * xt + y];
 }
 
-template <int PR, int NC>
+// POST: forward_backward_inference's smoothed interface posteriors instead of
+// the e_step's sums (the backward pass writes gamma_t, normalised exactly, and
+// keeps no transposes, count tables or xi accumulators)
+template <int PR, int NC, bool POST>
 __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int T = a.T;
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   int* AD = reinterpret_cast<int*>(XG + kXD);                                // [4][2][16]
 
   for (int i = tid; i < a.tab_rows * NP; i += kWThreads) tab[(i / NP) * NPS + i % NP] = a.tab[i];
-  for (int i = lane; i < (crows + 1) * NP; i += 64) Hl[i] = 0.0;
+  if constexpr (!POST)
+    for (int i = lane; i < (crows + 1) * NP; i += 64) Hl[i] = 0.0;
   __syncthreads();                                                           // the block's only barrier
 
   const long grp = (long)blockIdx.x * kWWaves + wave;
@@ -295,14 +299,14 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     if (active && g == 0) {
       const double ll = dead ? -DBL_MAX : log(zT) - (double)Ef * 0.69314718055994530942;
       if (a.ll) a.ll[b0 + j] = ll;
-      if (a.status) a.status[b0 + j] = dead ? 3u : 0u;
+      if (a.status) a.status[b0 + j] = dead ? (POST ? 1u : 3u) : 0u;
     }
   } else if (active && g == 0) {
     double ll = log(m2) - log(m1) + (double)(e2 - e1) * 0.69314718055994530942;
     const bool dd = dead || m2 == 0.0;
     if (dd) ll = -DBL_MAX;
     if (a.ll) a.ll[b0 + j] = ll;
-    if (a.status) a.status[b0 + j] = dd ? 3u : 0u;
+    if (a.status) a.status[b0 + j] = dd ? (POST ? 1u : 3u) : 0u;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -395,15 +399,42 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     }
   }
 
+  // gamma_t normalised exactly (the reference's per-step posteriors) to
+  // post[b][t]: 16-byte pieces where the rows are 32 wide and aligned
+  const bool pvec = POST && a.post_tstride == NP && (a.post_off & 1) == 0 && (a.post_bstride & 1) == 0 &&
+                    (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
+  auto post_store = [&](int t, const v4d (&G)[NT]) {
+    const double r = recip(seq_sum(G));
+    if (!active) return;
+    double* p = a.post + (size_t)(b0 + j) * a.post_bstride + (long)t * a.post_tstride + a.post_off;
+    if (pvec) {
+#pragma unroll
+      for (int q = 0; q < NT; q++) {
+        store_pol<NIPAMD_POST_NT>(reinterpret_cast<v2d*>(p + 16 * q + 2 * g), v2d{G[q].x * r, G[q].y * r});
+        store_pol<NIPAMD_POST_NT>(reinterpret_cast<v2d*>(p + 16 * q + 2 * g + 8), v2d{G[q].z * r, G[q].w * r});
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NT; q++) {
+        const double v[4] = {G[q].x * r, G[q].y * r, G[q].z * r, G[q].w * r};
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++)
+          if (16 * q + state_of(g, rr) < a.N) store_pol<NIPAMD_POST_NT>(p + 16 * q + state_of(g, rr), v[rr]);
+      }
+    }
+  };
+
   auto chunk = [&](int c, auto full) {
     constexpr bool FULL = decltype(full)::value;
     const CkRaw L = ck_raw(c - 3);
     const Raw Lc = codes_raw(c - 2);
     // the count rows of step g, both halves, for sequence j (element offsets
     // into the table; half 1 of a one-column request: the dummy row)
+    if constexpr (!POST) {
 #pragma unroll
-    for (int h = 0; h < 2; h++)
-      AD[(g * 2 + h) * 16 + j] = (h < NC ? cro[h] + (int)byte_of4(wc[h < NC ? h : 0], g) : crows) * NP;
+      for (int h = 0; h < 2; h++)
+        AD[(g * 2 + h) * 16 + j] = (h < NC ? cro[h] + (int)byte_of4(wc[h < NC ? h : 0], g) : crows) * NP;
+    }
     v4d x[NT] = {Cr[0], Cr[1]};                  // chunk c - 1's recomputation chain
     v4d nV[3][NT];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
@@ -426,6 +457,11 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
         Xb[q] = e[q] * Bt[q];
         if (k == 3) Xb[q] = ldexp4(Xb[q], E3 - Es);
         G[q] = cur[q] * Bt[q];
+      }
+      if constexpr (POST) {
+        matvec2(Ab, Xb, Bt);                     // beta~_{t-1} = A w_t
+        post_store(4 * c + k, G);
+        continue;
       }
       tp_write2(XA, j, g, prv);
       tp_write2(XW, j, g, Xb);
@@ -456,6 +492,19 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
           (void)__hip_atomic_fetch_add(Hl + cy + off[s], gv[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+#ifdef NIPAMD_CKW_SGB
+    if constexpr (FULL) {
+      // interleave: one MFMA, then LDS reads and VALU work that the matrix
+      // pipe's 64 cycles can absorb (176 MFMAs a chunk)
+#pragma unroll
+      for (int i = 0; i < 176; i++) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NIPAMD_CKW_SGB_R, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NIPAMD_CKW_SGB_V, 0);
+      }
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);
     // down one chunk
 #pragma unroll
@@ -481,6 +530,7 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   }
   if (c == 0) chunk(0, std::true_type{});
 
+  if constexpr (POST) return;
   // P0 = gamma_{-1}, normalised exactly, summed over the wave's sequences in
   // a fixed order (transpose, in-lane, then lane quarters)
   v4d p0[NT];
@@ -529,11 +579,12 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
 
 }  // namespace
 
-template <int PR, int NC>
+template <int PR, int NC, bool POST>
 static int ckw_launch(const EMwArgs& a, size_t lds, int blocks, hipStream_t stream) {
   static size_t set[kMaxDevices] = {};
-  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&chain_estep_ckw_kernel<PR, NC>), lds, set)) return rc;
-  hipLaunchKernelGGL((chain_estep_ckw_kernel<PR, NC>), dim3(blocks), dim3(kWThreads), lds, stream, a);
+  const void* k = reinterpret_cast<const void*>(&chain_estep_ckw_kernel<PR, NC, POST>);
+  if (int rc = ensure_dyn_lds(k, lds, set)) return rc;
+  hipLaunchKernelGGL((chain_estep_ckw_kernel<PR, NC, POST>), dim3(blocks), dim3(kWThreads), lds, stream, a);
   return 0;
 }
 
@@ -546,24 +597,35 @@ size_t chain_estep_ckw_scratch_bytes(long B, int T) {
   return (size_t)((B + 15) / 16) * (size_t)ckw_group_doubles(T) * sizeof(double);
 }
 
-int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream) {
+template <bool POST>
+static int ckw_dispatch(const EMwArgs& a, bool proper, hipStream_t stream) {
   if (!a.obs || a.N < 1 || a.N > NP || a.ncol < 1 || a.ncol > kMaxCol || a.T < 1 || a.n_unobs > 4)
     return kLaunchRefused;
+  if (POST && !a.post) return kLaunchRefused;
   int crows = 0;
   for (int c = 0; c < a.ncol; c++) {
     if (a.M[c] < 1 || a.M[c] + 2 > 255 || a.tab_off[c] % NP != 0) return kLaunchRefused;
     crows += a.M[c] + 2;
   }
-  const size_t lds = chain_estep_ckw_lds_bytes(a.tab_rows, crows);
+  const size_t lds = POST ? ((size_t)ckw_tab_doubles(a.tab_rows) * sizeof(double) + 15) & ~(size_t)15
+                          : chain_estep_ckw_lds_bytes(a.tab_rows, crows);
   if (lds > (size_t)kLdsPerCU) return kLaunchRefused;
   const long groups = (a.B + 15) / 16;
   const int blocks = (int)((groups + kWWaves - 1) / kWWaves);
   int rc = 0;
-  if (proper) rc = a.ncol == 1 ? ckw_launch<1, 1>(a, lds, blocks, stream) : ckw_launch<1, 2>(a, lds, blocks, stream);
-  else rc = a.ncol == 1 ? ckw_launch<0, 1>(a, lds, blocks, stream) : ckw_launch<0, 2>(a, lds, blocks, stream);
+  if (proper) rc = a.ncol == 1 ? ckw_launch<1, 1, POST>(a, lds, blocks, stream) : ckw_launch<1, 2, POST>(a, lds, blocks, stream);
+  else rc = a.ncol == 1 ? ckw_launch<0, 1, POST>(a, lds, blocks, stream) : ckw_launch<0, 2, POST>(a, lds, blocks, stream);
   if (rc) return rc;
-  g_last_kernel = "chain_estep_ckw_kernel";
+  g_last_kernel = POST ? "chain_fb_ckw_kernel" : "chain_estep_ckw_kernel";
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream) {
+  return ckw_dispatch<false>(a, proper, stream);
+}
+
+int chain_fb_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream) {
+  return ckw_dispatch<true>(a, proper, stream);
 }
 
 }  // namespace nipamd
