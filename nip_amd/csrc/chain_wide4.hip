@@ -658,6 +658,8 @@ void chain_wide4_kernel(WideArgs a) {
   const long b = blockIdx.x;
   const int T = a.T, Tr = chain_codes_row(T);
   L.Tr = Tr;
+  const unsigned long long k0 = a.diag ? __builtin_readcyclecounter() : 0;   // diagnostics: the block's entry
+  if (a.diag && tid == 0) a.diag[b * 16 + 11] = __builtin_amdgcn_s_memrealtime();
   double Ac[4][16];
   if (R64 && wave < 2) r64_load_A(a, wave == 0, lane, Ac);
   // stage the evidence tables and this sequence's codes
@@ -695,10 +697,15 @@ void chain_wide4_kernel(WideArgs a) {
         L.pcodes[k * 2 * L.PAB + i] = j < n ? codes[k * Tr + kW4G + t] : (uint8_t)a.M[k];
       }
     __syncthreads();
+    if (a.diag && tid == 0) a.diag[b * 16 + 9] = __builtin_readcyclecounter() - k0;   // staging
     if (wave == 0) r64_filter<true, NC>(a, L, lane, Ac, nAf, nAi, nBf, nBi);
     else if (wave == 1) r64_filter<false, NC>(a, L, lane, Ac, nAb, nAi, nBb, nBi);
     else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi, nAf, nBf);
     else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi, nAf, nBf);
+    if (a.diag && tid == 0) {
+      a.diag[b * 16 + 10] = __builtin_readcyclecounter() - k0;  // the block, entry to exit
+      a.diag[b * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    }
   } else {
     if (wave < kQ) w4_filter<true>(a, L, wave, lane, nAf, nAi, nBf, nBi);
     else if (wave < 2 * kQ) w4_filter<false>(a, L, wave - kQ, lane, nAb, nAi, nBb, nBi);

@@ -938,8 +938,15 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
       for (int b = 0; b < B; b++)
         for (int i = 0; i < 16; i++) m[i] += (double)h[(size_t)b * 16 + i] / B;
       std::fprintf(stderr, "[nipamd] wide4 cycles (total / wait / before / after barrier): fwd filter %.0f / %.0f / %.0f / %.0f  "
-                   "bwd filter %.0f / %.0f / %.0f / %.0f  partners %.0f %.0f\n", m[0], m[1], m[2], m[3], m[4], m[5], m[6],
-                   m[7], m[8], m[12]);
+                   "bwd filter %.0f / %.0f / %.0f / %.0f  partners %.0f %.0f  staging %.0f  block %.0f\n", m[0], m[1],
+                   m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[12], m[9], m[10]);
+      unsigned long long e0 = ~0ull, e1 = 0, x0 = ~0ull, x1 = 0;
+      for (int b = 0; b < B; b++) {
+        e0 = std::min(e0, h[(size_t)b * 16 + 11]); e1 = std::max(e1, h[(size_t)b * 16 + 11]);
+        x0 = std::min(x0, h[(size_t)b * 16 + 13]); x1 = std::max(x1, h[(size_t)b * 16 + 13]);
+      }
+      std::fprintf(stderr, "[nipamd] wide4 wall us: entries spread %.2f  first exit %.2f  last exit %.2f\n",
+                   (e1 - e0) / 100.0, (x0 - e0) / 100.0, (x1 - e0) / 100.0);
     }
 #endif
     return 0;

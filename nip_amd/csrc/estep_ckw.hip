@@ -235,6 +235,8 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     m = __builtin_ldexp(m, -k);
     e += k;
   };
+  v4d srow[NT];                                  // s_all on this lane's states (live in the forward pass only)
+  evid(wmiss, 0, srow);
   auto fstep = [&](const v4d (&e)[NT], bool rescale, int slot) {
     v4d u[NT];
     matvec2(Af, X, u);
@@ -245,9 +247,8 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     if (!PR) {
       z = seq_sum(p);
       v4d us[NT];
-      evid(wmiss, 0, us);
 #pragma unroll
-      for (int q = 0; q < NT; q++) us[q] = u[q] * us[q];
+      for (int q = 0; q < NT; q++) us[q] = u[q] * srow[q];
       m2 *= z;
       m1 *= seq_sum(us);
       renorm(m2, e2);
@@ -403,10 +404,11 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   // post[b][t]: 16-byte pieces where the rows are 32 wide and aligned
   const bool pvec = POST && a.post_tstride == NP && (a.post_off & 1) == 0 && (a.post_bstride & 1) == 0 &&
                     (reinterpret_cast<uintptr_t>(a.post) & 15) == 0;
+  double* const prow = POST ? a.post + (size_t)(active ? b0 + j : 0) * a.post_bstride + a.post_off : nullptr;
   auto post_store = [&](int t, const v4d (&G)[NT]) {
     const double r = recip(seq_sum(G));
     if (!active) return;
-    double* p = a.post + (size_t)(b0 + j) * a.post_bstride + (long)t * a.post_tstride + a.post_off;
+    double* p = prow + t * a.post_tstride;
     if (pvec) {
 #pragma unroll
       for (int q = 0; q < NT; q++) {
@@ -438,16 +440,8 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     v4d x[NT] = {Cr[0], Cr[1]};                  // chunk c - 1's recomputation chain
     v4d nV[3][NT];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
-#pragma unroll
-    for (int k = 3; k >= 0; k--) {
-      if (k < 3) {                               // chunk c - 1's recomputation, one step per step
-        v4d e[NT];
-        evid(wn, 2 - k, e);
-        recomp(x, e);
-#pragma unroll
-        for (int q = 0; q < NT; q++) nV[2 - k][q] = x[q];
-      }
-      if (!FULL && k > kmax) continue;
+    // backward step k of chunk c
+    auto bstep = [&](int k) {
       const v4d(&cur)[NT] = k == 3 ? C3 : V[k];
       const v4d(&prv)[NT] = k == 0 ? Cb : V[k - 1];
       v4d e[NT], Xb[NT], G[NT];
@@ -461,7 +455,7 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
       if constexpr (POST) {
         matvec2(Ab, Xb, Bt);                     // beta~_{t-1} = A w_t
         post_store(4 * c + k, G);
-        continue;
+        return;
       }
       tp_write2(XA, j, g, prv);
       tp_write2(XW, j, g, Xb);
@@ -479,32 +473,39 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
       // count rows: one add per sequence (lanes 0-31 column 0's row, 32-63
       // column 1's); every operand read before the first add, so the adds
       // (which the compiler must order against later LDS reads) cost one wait
-      {
-        const int4* ad = reinterpret_cast<const int4*>(AD + (k * 2 + ch) * 16);
-        const int4 o4[4] = {ad[0], ad[1], ad[2], ad[3]};
-        double gv[16];
+      const int4* ad = reinterpret_cast<const int4*>(AD + (k * 2 + ch) * 16);
+      const int4 o4[4] = {ad[0], ad[1], ad[2], ad[3]};
+      double gv[16];
 #pragma unroll
-        for (int s = 0; s < 16; s++) gv[s] = XG[s * NPS + cy];
-        const int off[16] = {o4[0].x, o4[0].y, o4[0].z, o4[0].w, o4[1].x, o4[1].y, o4[1].z, o4[1].w,
-                             o4[2].x, o4[2].y, o4[2].z, o4[2].w, o4[3].x, o4[3].y, o4[3].z, o4[3].w};
+      for (int s = 0; s < 16; s++) gv[s] = XG[s * NPS + cy];
+      const int off[16] = {o4[0].x, o4[0].y, o4[0].z, o4[0].w, o4[1].x, o4[1].y, o4[1].z, o4[1].w,
+                           o4[2].x, o4[2].y, o4[2].z, o4[2].w, o4[3].x, o4[3].y, o4[3].z, o4[3].w};
 #pragma unroll
-        for (int s = 0; s < 16; s++)
-          (void)__hip_atomic_fetch_add(Hl + cy + off[s], gv[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int s = 0; s < 16; s++)
+        (void)__hip_atomic_fetch_add(Hl + cy + off[s], gv[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+#if NIPAMD_CKW_RECOMP_FIRST
+      if (k < 3) {                               // chunk c - 1's recomputation, one step per step
+        v4d e[NT];
+        evid(wn, 2 - k, e);
+        recomp(x, e);
+#pragma unroll
+        for (int q = 0; q < NT; q++) nV[2 - k][q] = x[q];
       }
-    }
-#ifdef NIPAMD_CKW_SGB
-    if constexpr (FULL) {
-      // interleave: one MFMA, then LDS reads and VALU work that the matrix
-      // pipe's 64 cycles can absorb (176 MFMAs a chunk)
+      if (FULL || k <= kmax) bstep(k);
+#else
+      if (FULL || k <= kmax) bstep(k);
+      if (k < 3) {                               // chunk c - 1's recomputation, one step per step (after
+        v4d e[NT];                               // step k: V[k] is dead, nV[2 - k] may take its registers)
+        evid(wn, 2 - k, e);
+        recomp(x, e);
 #pragma unroll
-      for (int i = 0; i < 176; i++) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, NIPAMD_CKW_SGB_R, 0);
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NIPAMD_CKW_SGB_V, 0);
+        for (int q = 0; q < NT; q++) nV[2 - k][q] = x[q];
       }
-    }
 #endif
+    }
     __builtin_amdgcn_sched_barrier(0);
     // down one chunk
 #pragma unroll
