@@ -90,6 +90,7 @@ struct JtPlanDev {
   int pi_off, w_off;      // dp: prior of the previous interface (t = 0), m1 weights
   int ws_alpha, ws_beta, ws_out, ws_slab;   // workspace slots (ws_slab: e_step counts)
   int slab;               // e_step slab size (param_size), 0 otherwise
+  int n_ip, n_dp;         // pool sizes (ints, doubles): the kernels stage both in LDS when they fit
 };
 
 struct JtRun {
@@ -113,7 +114,17 @@ struct JtRun {
   int estep;              // status BAD_LUCK rules of e_step (nip.c:1827-1854)
   int chunk;              // posterior: time steps per unit
   int gunits;             // HBM workspace: slots per direction (<= kJtGlobalUnits; wsg holds 2 x gunits)
+  // round 6: the pools staged in LDS once per block, W waves per block
+  // sharing them (jt_stage_bytes; 0 / 1: the round-3 form, pools read from
+  // global memory, one wave per block)
+  int stage;
+  int waves;
 };
+
+// LDS bytes of the staged pools (ints, then doubles, 16-byte aligned)
+inline size_t jt_stage_bytes(const JtPlanDev& p) {
+  return (((size_t)p.n_ip * sizeof(int) + 15) & ~(size_t)15) + (size_t)p.n_dp * sizeof(double);
+}
 
 // launches (jtree.hip); L = lanes per sequence unit (16, 32 or 64)
 int jt_w_launch(const JtRun& r, double* w_out, int L, hipStream_t st);

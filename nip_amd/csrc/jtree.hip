@@ -22,7 +22,29 @@
 namespace nipamd {
 namespace {
 
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }   // a block is one wave
+// the units of a wave run the schedule in lock step and share nothing with
+// other waves: a wave-level fence orders their workspace traffic (a wave's
+// LDS operations execute in program order; the fence waits for its global
+// ones), no block barrier (round 6: several waves per block share the staged
+// pools, and units of one wave may skip an output at different steps)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// the plan's pools in LDS (once per block, before any unit starts; the
+// workspace units follow them), or read from global memory as uploaded
+__device__ __forceinline__ double* stage_pools(const JtRun& r, JtPlanDev& P, double* lds) {
+  if (!r.stage) return lds;
+  int* ip = reinterpret_cast<int*>(lds);
+  double* dp = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + (((size_t)P.n_ip * sizeof(int) + 15) & ~(size_t)15));
+  for (int i = threadIdx.x; i < P.n_ip; i += blockDim.x) ip[i] = P.ip[i];
+  for (int i = threadIdx.x; i < P.n_dp; i += blockDim.x) dp[i] = P.dp[i];
+  __syncthreads();
+  P.ip = ip;
+  P.dp = dp;
+  return dp + P.n_dp;
+}
 
 // sum over the L lanes of a unit (every lane receives the total)
 template <int L>
@@ -135,6 +157,10 @@ __device__ __forceinline__ double* unit_ws(const JtRun& r, double* lds, int u, i
   return r.wsg + (((long)blockIdx.y * gridDim.x + blockIdx.x) * U + u) * r.p.ws;
 }
 
+// units of the block: 64 / L per wave
+template <int L>
+__device__ __forceinline__ int block_units() { return (int)(blockDim.x / L); }
+
 // any evidence entered at this step (a step without any contributes exactly 0
 // to ll; DESIGN.md 6, the missing-value note)
 __device__ __forceinline__ bool row_has_evidence(const int32_t* orow, int nobs) {
@@ -145,13 +171,14 @@ __device__ __forceinline__ bool row_has_evidence(const int32_t* orow, int nobs) 
 // ---------------------------------------------------------------------------
 // filters: blockIdx.y = direction (0 forward, 1 backward) + dir_base
 template <int L, bool LDS>
-__global__ __launch_bounds__(64) void jt_filter_kernel(JtRun r, int dir_base) {
+__global__ __launch_bounds__(256) void jt_filter_kernel(JtRun r, int dir_base) {
   extern __shared__ double lds[];
-  constexpr int U = 64 / L;
+  const int U = block_units<L>();
   const int u = threadIdx.x / L, sub = threadIdx.x % L;
   const int dir = dir_base + (int)blockIdx.y;
-  const JtPlanDev& P = r.p;
-  double* ws = unit_ws<LDS>(r, lds, u, U);
+  JtPlanDev P = r.p;
+  double* const wsl = stage_pools(r, P, lds);
+  double* ws = unit_ws<LDS>(r, wsl, u, U);
   const int K = P.K;
   const JtVisit* V = reinterpret_cast<const JtVisit*>(P.ip + (dir == 0 ? P.fwd : P.bwd));
   const int* pres = P.ip + P.pres;
@@ -222,7 +249,7 @@ __global__ __launch_bounds__(64) void jt_filter_kernel(JtRun r, int dir_base) {
 template <int L, bool LDS>
 __global__ __launch_bounds__(64) void jt_w_kernel(JtRun r, double* w_out) {
   extern __shared__ double lds[];
-  constexpr int U = 64 / L;
+  constexpr int U = 64 / L;                 // one wave, pools from global memory (r.stage == 0)
   const int u = threadIdx.x / L, sub = threadIdx.x % L;
   const JtPlanDev& P = r.p;
   double* ws = unit_ws<LDS>(r, lds, u, U);
@@ -239,12 +266,13 @@ __global__ __launch_bounds__(64) void jt_w_kernel(JtRun r, double* w_out) {
 // ---------------------------------------------------------------------------
 // posterior sweep: unit = (sequence, chunk of r.chunk steps)
 template <int L, bool LDS>
-__global__ __launch_bounds__(64) void jt_post_kernel(JtRun r) {
+__global__ __launch_bounds__(256) void jt_post_kernel(JtRun r) {
   extern __shared__ double lds[];
-  constexpr int U = 64 / L;
+  const int U = block_units<L>();
   const int u = threadIdx.x / L, sub = threadIdx.x % L;
-  const JtPlanDev& P = r.p;
-  double* ws = unit_ws<LDS>(r, lds, u, U);
+  JtPlanDev P = r.p;
+  double* const wsl = stage_pools(r, P, lds);
+  double* ws = unit_ws<LDS>(r, wsl, u, U);
   const int K = P.K;
   const JtVisit* V = reinterpret_cast<const JtVisit*>(P.ip + P.post);
   const JtDown* Dn = reinterpret_cast<const JtDown*>(P.ip + P.down);
@@ -326,26 +354,37 @@ __global__ void jt_add_kernel(const double* __restrict__ src, double* __restrict
   if (i < n) dst[i] += src[i];
 }
 
+// the block: r.waves waves (1 unless the pools are staged), its LDS the
+// staged pools and, with LDS workspaces, every unit's workspace
+template <int L, bool LDS>
+static size_t block_lds(const JtRun& r, int U) {
+  return (r.stage ? jt_stage_bytes(r.p) : 0) + (LDS ? (size_t)U * r.p.ws * sizeof(double) : 0);
+}
+
 template <int L, bool LDS>
 int filter_launch(const JtRun& r, int dirs, hipStream_t st) {
-  constexpr int U = 64 / L;
+  const int W = r.stage ? r.waves : 1, U = W * (64 / L);
   long blocks = (r.B + U - 1) / U;
   if (!LDS && blocks > r.gunits / U) blocks = r.gunits / U;
-  const size_t shm = LDS ? (size_t)U * r.p.ws * sizeof(double) : 0;
+  const size_t shm = block_lds<L, LDS>(r, U);
+  static size_t set[kMaxDevices] = {};
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&jt_filter_kernel<L, LDS>), shm, set)) return rc;
   const int dir_base = dirs == 2 ? 0 : (dirs == 0 ? 0 : 1);   // dirs: 0 fwd only, 1 bwd only, 2 both
-  hipLaunchKernelGGL((jt_filter_kernel<L, LDS>), dim3((unsigned)blocks, dirs == 2 ? 2 : 1), dim3(64),
+  hipLaunchKernelGGL((jt_filter_kernel<L, LDS>), dim3((unsigned)blocks, dirs == 2 ? 2 : 1), dim3(64 * W),
                      shm, st, r, dir_base);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 template <int L, bool LDS>
 int post_launch(const JtRun& r, hipStream_t st) {
-  constexpr int U = 64 / L;
+  const int W = r.stage ? r.waves : 1, U = W * (64 / L);
   const long nch = (r.T + r.chunk - 1) / r.chunk;
   long blocks = (r.B * nch + U - 1) / U;
   if (!LDS && blocks > r.gunits / U) blocks = r.gunits / U;
-  const size_t shm = LDS ? (size_t)U * r.p.ws * sizeof(double) : 0;
-  hipLaunchKernelGGL((jt_post_kernel<L, LDS>), dim3((unsigned)blocks), dim3(64), shm, st, r);
+  const size_t shm = block_lds<L, LDS>(r, U);
+  static size_t set[kMaxDevices] = {};
+  if (int rc = ensure_dyn_lds(reinterpret_cast<const void*>(&jt_post_kernel<L, LDS>), shm, set)) return rc;
+  hipLaunchKernelGGL((jt_post_kernel<L, LDS>), dim3((unsigned)blocks), dim3(64 * W), shm, st, r);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

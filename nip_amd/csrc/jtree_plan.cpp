@@ -49,6 +49,7 @@ struct Plan {
   double* d_dp = nullptr;
   int slab = 0;
   int stride = 0;           // query row width
+  int stage = 0, waves = 1; // the pools staged in LDS, waves per block (jt_stage_bytes)
   std::vector<int> hI;      // host copies of the pools (until uploaded)
   std::vector<double> hD;
 };
@@ -396,6 +397,21 @@ static int build_plan(const nipamd_model* mm, int n_obs, const int* obs_vars, in
     if (l == 16 || l == 32 || l == 64) P.L = l;
   }
   P.lds = (size_t)(64 / P.L) * p.ws * sizeof(double) <= 64 * 1024;
+  // round 6: every block stages the pools (schedule, index maps, pre-images,
+  // base tables) in LDS once and runs up to four waves on them, instead of
+  // each unit reading them from L2 at every step; NIPAMD_JT_STAGE=0 in
+  // diagnostics builds keeps the round-3 form
+  p.n_ip = (int)I.size();
+  p.n_dp = (int)B.dp.size();
+  {
+    const size_t sb = jt_stage_bytes(p), wsb = P.lds ? (size_t)(64 / P.L) * p.ws * sizeof(double) : 0;
+    int W = 4;
+    while (W > 1 && sb + W * wsb > 160 * 1024) W /= 2;
+    P.stage = sb + W * wsb <= 160 * 1024 ? 1 : 0;
+    P.waves = P.stage ? W : 1;
+    if (const char* e = diag_env("NIPAMD_JT_STAGE"))
+      if (std::atoi(e) == 0) { P.stage = 0; P.waves = 1; }
+  }
   P.hI = std::move(I);
   P.hD = std::move(B.dp);
   return 0;
@@ -519,6 +535,8 @@ int jt_fb(nipamd_model* mm, const int32_t* d_obs, int n_obs, const int* obs_vars
     r.ll = d_ll ? d_ll + b0 : nullptr;
     r.status = d_status ? (unsigned*)d_status + b0 : nullptr;
     r.filter = filt ? 1 : 0;
+    r.stage = P->stage;
+    r.waves = P->waves;
     // posterior units: (sequence, chunk of steps), enough of them to fill the chip
     long nch = std::max<long>(1, std::min<long>(T, 16384 / std::max<long>(1, nb)));
     r.chunk = (int)((T + nch - 1) / nch);
@@ -595,6 +613,8 @@ int jt_estep_partial(nipamd_model* mm, const int32_t* d_obs, int n_obs, const in
     r.slabs = slab;
     r.estep = 1;
     r.chunk = tch;
+    r.stage = P->stage;
+    r.waves = P->waves;
     if (jt_filter_launch(r, P->L, P->lds, 2, st) || jt_post_launch(r, P->L, P->lds, st))
       return set_error(NIPAMD_ERROR_DEVICE, std::string("jtree e_step launch: ") + hipGetErrorString(hipGetLastError()));
     double* out = nchunks == 1 ? d_partial : cres + (size_t)c * S;
