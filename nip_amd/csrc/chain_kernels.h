@@ -338,7 +338,9 @@ int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream);
 // the same kernel's forward_backward_inference form (chain_fb_ckw_kernel):
 // the interface posteriors to post (normalised per step), ll, status (1 for
 // zero mass); scratch chain_estep_ckw_scratch_bytes; no slab
-int chain_fb_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream);
+// vl: the recomputed messages in LDS, two waves per SIMD (the default; false:
+// in registers, one wave per SIMD)
+int chain_fb_ckw_launch(const EMwArgs& a, bool proper, bool vl, hipStream_t stream);
 
 size_t chain_lds_bytes(int M, int T, bool estep);
 int chain_fb_launch(const ChainArgs& a, hipStream_t stream);

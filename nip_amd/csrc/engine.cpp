@@ -851,7 +851,12 @@ static int launch_cur(nipamd_model* mm, const Route& r, ReqTables* rt, int kind,
         a.A = d->A64; a.pi = d->pi64; a.w = rt->wv; a.S = d->S;
         a.ll = d_ll; a.status = d_status;
         a.post = dst; a.post_bstride = dbs; a.post_tstride = dts; a.post_off = doff;
-        const int lrc = nipamd::chain_fb_ckw_launch(a, chain_proper(P), (hipStream_t)stream);
+#ifndef NIPAMD_FB_CKW_VL
+#define NIPAMD_FB_CKW_VL 1          // A/B builds: 0 = the recomputed messages in registers, one wave per SIMD
+#endif
+        const char* vl = nipamd::diag_env("NIPAMD_FB_CKW_VL");
+        const bool use_vl = vl ? std::atoi(vl) != 0 : NIPAMD_FB_CKW_VL != 0;
+        const int lrc = nipamd::chain_fb_ckw_launch(a, chain_proper(P), use_vl, (hipStream_t)stream);
         if (lrc != nipamd::kLaunchRefused) return lrc ? launch_fail(lrc, "chain_fb_ckw_kernel") : 0;
       }
     }

@@ -79,6 +79,19 @@ __device__ __forceinline__ void matvec2(const double (&Aop)[NT][NT][4], const v4
   }
 }
 
+// matvec2 with the operands read from LDS ([qo][qi][r][lane] doubles, the
+// block's copy: every wave's lane l holds the same A entries)
+__device__ __forceinline__ void matvec2_lds(const double* Al, int lane, const v4d (&X)[NT], v4d (&d)[NT]) {
+  double Aop[NT][NT][4];
+#pragma unroll
+  for (int qo = 0; qo < NT; qo++)
+#pragma unroll
+    for (int qi = 0; qi < NT; qi++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) Aop[qo][qi][r] = Al[((qo * NT + qi) * 4 + r) * 64 + lane];
+  matvec2(Aop, X, d);
+}
+
 // sum of a sequence's 32 states (its two tiles in the sequence's 4 lanes)
 __device__ __forceinline__ double seq_sum(const v4d (&v)[NT]) {
   return sum_lanes16(sum_lanes32(((v[0].x + v[0].y) + (v[0].z + v[0].w)) + ((v[1].x + v[1].y) + (v[1].z + v[1].w))));
@@ -107,8 +120,13 @@ __device__ __forceinline__ void tp_read2(const double* buf, int lane, double (&r
 // POST: forward_backward_inference's smoothed interface posteriors instead of
 // the e_step's sums (the backward pass writes gamma_t, normalised exactly, and
 // keeps no transposes, count tables or xi accumulators)
-template <int PR, int NC, bool POST>
-__global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a) {
+// VL (POST only): the chunk's recomputed messages in LDS, not registers
+// ([3 slots][4 pieces][64 lanes] 16-byte pieces per wave, 12 KB): the wave
+// fits 256 registers and two of them share a SIMD (eight waves per block)
+template <int PR, int NC, bool POST, bool VL = false>
+__global__ __launch_bounds__(VL ? 512 : kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a) {
+  static_assert(POST || !VL, "messages in LDS: the posterior mode only");
+  constexpr int WV = VL ? 8 : kWWaves, WT = 64 * WV;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -121,19 +139,29 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     crows += c < a.ncol ? a.M[c] + 2 : 0;
   }
   double* tab = reinterpret_cast<double*>(smem);                               // [tab_rows][NPS]
-  double* wl = tab + ckw_tab_doubles(a.tab_rows) + (size_t)wave * ckw_wave_doubles(crows);
+  // VL: the block's copy of the forward operands (the backward pass's
+  // recomputation reads them from LDS: 32 registers fewer), then the waves'
+  double* const AfL = tab + ckw_tab_doubles(a.tab_rows);                    // VL: [2][2][4][64]
+  double* wl = AfL + (VL ? NT * NT * 4 * 64 : 0) + (size_t)wave * (VL ? 3 * 512 : ckw_wave_doubles(crows));
+  double* const Vl = wl;                                                     // VL: [3][4][64] v2d
   double* Hl = wl;                                                           // [crows + 1][NP]
   double* XA = Hl + (crows + 1) * NP;
   double* XW = XA + kXD;
   double* XG = XW + kXD;
   int* AD = reinterpret_cast<int*>(XG + kXD);                                // [4][2][16]
 
-  for (int i = tid; i < a.tab_rows * NP; i += kWThreads) tab[(i / NP) * NPS + i % NP] = a.tab[i];
+  for (int i = tid; i < a.tab_rows * NP; i += WT) tab[(i / NP) * NPS + i % NP] = a.tab[i];
+  if constexpr (VL)
+    for (int i = tid; i < NT * NT * 4 * 64; i += WT) {
+      const int l = i & 63, r = (i >> 6) & 3, qi = (i >> 8) & 1, qo = i >> 9;
+      const int gl = l >> 4, jl = l & 15;
+      AfL[i] = a.A[(16 * qi + state_of(gl, r)) * 64 + 16 * qo + state_of(jl & 3, jl >> 2)];
+    }
   if constexpr (!POST)
     for (int i = lane; i < (crows + 1) * NP; i += 64) Hl[i] = 0.0;
   __syncthreads();                                                           // the block's only barrier
 
-  const long grp = (long)blockIdx.x * kWWaves + wave;
+  const long grp = (long)blockIdx.x * WV + wave;
   const long b0 = grp * 16;
   if (b0 >= a.B) return;
   const int j = lane & 15, g = lane >> 4;
@@ -367,13 +395,28 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
   const int ch = lane >> 5, cy = lane & 31;
   auto recomp = [&](v4d (&x)[NT], const v4d (&e)[NT]) {
     v4d u[NT];
-    matvec2(Af, x, u);
+    if constexpr (VL) matvec2_lds(AfL, lane, x, u);
+    else matvec2(Af, x, u);
 #pragma unroll
     for (int q = 0; q < NT; q++) x[q] = u[q] * e[q];
   };
 
+  // VL: slot s of the wave's message buffer
+  auto vstore = [&](int sl, const v4d (&m)[NT]) {
+    v2d* v = reinterpret_cast<v2d*>(Vl + sl * 512) + lane;
+    v[0] = v2d{m[0].x, m[0].y};
+    v[64] = v2d{m[0].z, m[0].w};
+    v[128] = v2d{m[1].x, m[1].y};
+    v[192] = v2d{m[1].z, m[1].w};
+  };
+  auto vload = [&](int sl, v4d (&m)[NT]) {
+    const v2d* v = reinterpret_cast<const v2d*>(Vl + sl * 512) + lane;
+    const v2d p0 = v[0], p1 = v[64], p2 = v[128], p3 = v[192];
+    m[0] = v4d{p0.x, p0.y, p1.x, p1.y};
+    m[1] = v4d{p2.x, p2.y, p3.x, p3.y};
+  };
   // the top chunk's state
-  v4d C3[NT], Cb[NT], Cr[NT], V[3][NT];
+  v4d C3[NT], Cb[NT], Cr[NT], V[VL ? 1 : 3][NT];
   int E3, Es, Er;
   unsigned wc[NC], wn[NC];
   {
@@ -395,8 +438,10 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
       v4d e[NT];
       evid(wc, k, e);
       recomp(x, e);
+      if constexpr (VL) vstore(k, x);            // the top chunk: slot k (parity 0)
+      else
 #pragma unroll
-      for (int q = 0; q < NT; q++) V[k][q] = x[q];
+        for (int q = 0; q < NT; q++) V[k][q] = x[q];
     }
   }
 
@@ -426,8 +471,13 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     }
   };
 
-  auto chunk = [&](int c, auto full) {
+  // VL: chunk c's message k lives in slot k (parity 0) or 2 - k (parity 1);
+  // the recomputation writes chunk c - 1's message m where chunk c's message
+  // 2 - m was (read at step 2 - m, before the write)
+  auto chunk = [&](int c, auto full, auto parity) {
     constexpr bool FULL = decltype(full)::value;
+    constexpr int P = decltype(parity)::value;
+    auto sig = [](int pp, int k) { return pp ? 2 - k : k; };
     const CkRaw L = ck_raw(c - 3);
     const Raw Lc = codes_raw(c - 2);
     // the count rows of step g, both halves, for sequence j (element offsets
@@ -438,12 +488,17 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
         AD[(g * 2 + h) * 16 + j] = (h < NC ? cro[h] + (int)byte_of4(wc[h < NC ? h : 0], g) : crows) * NP;
     }
     v4d x[NT] = {Cr[0], Cr[1]};                  // chunk c - 1's recomputation chain
-    v4d nV[3][NT];
+    v4d nV[VL ? 1 : 3][NT];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
     // backward step k of chunk c
     auto bstep = [&](int k) {
-      const v4d(&cur)[NT] = k == 3 ? C3 : V[k];
-      const v4d(&prv)[NT] = k == 0 ? Cb : V[k - 1];
+      v4d curv[NT];
+      if constexpr (VL) {
+        if (k == 3) { curv[0] = C3[0]; curv[1] = C3[1]; }
+        else vload(sig(P, k), curv);
+      }
+      const v4d(&cur)[NT] = VL ? curv : (k == 3 ? C3 : V[k]);
+      const v4d(&prv)[NT] = k == 0 ? Cb : V[VL ? 0 : k - 1];
       v4d e[NT], Xb[NT], G[NT];
       evid(wc, k, e);
 #pragma unroll
@@ -501,8 +556,10 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
         v4d e[NT];                               // step k: V[k] is dead, nV[2 - k] may take its registers)
         evid(wn, 2 - k, e);
         recomp(x, e);
+        if constexpr (VL) vstore(sig(1 - P, 2 - k), x);
+        else
 #pragma unroll
-        for (int q = 0; q < NT; q++) nV[2 - k][q] = x[q];
+          for (int q = 0; q < NT; q++) nV[2 - k][q] = x[q];
       }
 #endif
     }
@@ -512,8 +569,9 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     for (int q = 0; q < NT; q++) {
       C3[q] = Cb[q];
       Cb[q] = Cr[q];
+      if constexpr (!VL)
 #pragma unroll
-      for (int k = 0; k < 3; k++) V[k][q] = nV[k][q];
+        for (int k = 0; k < 3; k++) V[k][q] = nV[k][q];
     }
     E3 = Es;
     Es = Er;
@@ -522,14 +580,16 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
     for (int q = 0; q < NC; q++) wc[q] = wn[q];
     codes_pack(Lc, c - 2, wn);
   };
-  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{});
-  else chunk(ctop, std::false_type{});
+  const std::integral_constant<int, 0> p0c{};
+  const std::integral_constant<int, 1> p1c{};
+  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{}, p0c);
+  else chunk(ctop, std::false_type{}, p0c);
   int c = ctop - 1;
   for (; c >= 1; c -= 2) {
-    chunk(c, std::true_type{});
-    chunk(c - 1, std::true_type{});
+    chunk(c, std::true_type{}, p1c);
+    chunk(c - 1, std::true_type{}, p0c);
   }
-  if (c == 0) chunk(0, std::true_type{});
+  if (c == 0) chunk(0, std::true_type{}, p1c);
 
   if constexpr (POST) return;
   // P0 = gamma_{-1}, normalised exactly, summed over the wave's sequences in
@@ -580,12 +640,15 @@ __global__ __launch_bounds__(kWThreads, 1) void chain_estep_ckw_kernel(EMwArgs a
 
 }  // namespace
 
-template <int PR, int NC, bool POST>
-static int ckw_launch(const EMwArgs& a, size_t lds, int blocks, hipStream_t stream) {
+template <int PR, int NC, bool POST, bool VL>
+static int ckw_launch(const EMwArgs& a, size_t lds, hipStream_t stream) {
   static size_t set[kMaxDevices] = {};
-  const void* k = reinterpret_cast<const void*>(&chain_estep_ckw_kernel<PR, NC, POST>);
+  const void* k = reinterpret_cast<const void*>(&chain_estep_ckw_kernel<PR, NC, POST, VL>);
   if (int rc = ensure_dyn_lds(k, lds, set)) return rc;
-  hipLaunchKernelGGL((chain_estep_ckw_kernel<PR, NC, POST>), dim3(blocks), dim3(kWThreads), lds, stream, a);
+  const int wv = VL ? 8 : kWWaves;
+  const long groups = (a.B + 15) / 16;
+  const int blocks = (int)((groups + wv - 1) / wv);
+  hipLaunchKernelGGL((chain_estep_ckw_kernel<PR, NC, POST, VL>), dim3(blocks), dim3(64 * wv), lds, stream, a);
   return 0;
 }
 
@@ -598,7 +661,7 @@ size_t chain_estep_ckw_scratch_bytes(long B, int T) {
   return (size_t)((B + 15) / 16) * (size_t)ckw_group_doubles(T) * sizeof(double);
 }
 
-template <bool POST>
+template <bool POST, bool VL>
 static int ckw_dispatch(const EMwArgs& a, bool proper, hipStream_t stream) {
   if (!a.obs || a.N < 1 || a.N > NP || a.ncol < 1 || a.ncol > kMaxCol || a.T < 1 || a.n_unobs > 4)
     return kLaunchRefused;
@@ -608,25 +671,24 @@ static int ckw_dispatch(const EMwArgs& a, bool proper, hipStream_t stream) {
     if (a.M[c] < 1 || a.M[c] + 2 > 255 || a.tab_off[c] % NP != 0) return kLaunchRefused;
     crows += a.M[c] + 2;
   }
-  const size_t lds = POST ? ((size_t)ckw_tab_doubles(a.tab_rows) * sizeof(double) + 15) & ~(size_t)15
+  const size_t tabb = (size_t)ckw_tab_doubles(a.tab_rows) * sizeof(double);
+  const size_t lds = POST ? ((tabb + (VL ? (size_t)(NT * NT * 4 * 64 + 8 * 3 * 512) * sizeof(double) : 0)) + 15) & ~(size_t)15
                           : chain_estep_ckw_lds_bytes(a.tab_rows, crows);
   if (lds > (size_t)kLdsPerCU) return kLaunchRefused;
-  const long groups = (a.B + 15) / 16;
-  const int blocks = (int)((groups + kWWaves - 1) / kWWaves);
   int rc = 0;
-  if (proper) rc = a.ncol == 1 ? ckw_launch<1, 1, POST>(a, lds, blocks, stream) : ckw_launch<1, 2, POST>(a, lds, blocks, stream);
-  else rc = a.ncol == 1 ? ckw_launch<0, 1, POST>(a, lds, blocks, stream) : ckw_launch<0, 2, POST>(a, lds, blocks, stream);
+  if (proper) rc = a.ncol == 1 ? ckw_launch<1, 1, POST, VL>(a, lds, stream) : ckw_launch<1, 2, POST, VL>(a, lds, stream);
+  else rc = a.ncol == 1 ? ckw_launch<0, 1, POST, VL>(a, lds, stream) : ckw_launch<0, 2, POST, VL>(a, lds, stream);
   if (rc) return rc;
   g_last_kernel = POST ? "chain_fb_ckw_kernel" : "chain_estep_ckw_kernel";
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int chain_estep_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream) {
-  return ckw_dispatch<false>(a, proper, stream);
+  return ckw_dispatch<false, false>(a, proper, stream);
 }
 
-int chain_fb_ckw_launch(const EMwArgs& a, bool proper, hipStream_t stream) {
-  return ckw_dispatch<true>(a, proper, stream);
+int chain_fb_ckw_launch(const EMwArgs& a, bool proper, bool vl, hipStream_t stream) {
+  return vl ? ckw_dispatch<true, true>(a, proper, stream) : ckw_dispatch<true, false>(a, proper, stream);
 }
 
 }  // namespace nipamd
