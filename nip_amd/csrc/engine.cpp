@@ -1845,7 +1845,9 @@ static int estep_partial_routes(nipamd_model* mm, const int32_t* d_obs, int n_ob
     // an operator-chain request on a partial too small for its section (the
     // capacity-free nipamd_estep_partial): say so in nipamd_last_kernel
     if (capacity >= 0 && op_estep_route(mm, n_obs, obs_vars, T, -1))
-      nipamd::g_last_kernel = "general engine (operator-chain request on a partial without room for its section)";
+      nipamd::g_last_kernel =
+          "jt_filter_kernel + jt_post_kernel (general engine: an operator-chain request on a partial without room "
+          "for its section)";
     if (nipamd::estep_tag_launch(d_partial + estep_body_size(mm), 0.0, 1.0, 0.0, (hipStream_t)stream))
       return fail(NIPAMD_ERROR_DEVICE, "tag launch failed");
     return zero_tail(mm, d_partial, nipamd::param_size(mm->m), (hipStream_t)stream);
