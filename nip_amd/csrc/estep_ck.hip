@@ -350,96 +350,99 @@ __global__ __launch_bounds__(kCkThreads, 2) void chain_estep_ck_kernel(ChainArgs
 
   // What chunk c needs, all at hand when it starts (loaded or recomputed
   // during chunk c + 1): V[0..2] = alpha^_{4c..4c+2} (recomputed from the
-  // checkpoint below, exponent Es), S3 = alpha^_{4c+3} (checkpoint c, E3;
+  // checkpoint below, exponent Es), C3 = alpha^_{4c+3} (checkpoint c, E3;
   // the top chunk's is the forward pass's X when T % 4 == 0, unused
-  // otherwise), Sb = alpha^_{4c-1} (checkpoint c - 1 or the prior, Es), Sr =
-  // checkpoint c - 2 (chunk c - 1's recomputation starts from it), the codes
-  // of chunk c (wc) and of chunk c - 1 (wn).  Every load is consumed by the
-  // next chunk, and two states alternate (two chunks per loop iteration):
-  // no loaded register is ever copied, so no wait on an in-flight load lands
-  // in the loop.  Checkpoints c - 1 and c - 2 are read again from L2 rather
-  // than carried in registers across chunks.
-  struct CkState {
-    v4d V[3];
-    CkRaw S3, Sb, Sr;
-    int4 wc, wn;
-  };
-  auto load_state = [&](CkState& n, int c) {   // the loads chunk c consumes (issued during chunk c + 1)
-    n.S3 = ck_raw(c);
-    n.Sb = ck_raw(c - 1);
-    n.Sr = ck_raw(c - 2);
-    n.wc = codes_raw(c);
-    n.wn = codes_raw(c - 1);
-  };
-  CkState A, B;
-  load_state(A, ctop);
-  v4d topX = X;                                 // the top chunk's alpha^_{4 ctop + 3} when T % 4 == 0
+  // otherwise), Cb = alpha^_{4c-1} (checkpoint c - 1 or the prior, Es), Cr =
+  // checkpoint c - 2 (chunk c - 1's recomputation starts from it), the packed
+  // codes of chunk c (wc) and of chunk c - 1 (wn).  A chunk passes C3, Cb, Cr
+  // and wn down and loads one checkpoint (c - 3) and the raw codes of chunk
+  // c - 2: issued at its start, converted at its end (round 6: the earlier
+  // form reloaded checkpoints c - 1 and c - 2 from L2 in every chunk, 0.95 GB
+  // of extra fetches per config-4 launch, profiles/pmc_traffic.json r06y).
+  v4d V[3], C3, Cb, Cr;
+  int E3, Es, Er;
+  unsigned wc, wn;
   {
-    const unsigned w = codes_pack(A.wc, ctop);
-    v4d x = ck_val(A.Sb, ctop - 1);
+    const CkRaw r3 = ck_raw(ctop), rb = ck_raw(ctop - 1), rr = ck_raw(ctop - 2);
+    const int4 c0 = codes_raw(ctop), c1 = codes_raw(ctop - 1);
+    const bool top = (T & 3) == 0;
+    C3 = top ? X : ck_val(r3, ctop);
+    E3 = top ? Ef : ck_exp(r3, ctop);
+    Cb = ck_val(rb, ctop - 1);
+    Es = ck_exp(rb, ctop - 1);
+    Cr = ck_val(rr, ctop - 2);
+    Er = ck_exp(rr, ctop - 2);
+    wc = codes_pack(c0, ctop);
+    wn = codes_pack(c1, ctop - 1);
+    v4d x = Cb;
 #pragma unroll
-    for (int k = 0; k < 3; k++) { x = matvec(Af, x) * evid(w, k); A.V[k] = x; }
+    for (int k = 0; k < 3; k++) { x = matvec(Af, x) * evid(wc, k); V[k] = x; }
   }
 
   // one chunk: its steps t = 4c + k, k = kmax..0 (kmax = 3 but in a short top
-  // chunk), chunk c - 1's recomputation issued one step per step, its loads
-  // into the other state
-  auto chunk = [&](int c, auto full, CkState& cs, CkState& ns) {
+  // chunk), chunk c - 1's recomputation one step after each step
+  auto chunk = [&](int c, auto full) {
     constexpr bool FULL = decltype(full)::value;
-    // the values this chunk consumes, from the loads of chunk c + 1
-    const unsigned wc = codes_pack(cs.wc, c), wn = codes_pack(cs.wn, c - 1);
-    const bool top = c == ctop && (T & 3) == 0;
-    const v4d S3 = top ? topX : ck_val(cs.S3, c), Sb = ck_val(cs.Sb, c - 1), Sr = ck_val(cs.Sr, c - 2);
-    const int E3 = top ? Ef : ck_exp(cs.S3, c), Es = ck_exp(cs.Sb, c - 1);
+    const CkRaw L = ck_raw(c - 3);
+    const int4 Lc = codes_raw(c - 2);
     if (g == 0) CW[j] = wc;                      // this chunk's packed codes, for the sequence-major lanes
-    // chunk c - 1's evidence (its recomputation); branch-free: at c = 0 the
-    // recomputation of chunk -1 runs on missing codes and is never used
-    const v4d en0 = evid(wn, 0), en1 = evid(wn, 1), en2 = evid(wn, 2);
-    load_state(ns, c - 1);
     const unsigned cq0 = CW[tk], cq1 = CW[4 + tk], cq2 = CW[8 + tk], cq3 = CW[12 + tk];
     const int kmax = FULL ? 3 : ((T - 1) & 3);
-    v4d x = Sr;                                  // chunk c - 1's recomputation chain
+    v4d x = Cr;                                  // chunk c - 1's recomputation chain
+    v4d nV[3];
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
-      if (k < 3) {                               // one recomputed step per step: ns.V[0], V[1], V[2]
-        x = matvec(Af, x) * (k == 2 ? en0 : k == 1 ? en1 : en2);
-        ns.V[2 - k] = x;
+      if (FULL || k <= kmax) {                   // (the top chunk's steps past T - 1 skipped)
+        const v4d cur = k == 3 ? C3 : V[k];      // alpha^_t
+        const v4d prv = k == 0 ? Cb : V[k - 1];  // alpha^_{t-1}
+        // w_t = e_t o beta~_t, times 2^(Ef_t - Ef_{t-1}) at the chunk's top step
+        // (alpha^_{4c+3} carries the forward pass's rescale, the others Es)
+        v4d Xb = evid(wc, k) * Bt;
+        if (k == 3) Xb = ldexp4(Xb, E3 - Es);
+        tp_write(XA, j, g, prv);
+        tp_write(XW, j, g, Xb);
+        tp_write(XG, j, g, cur * Bt);            // gamma_t
+        Bt = matvec(Ab, Xb);                     // beta~_{t-1} = A w_t
+        const v4d aT = tp_read(XA, lane), wT = tp_read(XW, lane), gT = tp_read(XG, lane);
+        Kd = mfma4(aT, wT, Kd);
+        // M1 counts: lane (tk, ty) adds gamma_t(ty) of sequences 4q + tk to
+        // table tk, row = its code.  LDS adds without return (ds_add_f64): no
+        // two lanes of one instruction share a cell, and a wave's LDS operations
+        // execute in program order, so every cell sums its terms in a fixed
+        // order -- deterministic -- without the read-add-write chain's waits
+        count_add(Hk + byte_of(cq0, k) * 16, gT.x);
+        count_add(Hk + byte_of(cq1, k) * 16, gT.y);
+        count_add(Hk + byte_of(cq2, k) * 16, gT.z);
+        count_add(Hk + byte_of(cq3, k) * 16, gT.w);
       }
-      if (!FULL && k > kmax) continue;           // the top chunk's steps past T - 1
-      const v4d cur = k == 3 ? S3 : cs.V[k];     // alpha^_t
-      const v4d prv = k == 0 ? Sb : cs.V[k - 1];      // alpha^_{t-1}
-      // w_t = e_t o beta~_t, times 2^(Ef_t - Ef_{t-1}) at the chunk's top step
-      // (alpha^_{4c+3} carries the forward pass's rescale, the others Es)
-      v4d Xb = evid(wc, k) * Bt;
-      if (k == 3) Xb = ldexp4(Xb, E3 - Es);
-      tp_write(XA, j, g, prv);
-      tp_write(XW, j, g, Xb);
-      tp_write(XG, j, g, cur * Bt);              // gamma_t
-      Bt = matvec(Ab, Xb);                       // beta~_{t-1} = A w_t
-      const v4d aT = tp_read(XA, lane), wT = tp_read(XW, lane), gT = tp_read(XG, lane);
-      Kd = mfma4(aT, wT, Kd);
-      // M1 counts: lane (tk, ty) adds gamma_t(ty) of sequences 4q + tk to
-      // table tk, row = its code.  LDS adds without return (ds_add_f64): no
-      // two lanes of one instruction share a cell, and a wave's LDS operations
-      // execute in program order, so every cell sums its terms in a fixed
-      // order -- deterministic -- without the read-add-write chain's waits
-      count_add(Hk + byte_of(cq0, k) * 16, gT.x);
-      count_add(Hk + byte_of(cq1, k) * 16, gT.y);
-      count_add(Hk + byte_of(cq2, k) * 16, gT.z);
-      count_add(Hk + byte_of(cq3, k) * 16, gT.w);
+      if (k < 3) {                               // chunk c - 1's recomputation (after step k: V[k] is dead);
+        x = matvec(Af, x) * evid(wn, 2 - k);     // at c = 0 it runs on missing codes and is never used
+        nV[2 - k] = x;
+      }
     }
     // keep the next chunk's unpacking of these loads out of this chunk: the
     // scheduler would hoist it here and wait for loads issued a moment ago
     __builtin_amdgcn_sched_barrier(0);
+    // down one chunk
+    C3 = Cb;
+    Cb = Cr;
+    E3 = Es;
+    Es = Er;
+    Cr = ck_val(L, c - 3);
+    Er = ck_exp(L, c - 3);
+#pragma unroll
+    for (int k = 0; k < 3; k++) V[k] = nV[k];
+    wc = wn;
+    wn = codes_pack(Lc, c - 2);
   };
-  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{}, A, B);
-  else chunk(ctop, std::false_type{}, A, B);
+  if (((T - 1) & 3) == 3) chunk(ctop, std::true_type{});
+  else chunk(ctop, std::false_type{});
   int c = ctop - 1;
   for (; c >= 1; c -= 2) {
-    chunk(c, std::true_type{}, B, A);
-    chunk(c - 1, std::true_type{}, A, B);
+    chunk(c, std::true_type{});
+    chunk(c - 1, std::true_type{});
   }
-  if (c == 0) chunk(0, std::true_type{}, B, A);
+  if (c == 0) chunk(0, std::true_type{});
 
   // P0 = gamma_{-1}: prior o beta^_{-1}, normalised exactly; summed over the
   // wave's sequences in a fixed order (transpose, in-lane, then lane quarters)
