@@ -188,3 +188,20 @@ def test_ckw_peaked_model_takes_the_mw_kernel():
     ok = rb == 0
     assert np.array_equal(st != 0, rb != 0)
     assert close(ll[ok], rl[ok], LL_RTOL)
+
+
+def test_ckw_batch_over_two_launches_matches_tree():
+    """B above one launch (65,536 sequences): the launch trees combine into
+    the batch tree exactly (power-of-two chunks)."""
+    m = nip_amd.Model.from_spec(*synth.demo1_spec(32, seed=4))
+    ov = [m.variable("A1"), m.variable("B1")]
+    B, T = 81920, 5
+    obs = torch.from_numpy(gappy(B, T, (32, 32), 17)).cuda().contiguous()
+    whole, _, _ = nip_amd.estep_partial(m, obs, ov)
+    whole = whole.clone()
+    assert nip_amd.last_kernel() == CKW
+    a, _, _ = nip_amd.estep_partial(m, obs[:65536].contiguous(), ov)
+    a = a.clone()
+    b, _, _ = nip_amd.estep_partial(m, obs[65536:].contiguous(), ov)
+    torch.cuda.synchronize()
+    assert torch.equal(tree_sum(torch.stack([a, b.clone()]))[:-3], whole[:-3])
