@@ -143,3 +143,20 @@ def test_fb_ckw_matches_the_mfma_wide_kernel():
     assert str(outs[0]["k"]) == FBCK and str(outs[1]["k"]).startswith("chain_mfma_wide_kernel")
     assert np.abs(outs[0]["p"] - outs[1]["p"]).max() <= 1e-12
     assert np.all(np.abs(outs[0]["l"] - outs[1]["l"]) <= 1e-11 * np.maximum(1.0, np.abs(outs[1]["l"])))
+
+
+def test_fb_ckw_several_queries_vs_oracle():
+    """The interface and two derived variables in one request: the interface
+    rows land inside wider posterior rows (the kernel's strided store path)."""
+    m = demo1(32, 13, False)
+    ov = [m.variable("A1"), m.variable("B1")]
+    obs = gappy(7, 22, (32, 32), 19)
+    check_vs_oracle(m, obs, ov, [m.variable("C1"), m.variable("A1"), m.variable("D1")], kernel="")
+
+
+def test_fb_ckw_interface_not_first_in_the_query():
+    """The interface variable after another one: its rows start at an offset."""
+    m = demo1(24, 5, True)
+    ov = [m.variable("B1")]
+    obs = gappy(5, 17, (24,), 23)
+    check_vs_oracle(m, obs, ov, [m.variable("D1"), m.variable("C1")], kernel="")
