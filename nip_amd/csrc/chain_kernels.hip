@@ -1042,21 +1042,28 @@ void estep_finalize_kernel(const double* __restrict__ R, ChainFinalize f, double
   }
 }
 
+// One wave per count (CSR row): lane l sums terms l, l + 64, ... of the row,
+// then a fixed butterfly -- a fixed order, independent of the launch.  (A
+// thread per row summed the long rows -- a hidden parent's count over a
+// whole xi block -- serially: 0.168 ms of config 3's e_step,
+// profiles/r06ao_timed_region.txt.)
 __global__ __launch_bounds__(256)
 void estep_map_finalize_kernel(const double* __restrict__ R, int n, const int* __restrict__ ptr,
                                const int* __restrict__ idx, const double* __restrict__ coef,
                                double* __restrict__ counts) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (p >= n) return;                          // wave-uniform
   double acc = 0.0;
-  for (int j = ptr[p]; j < ptr[p + 1]; j++) acc += coef[j] * R[idx[j]];
-  counts[p] += acc;
+  for (int j = ptr[p] + lane; j < ptr[p + 1]; j += 64) acc += coef[j] * R[idx[j]];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) counts[p] += acc;
 }
 
 int estep_map_finalize_launch(const double* R, int n, const int* ptr, const int* idx, const double* coef,
                               double* counts, hipStream_t stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(estep_map_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, R, n, ptr, idx,
+  hipLaunchKernelGGL(estep_map_finalize_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, R, n, ptr, idx,
                      coef, counts);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -22,7 +22,7 @@ import sys
 
 
 # bench labels (nipamd_last_kernel) whose kernel symbol differs
-ALIAS = {"chain_row64_kernel": "chain_wide4_kernel"}
+ALIAS = {"chain_row64_kernel": "chain_wide4_kernel", "chain_fb_ckw_kernel": "chain_estep_ckw_kernel"}
 
 
 def trace_rows(d):
