@@ -427,6 +427,12 @@ __device__ __forceinline__ void r64_load_A(const WideArgs& a, bool fwd, int y, d
     for (int j = 0; j < 16; j++) Ac[b][j] = fwd ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
 }
 
+// timing-only diagnostics builds (wrong results): the filters run their steps
+// without the chunk, phase and closing barriers and the partners do nothing,
+// so the stamps give the filter step's own cost in the kernel's code
+#ifndef NIPAMD_R64_SOLO
+#define NIPAMD_R64_SOLO 0
+#endif
 template <bool FWD, int NC>
 __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, int y, const double (&Ac)[4][16],
                                            int nA, int nAi, int nB, int nBi) {
@@ -520,16 +526,17 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
         for (int j = 0; j < 8; j++) tc[k][j] = tn[k][j];
       }
       const unsigned long long tb = dg ? __builtin_readcyclecounter() : 0;
-      block_barrier();                                  // the chunk to the partner
+      if (NIPAMD_R64_SOLO) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else block_barrier();                             // the chunk to the partner
       if (dg) twait += __builtin_readcyclecounter() - tb;
     }
   };
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
   phase(nA, nAi, 0);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  if (!NIPAMD_R64_SOLO) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
   phase(nB, nBi, 1);
-  block_barrier();                                      // the partners' ll hand-over
+  if (!NIPAMD_R64_SOLO) block_barrier();                // the partners' ll hand-over
   if (dg && y == 0) {
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 0] = __builtin_readcyclecounter() - c0;
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 1] = twait;
@@ -700,6 +707,7 @@ void chain_wide4_kernel(WideArgs a) {
     if (a.diag && tid == 0) a.diag[b * 16 + 9] = __builtin_readcyclecounter() - k0;   // staging
     if (wave == 0) r64_filter<true, NC>(a, L, lane, Ac, nAf, nAi, nBf, nBi);
     else if (wave == 1) r64_filter<false, NC>(a, L, lane, Ac, nAb, nAi, nBb, nBi);
+    else if (NIPAMD_R64_SOLO) return;
     else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi, nAf, nBf);
     else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi, nAf, nBf);
     if (a.diag && tid == 0) {
