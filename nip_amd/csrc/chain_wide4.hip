@@ -427,9 +427,10 @@ __device__ __forceinline__ void r64_load_A(const WideArgs& a, bool fwd, int y, d
     for (int j = 0; j < 16; j++) Ac[b][j] = fwd ? a.A[(16 * b + j) * 64 + y] : a.A[y * 64 + 16 * b + j];
 }
 
-// timing-only diagnostics builds (wrong results): the filters run their steps
-// without the chunk, phase and closing barriers and the partners do nothing,
-// so the stamps give the filter step's own cost in the kernel's code
+// timing-only diagnostics builds (wrong results): 1 -- the filters run their
+// steps without the chunk, phase and closing barriers and the partners do
+// nothing, so the stamps give the filter step's own cost in the kernel's
+// code; 2 -- every barrier kept, the partners doing nothing else
 #ifndef NIPAMD_R64_SOLO
 #define NIPAMD_R64_SOLO 0
 #endif
@@ -526,17 +527,17 @@ __device__ __forceinline__ void r64_filter(const WideArgs& a, const W4Lds& L, in
         for (int j = 0; j < 8; j++) tc[k][j] = tn[k][j];
       }
       const unsigned long long tb = dg ? __builtin_readcyclecounter() : 0;
-      if (NIPAMD_R64_SOLO) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (NIPAMD_R64_SOLO == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else block_barrier();                             // the chunk to the partner
       if (dg) twait += __builtin_readcyclecounter() - tb;
     }
   };
   // phase A: forward alpha_0..alpha_{H-1}; backward beta_{T-2}..beta_H
   phase(nA, nAi, 0);
-  if (!NIPAMD_R64_SOLO) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
+  if (NIPAMD_R64_SOLO != 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // phase barrier
   // phase B: forward alpha_H..alpha_{T-1}; backward beta_{H-1}..beta_0
   phase(nB, nBi, 1);
-  if (!NIPAMD_R64_SOLO) block_barrier();                // the partners' ll hand-over
+  if (NIPAMD_R64_SOLO != 1) block_barrier();            // the partners' ll hand-over
   if (dg && y == 0) {
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 0] = __builtin_readcyclecounter() - c0;
     a.diag[blockIdx.x * 16 + (FWD ? 0 : 4) + 1] = twait;
@@ -707,7 +708,14 @@ void chain_wide4_kernel(WideArgs a) {
     if (a.diag && tid == 0) a.diag[b * 16 + 9] = __builtin_readcyclecounter() - k0;   // staging
     if (wave == 0) r64_filter<true, NC>(a, L, lane, Ac, nAf, nAi, nBf, nBi);
     else if (wave == 1) r64_filter<false, NC>(a, L, lane, Ac, nAb, nAi, nBb, nBi);
-    else if (NIPAMD_R64_SOLO) return;
+    else if (NIPAMD_R64_SOLO == 1) return;
+    else if (NIPAMD_R64_SOLO == 2) {
+      // the partners' barriers only (the filters' chunk, phase and closing ones)
+      for (int c = 0; c < nAi; c += 8) block_barrier();
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      for (int c = 0; c < nBi; c += 8) block_barrier();
+      block_barrier();
+    }
     else if (wave == 2) r64_partner<true>(a, L, lane, b, nAf, nAi, nBf, nBi, nAf, nBf);
     else r64_partner<false>(a, L, lane, b, nAb, nAi, nBb, nBi, nAf, nBf);
     if (a.diag && tid == 0) {
