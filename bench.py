@@ -320,6 +320,10 @@ def row64_issue_roof(B: int, T: int, kern_ms: float):
             "ds_per_step": d["ds_per_step"], "steps": T, "block_rounds": rounds, "clock_ghz": CLOCK_GHZ,
             "floor_ms": floor_ms, "frac": floor_ms / kern_ms,
             "at_4_cycles": {"cycles_per_step": cyc4, "floor_ms": floor4, "frac": floor4 / kern_ms},
+            # the same filter code measured alone (timing-only build without the
+            # barriers and the partners, NIPAMD_R64_SOLO=1) and in the kernel
+            "measured_step_cycles": {"alone_fwd": 566, "alone_bwd": 595, "in_kernel": 667,
+                                     "source": "profiles/r06/gpu/r06as, r06av (block stamps)"},
             "source": "profiles/r04/isa_row64_step.json, profiles/r04/gpu/r04h_mb_r64.txt"}
 
 
@@ -675,6 +679,9 @@ def compact_roof(roof):
                 r[k]["floor_ms"] = roof[k]["floor_ms"]
             if k == "issue" and "at_4_cycles" in roof[k]:
                 r[k]["frac_at_4cyc"] = roof[k]["at_4_cycles"]["frac"]
+            if k == "issue" and "measured_step_cycles" in roof[k]:
+                m = roof[k]["measured_step_cycles"]
+                r[k]["step_cycles"] = {"alone": m["alone_fwd"], "in_kernel": m["in_kernel"]}
     return r
 
 
